@@ -1,0 +1,288 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see ref_rng.h header).
+// C entry points for ctypes (tests/, smoke(), bench.py cpu_baseline).  The
+// names are prefixed `oref_` so they can never be confused with the product
+// library's `os_` C-ABI.
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ref_games.h"
+#include "ref_mcts.h"
+#include "ref_rng.h"
+
+using namespace oref;
+
+namespace {
+thread_local std::string g_err;
+
+struct OGame {
+  std::unique_ptr<RGame> game;
+};
+
+std::unique_ptr<RState> Replay(const RGame& g, const int64_t* a, int64_t n) {
+  auto s = g.NewInitialState();
+  for (int64_t i = 0; i < n; ++i) s->ApplyAction(a[i]);
+  return s;
+}
+
+void JsonEscape(const std::string& in, std::string* out) {
+  for (char c : in) {
+    switch (c) {
+      case '"': *out += "\\\""; break;
+      case '\\': *out += "\\\\"; break;
+      case '\n': *out += "\\n"; break;
+      default: *out += c;
+    }
+  }
+}
+
+// Per-root search output, child-ordered (the tree's shuffled order).
+struct RootOut {
+  int32_t* child_action;
+  int32_t* child_n;
+  double* child_w;
+  int8_t* child_out;   // outcome for the child's player, 2 = unsolved
+  int32_t* nchild;
+  int32_t* root_n;
+  double* root_w;
+  int8_t* root_out;
+  int64_t* best_action;
+  int32_t* nodes;
+};
+
+void FillOut(const SearchNode& root, int max_children, int64_t r,
+             const SearchStats& st, const RootOut& o) {
+  int nc = static_cast<int>(root.children.size());
+  o.nchild[r] = nc;
+  for (int k = 0; k < nc && k < max_children; ++k) {
+    const SearchNode& c = root.children[k];
+    o.child_action[r * max_children + k] = static_cast<int32_t>(c.action);
+    o.child_n[r * max_children + k] = c.explore_count;
+    o.child_w[r * max_children + k] = c.total_reward;
+    o.child_out[r * max_children + k] =
+        c.outcome.empty() ? 2 : static_cast<int8_t>(c.outcome[c.player]);
+  }
+  o.root_n[r] = root.explore_count;
+  o.root_w[r] = root.total_reward;
+  o.root_out[r] = root.outcome.empty() ? 2
+                                        : static_cast<int8_t>(root.outcome[root.player]);
+  o.best_action[r] = nc > 0 ? root.BestChild().action : -1;
+  o.nodes[r] = st.nodes;
+}
+}  // namespace
+
+extern "C" {
+
+const char* oref_last_error() { return g_err.c_str(); }
+
+void* oref_game_new(const char* game_string) {
+  std::string err;
+  auto g = LoadGame(game_string, &err);
+  if (!g) {
+    g_err = err;
+    return nullptr;
+  }
+  auto* og = new OGame;
+  og->game = std::move(g);
+  return og;
+}
+
+void oref_game_free(void* g) { delete static_cast<OGame*>(g); }
+
+int oref_game_info(void* g, int32_t* num_actions, int32_t* max_len) {
+  auto* og = static_cast<OGame*>(g);
+  *num_actions = og->game->NumDistinctActions();
+  *max_len = og->game->MaxGameLength();
+  return 0;
+}
+
+// Replays `actions` and writes a JSON object describing the reached state.
+// Returns the number of bytes needed (excluding NUL); truncates to buflen-1.
+int64_t oref_state_json(void* g, const int64_t* actions, int64_t n, char* buf,
+                        int64_t buflen) {
+  auto* og = static_cast<OGame*>(g);
+  auto s = Replay(*og->game, actions, n);
+  std::string j = "{\"is_terminal\":";
+  j += s->IsTerminal() ? "true" : "false";
+  j += ",\"current_player\":" + std::to_string(s->CurrentPlayer());
+  auto r = s->Returns();
+  char tmp[64];
+  std::snprintf(tmp, sizeof tmp, ",\"returns\":[%.17g,%.17g]", r[0], r[1]);
+  j += tmp;
+  j += ",\"legal_actions\":[";
+  auto la = s->LegalActions();
+  for (size_t i = 0; i < la.size(); ++i) {
+    if (i) j += ",";
+    j += std::to_string(la[i]);
+  }
+  j += "],\"string_legal_actions\":[";
+  for (size_t i = 0; i < la.size(); ++i) {
+    if (i) j += ",";
+    j += "\"";
+    JsonEscape(s->ActionToString(s->CurrentPlayer(), la[i]), &j);
+    j += "\"";
+  }
+  j += "],\"observation_string\":\"";
+  JsonEscape(s->ToString(), &j);
+  j += "\"}";
+  if (buflen > 0) {
+    int64_t m = std::min<int64_t>(buflen - 1, static_cast<int64_t>(j.size()));
+    std::memcpy(buf, j.data(), m);
+    buf[m] = 0;
+  }
+  return static_cast<int64_t>(j.size());
+}
+
+// n random playouts from the replayed root, evaluator seed seeds[i] each
+// (one RandomRolloutEvaluator(n_rollouts, seed) per playout).
+int oref_rollouts(void* g, const int64_t* actions, int64_t n_actions,
+                  int64_t n, int32_t n_rollouts, const uint32_t* seeds,
+                  double* out_returns, int32_t* out_moves) {
+  auto* og = static_cast<OGame*>(g);
+  auto root = Replay(*og->game, actions, n_actions);
+  for (int64_t i = 0; i < n; ++i) {
+    RandomRolloutEvaluator ev(n_rollouts, seeds[i]);
+    if (out_moves) {
+      // Count moves of a single rollout separately (diagnostic only).
+      std::mt19937 g2(seeds[i]);
+      auto ws = root->Clone();
+      int m = 0;
+      while (!ws->IsTerminal()) {
+        auto a = ws->LegalActions();
+        ws->ApplyAction(a[AbslUniformU64(g2, a.size())]);
+        ++m;
+      }
+      out_moves[i] = m;
+    }
+    auto r = ev.Evaluate(*root);
+    out_returns[2 * i] = r[0];
+    out_returns[2 * i + 1] = r[1];
+  }
+  return 0;
+}
+
+// Batched independent searches (the C++ MCTSBot path, mcts.cc), one bot +
+// one RandomRolloutEvaluator per root, `threads` host threads with static
+// round-robin root assignment.  Writes child-ordered outputs.
+int oref_mcts_batch(void* g, int64_t num_roots, const int64_t* root_actions,
+                    const int64_t* root_offsets, double uct_c,
+                    int32_t max_simulations, int32_t n_rollouts,
+                    int64_t max_memory_mb, int32_t solve,
+                    const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                    int32_t max_children, int32_t* child_action,
+                    int32_t* child_n, double* child_w, int8_t* child_out,
+                    int32_t* nchild, int32_t* root_n, double* root_w,
+                    int8_t* root_out, int64_t* best_action, int32_t* nodes,
+                    int32_t threads) {
+  auto* og = static_cast<OGame*>(g);
+  RootOut o{child_action, child_n, child_w, child_out, nchild,
+            root_n,       root_w,  root_out, best_action, nodes};
+  if (threads < 1) threads = 1;
+  auto work = [&](int t) {
+    for (int64_t r = t; r < num_roots; r += threads) {
+      auto state = Replay(*og->game, root_actions + root_offsets[r],
+                          root_offsets[r + 1] - root_offsets[r]);
+      RandomRolloutEvaluator ev(n_rollouts, eval_seeds[r]);
+      MCTSBot bot(*og->game, &ev, uct_c, max_simulations, max_memory_mb,
+                  solve != 0, bot_seeds[r]);
+      SearchStats st;
+      auto root = bot.MCTSearch(*state, &st);
+      FillOut(*root, max_children, r, st, o);
+    }
+  };
+  if (threads == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(work, t);
+    for (auto& t : ts) t.join();
+  }
+  return 0;
+}
+
+// The Python mcts.py path with one shared numpy RandomState(seed).
+int oref_mcts_numpy(void* g, const int64_t* actions, int64_t n_actions,
+                    double uct_c, int32_t max_simulations, int32_t n_rollouts,
+                    int32_t solve, uint32_t seed, int32_t max_children,
+                    int32_t* child_action, int32_t* child_n, double* child_w,
+                    int8_t* child_out, int32_t* nchild, int32_t* root_n,
+                    double* root_w, int8_t* root_out, int64_t* best_action,
+                    int32_t* nodes, uint32_t* rng_state_out) {
+  auto* og = static_cast<OGame*>(g);
+  auto state = Replay(*og->game, actions, n_actions);
+  std::mt19937 rng(seed);
+  NumpyMCTSBot bot(*og->game, &rng, uct_c, max_simulations, n_rollouts,
+                   solve != 0);
+  SearchStats st;
+  auto root = bot.Search(*state, &st);
+  RootOut o{child_action, child_n, child_w, child_out, nchild,
+            root_n,       root_w,  root_out, best_action, nodes};
+  FillOut(*root, max_children, 0, st, o);
+  if (rng_state_out) rng_state_out[0] = rng();  // next raw word, for tests
+  return 0;
+}
+
+// Raw known-answer vectors: n words of std::mt19937(seed) / mt19937_64.
+void oref_mt19937(uint32_t seed, int64_t n, uint32_t* out) {
+  std::mt19937 g(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = g();
+}
+void oref_mt19937_64(uint64_t seed, int64_t n, uint64_t* out) {
+  std::mt19937_64 g(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = g();
+}
+// k draws of absl::Uniform(rng, 0u, n) from mt19937(seed).
+void oref_absl_uniform(uint32_t seed, uint64_t n, int64_t k, uint64_t* out) {
+  std::mt19937 g(seed);
+  for (int64_t i = 0; i < k; ++i) out[i] = AbslUniformU64(g, n);
+}
+// std::shuffle of [0..n) with mt19937(seed) (libstdc++ of this toolchain).
+void oref_std_shuffle(uint32_t seed, int32_t n, int32_t* out) {
+  std::mt19937 g(seed);
+  std::vector<std::pair<int64_t, double>> v;
+  for (int i = 0; i < n; ++i) v.emplace_back(i, 1.0 / n);
+  std::shuffle(v.begin(), v.end(), g);
+  for (int i = 0; i < n; ++i) out[i] = static_cast<int32_t>(v[i].first);
+}
+
+// Wall-clock helper for the CPU baseline: runs oref_mcts_batch on the first
+// `num_roots` roots with `threads` threads and returns seconds.
+double oref_time_mcts_batch(void* g, int64_t num_roots,
+                            const int64_t* root_actions,
+                            const int64_t* root_offsets, double uct_c,
+                            int32_t max_simulations, int32_t n_rollouts,
+                            int64_t max_memory_mb, int32_t solve,
+                            const uint32_t* bot_seeds,
+                            const uint32_t* eval_seeds, int32_t threads,
+                            int64_t* total_sims) {
+  auto* og = static_cast<OGame*>(g);
+  std::atomic<int64_t> sims{0};
+  if (threads < 1) threads = 1;
+  auto t0 = std::chrono::steady_clock::now();
+  auto work = [&](int t) {
+    int64_t local = 0;
+    for (int64_t r = t; r < num_roots; r += threads) {
+      auto state = Replay(*og->game, root_actions + root_offsets[r],
+                          root_offsets[r + 1] - root_offsets[r]);
+      RandomRolloutEvaluator ev(n_rollouts, eval_seeds[r]);
+      MCTSBot bot(*og->game, &ev, uct_c, max_simulations, max_memory_mb,
+                  solve != 0, bot_seeds[r]);
+      SearchStats st;
+      auto root = bot.MCTSearch(*state, &st);
+      local += root->explore_count;
+    }
+    sims += local;
+  };
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t) ts.emplace_back(work, t);
+  for (auto& t : ts) t.join();
+  auto t1 = std::chrono::steady_clock::now();
+  *total_sims = sims.load();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"
