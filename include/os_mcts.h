@@ -1,0 +1,179 @@
+/*
+ * os_mcts.h — C-ABI of libos_mcts.so, the MI355X-native batched MCTS engine.
+ *
+ * Drop-in boundary for OpenSpiel's MCTS random-rollout bot path.  Plain C
+ * types only (no torch / HIP types in signatures).  Every entry point cites the
+ * reference interface it replaces (paths are under open_spiel/ in
+ * Tyjch/open_spiel-1).
+ *
+ * Conventions
+ *   - Return value: 0 (OS_OK) on success, < 0 on error; os_last_error()
+ *     returns a thread-local message for the last failure on this thread.
+ *     The reference reports the same conditions through SpielFatalError
+ *     (spiel_utils.cc:94-110), surfaced in Python as RuntimeError
+ *     (pyspiel.cc:67-78, :839-840); unsupported game types raise ValueError in
+ *     python/algorithms/mcts.py:241-245 — OS_ERR_UNSUPPORTED maps to that.
+ *   - The caller owns every host buffer; an engine owns its device memory.
+ *   - Calls are synchronous unless named *_async.  One engine per device;
+ *     engines on different devices may be driven from different threads.
+ *   - Roots cross the ABI as action histories from the initial state (the
+ *     reference's default State::Serialize, spiel.h:541): root r is
+ *     root_actions[root_offsets[r] .. root_offsets[r+1]).
+ *   - Child outputs are in the tree's child order (the shuffled expansion
+ *     order of mcts.cc:275), stride max_children per root.
+ *   - Outcomes are int8: the value for the node's own player (the reference's
+ *     `outcome[player]`), or 2 when the node is unsolved (empty vector).
+ */
+#ifndef OS_MCTS_C_ABI_H_
+#define OS_MCTS_C_ABI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OS_OK 0
+#define OS_ERR_INVALID (-1)      /* bad argument / illegal action          */
+#define OS_ERR_UNSUPPORTED (-2)  /* game or parameter not supported        */
+#define OS_ERR_DEVICE (-3)       /* HIP runtime failure                     */
+#define OS_ERR_CAPACITY (-4)     /* node arena / path capacity exceeded     */
+
+typedef struct os_game os_game;
+typedef struct os_state os_state;
+typedef struct os_engine os_engine;
+
+/* Thread-local description of the last error on this thread. */
+const char* os_last_error(void);
+
+/* ---- Game / State: replaces pyspiel.load_game / pyspiel.State ------------
+ * pyspiel.cc:675-684 load_game; spiel.cc:176-204 LoadGame;
+ * game_parameters.cc:101-130 "name(k=v,...)" parsing.                    */
+int os_game_load(const char* game_string, os_game** out);
+void os_game_free(os_game* game);
+
+typedef struct {
+  int32_t kind;               /* 0 ttt, 1 connect_four, 2 breakthrough, 3 hex, 4 go */
+  int32_t num_distinct_actions;  /* Game::NumDistinctActions (spiel.h:601-750) */
+  int32_t max_game_length;    /* Game::MaxGameLength */
+  int32_t num_players;        /* 2 */
+  int32_t max_children;       /* upper bound on |LegalActions()| */
+  int32_t rows, cols;         /* board geometry */
+  double min_utility, max_utility, utility_sum;
+  double komi;                /* go only */
+  int32_t handicap;           /* go only */
+  int32_t state_bytes;        /* sizeof the device state record */
+} os_game_info;
+int os_game_get_info(const os_game* game, os_game_info* out);
+/* Canonical game string, e.g. "go(board_size=9,komi=7.5)". Returns length. */
+int64_t os_game_to_string(const os_game* game, char* buf, int64_t cap);
+
+/* State (spiel.h:173-592; pybind pyspiel.cc:292-360). */
+int os_state_new(const os_game* game, os_state** out);      /* NewInitialState */
+int os_state_clone(const os_state* s, os_state** out);      /* Clone (spiel.h:459) */
+void os_state_free(os_state* s);
+int os_state_apply(os_state* s, int64_t action);            /* ApplyAction (spiel.h:205) */
+int32_t os_state_current_player(const os_state* s);         /* CurrentPlayer (-4 terminal) */
+int32_t os_state_is_terminal(const os_state* s);            /* IsTerminal (spiel.h:283) */
+int os_state_returns(const os_state* s, double* out2);      /* Returns (spiel.h:309) */
+/* LegalActions (spiel.h:240), ascending; returns the count (may exceed cap). */
+int32_t os_state_legal_actions(const os_state* s, int64_t* out, int32_t cap);
+int32_t os_state_history(const os_state* s, int64_t* out, int32_t cap);
+int64_t os_state_to_string(const os_state* s, char* buf, int64_t cap);
+int64_t os_state_action_to_string(const os_state* s, int32_t player,
+                                  int64_t action, char* buf, int64_t cap);
+
+/* ---- Engine: replaces algorithms::MCTSBot / RandomRolloutEvaluator --------
+ * mcts.h:152-159 MCTSBot(game, evaluator, uct_c, max_simulations,
+ * max_memory_mb, solve, seed, verbose); mcts.h:94-95
+ * RandomRolloutEvaluator(n_rollouts, seed); pyspiel.cc:499-524.          */
+int os_engine_create(const char* game_string, int32_t device, os_engine** out);
+int os_engine_destroy(os_engine* e);
+
+#define OS_POLICY_CPP 0    /* mcts.cc: std::mt19937 bot + evaluator streams   */
+#define OS_POLICY_NUMPY 1  /* mcts.py: numpy RandomState (shared or separate) */
+
+typedef struct {
+  double uct_c;                 /* MCTSBot uct_c */
+  int32_t max_simulations;      /* MCTSBot max_simulations */
+  int32_t n_rollouts;           /* RandomRolloutEvaluator n_rollouts */
+  int64_t max_memory_mb;        /* MCTSBot max_memory_mb (drives GC, mcts.cc:402) */
+  int32_t solve;                /* MCTSBot solve (MCTS-Solver backup) */
+  int32_t policy;               /* OS_POLICY_* */
+  int32_t block_size;           /* 0 = default; lanes per workgroup */
+  int32_t pad;
+  int64_t arena_nodes;          /* 0 = exact worst case; else nodes per root */
+} os_mcts_params;
+
+/* Batched independent searches: MCTSBot::MCTSearch (mcts.cc:325-428) on every
+ * root, bot seed bot_seeds[r], evaluator seed eval_seeds[r].  Bit-exact with
+ * the reference given the same seeds.  Under OS_POLICY_NUMPY the two seeds
+ * seed numpy-style streams (equal seeds => the test's shared RandomState is
+ * NOT modelled; use os_mcts_numpy_state for a shared stream). */
+int os_mcts_batch(os_engine* e, const os_mcts_params* p, int64_t num_roots,
+                  const int64_t* root_actions, const int64_t* root_offsets,
+                  const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                  int32_t max_children, int32_t* child_action,
+                  int32_t* child_n, double* child_w, int8_t* child_out,
+                  int32_t* nchild, int32_t* root_n, double* root_w,
+                  int8_t* root_out, int64_t* best_action, int32_t* nodes);
+
+/* One search under OS_POLICY_NUMPY driven by caller-provided MT19937 states in
+ * numpy's legacy (key[624], pos) form, updated in place on return — the
+ * python/algorithms/mcts.py path with np.random.RandomState objects.
+ * shared != 0: one stream (bot_key) serves bot and evaluator
+ * (mcts_test.py:41-54); else eval_key/eval_pos is the evaluator's. */
+int os_mcts_numpy_state(os_engine* e, const os_mcts_params* p,
+                        const int64_t* root_actions, int64_t n_actions,
+                        int32_t shared, uint32_t* bot_key, int32_t* bot_pos,
+                        uint32_t* eval_key, int32_t* eval_pos,
+                        int32_t max_children, int32_t* child_action,
+                        int32_t* child_n, double* child_w, int8_t* child_out,
+                        int32_t* nchild, int32_t* root_n, double* root_w,
+                        int8_t* root_out, int64_t* best_action, int32_t* nodes);
+
+/* Whole search tree of root r of the last os_mcts_batch / numpy call, for
+ * materialising SearchNode objects (mcts.h:109-137).  First call with
+ * first == NULL to get the node count in *count. */
+int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
+                   int32_t* n, double* w, int32_t* action, int32_t* nchild,
+                   int8_t* out0);
+
+/* RandomRolloutEvaluator::Evaluate (mcts.cc:42-71) for n independent
+ * evaluators, seeds[i], from one root; out_returns[2*i+{0,1}]. */
+int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
+                      int64_t n_actions, int64_t n, int32_t n_rollouts,
+                      const uint32_t* seeds, double* out_returns);
+
+/* ---- Device-resident pipeline (inputs already in HBM; for benchmarks) ---
+ * prepare: upload roots + seeds and size the arena; run: launch the search
+ * kernel on `hip_stream` (a hipStream_t, or NULL for the null stream) with no
+ * host synchronisation; fetch: synchronise and copy results out (same layout
+ * as os_mcts_batch). */
+int os_engine_prepare(os_engine* e, const os_mcts_params* p, int64_t num_roots,
+                      const int64_t* root_actions, const int64_t* root_offsets,
+                      const uint32_t* bot_seeds, const uint32_t* eval_seeds);
+int os_engine_run_async(os_engine* e, void* hip_stream);
+int os_engine_fetch(os_engine* e, int32_t max_children, int32_t* child_action,
+                    int32_t* child_n, double* child_w, int8_t* child_out,
+                    int32_t* nchild, int32_t* root_n, double* root_w,
+                    int8_t* root_out, int64_t* best_action, int32_t* nodes);
+/* Summed simulations over the prepared roots of the last run (after fetch). */
+int64_t os_engine_last_sims(os_engine* e);
+
+/* Deterministic benchmark roots: root i = initial state plus
+ * k_i = g() % (max_plies + 1) uniformly random legal plies drawn from
+ * std::mt19937 g(seed_base + i), stopping before any ply that would end the
+ * game.  Writes histories (offsets has num_roots + 1 entries); returns the
+ * total action count, or < 0 on error.  actions may be NULL to size. */
+int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base,
+                      int32_t max_plies, int64_t* actions, int64_t* offsets);
+
+/* Library/kernel build info string (arch, build flags). */
+const char* os_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OS_MCTS_C_ABI_H_ */

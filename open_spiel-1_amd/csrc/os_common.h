@@ -1,0 +1,100 @@
+// Common host/device helpers for the MI355X MCTS engine.
+//
+// Everything in csrc/*.h compiles both for the host (hipcc host pass / g++)
+// and for gfx950; the same game state machines back the host State API and
+// the device search kernel, so there is one implementation of each rule set.
+#ifndef OS_COMMON_H_
+#define OS_COMMON_H_
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define OS_HD __host__ __device__ __forceinline__
+#define OS_HDNI __host__ __device__
+#else
+#define OS_HD inline
+#define OS_HDNI
+#endif
+
+namespace osm {
+
+OS_HD int popc64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popcll(x);
+#else
+  return __builtin_popcountll(x);
+#endif
+}
+
+OS_HD int ctz64(uint64_t x) {  // x != 0
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ffsll(static_cast<unsigned long long>(x)) - 1;
+#else
+  return __builtin_ctzll(x);
+#endif
+}
+
+// Index of the k-th (0-based) set bit of x, ascending.  Requires k < popc(x).
+OS_HD int select64(uint64_t x, int k) {
+  // Binary search on popcounts of the low half (6 steps, branch-light).
+  int base = 0;
+  int c = popc64(x & 0xFFFFFFFFull);
+  if (k >= c) { k -= c; x >>= 32; base += 32; }
+  c = popc64(x & 0xFFFFull);
+  if (k >= c) { k -= c; x >>= 16; base += 16; }
+  c = popc64(x & 0xFFull);
+  if (k >= c) { k -= c; x >>= 8; base += 8; }
+  c = popc64(x & 0xFull);
+  if (k >= c) { k -= c; x >>= 4; base += 4; }
+  c = popc64(x & 0x3ull);
+  if (k >= c) { k -= c; x >>= 2; base += 2; }
+  c = static_cast<int>(x & 1ull);
+  if (k >= c) { base += 1; }
+  return base;
+}
+
+// 128-bit bitboard (two u64 words).  Bit i = cell i.
+struct B128 {
+  uint64_t lo, hi;
+};
+OS_HD B128 b128(uint64_t lo, uint64_t hi) { B128 r; r.lo = lo; r.hi = hi; return r; }
+OS_HD B128 operator|(B128 a, B128 b) { return b128(a.lo | b.lo, a.hi | b.hi); }
+OS_HD B128 operator&(B128 a, B128 b) { return b128(a.lo & b.lo, a.hi & b.hi); }
+OS_HD B128 operator^(B128 a, B128 b) { return b128(a.lo ^ b.lo, a.hi ^ b.hi); }
+OS_HD B128 operator~(B128 a) { return b128(~a.lo, ~a.hi); }
+OS_HD bool operator==(B128 a, B128 b) { return a.lo == b.lo && a.hi == b.hi; }
+OS_HD bool operator!=(B128 a, B128 b) { return !(a == b); }
+OS_HD bool any(B128 a) { return (a.lo | a.hi) != 0; }
+OS_HD int popc(B128 a) { return popc64(a.lo) + popc64(a.hi); }
+OS_HD B128 shl(B128 a, int s) {  // 0 < s < 64
+  return b128(a.lo << s, (a.hi << s) | (a.lo >> (64 - s)));
+}
+OS_HD B128 shr(B128 a, int s) {  // 0 < s < 64
+  return b128((a.lo >> s) | (a.hi << (64 - s)), a.hi >> s);
+}
+OS_HD B128 bit128(int i) {
+  return i < 64 ? b128(1ull << i, 0) : b128(0, 1ull << (i - 64));
+}
+OS_HD bool test(B128 a, int i) {
+  return i < 64 ? ((a.lo >> i) & 1) : ((a.hi >> (i - 64)) & 1);
+}
+OS_HD int lowest(B128 a) {  // a != 0
+  return a.lo ? ctz64(a.lo) : 64 + ctz64(a.hi);
+}
+OS_HD int select128(B128 a, int k) {
+  int c = popc64(a.lo);
+  return k < c ? select64(a.lo, k) : 64 + select64(a.hi, k - c);
+}
+// Mask of the low n bits (0 <= n <= 128).
+OS_HD B128 lowmask128(int n) {
+  if (n <= 0) return b128(0, 0);
+  if (n < 64) return b128((1ull << n) - 1, 0);
+  if (n == 64) return b128(~0ull, 0);
+  if (n < 128) return b128(~0ull, (1ull << (n - 64)) - 1);
+  return b128(~0ull, ~0ull);
+}
+
+}  // namespace osm
+
+#endif  // OS_COMMON_H_

@@ -1,0 +1,903 @@
+// libos_mcts.so — gfx950 search / rollout kernels and the C-ABI declared in
+// include/os_mcts.h.
+//
+// Execution model: one lane = one independent search
+// (MCTSBot::MCTSearch, mcts.cc:325-428).  A lane keeps its working game state
+// in registers, its two MT19937 streams (bot + evaluator, 2 x 624 words) and
+// its flat node arena in HBM, and its path / expansion buffers in private
+// scratch.  Searches never share memory, so there are no atomics and results
+// are bit-exact regardless of scheduling.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <random>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/os_mcts.h"
+#include "os_host.h"
+#include "os_mcts.h"
+
+using namespace osm;
+
+// ---------------------------------------------------------------------------
+// Errors
+namespace {
+thread_local std::string g_err;
+int Fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess)                                                    \
+      return Fail(OS_ERR_DEVICE, std::string(#expr " failed: ") +            \
+                                     hipGetErrorString(_e));                 \
+  } while (0)
+}  // namespace
+
+struct os_game {
+  HostGame g;
+};
+struct os_state {
+  HostState s;
+};
+
+// ---------------------------------------------------------------------------
+// Device code
+namespace {
+
+constexpr int kGoLogCap = 248;  // >= 2 * 11 * 11 + 4
+
+struct DevArgs {
+  GameCfg cfg;
+  SearchParams sp;
+  int64_t num_roots;      // roots in this launch
+  int64_t root_base;      // global index of the first root of this launch
+  const void* roots;      // [total] G::State
+  const uint32_t* bot_seeds;
+  const uint32_t* eval_seeds;
+  uint32_t* mt;           // [num_roots][2][624]
+  void* arena;            // [num_roots][cap] Node<R>
+  uint32_t cap;
+  int32_t import_state;   // numpy (key, pos) import / export
+  int32_t shared_stream;  // numpy: one RandomState for bot + evaluator
+  int32_t* mt_pos;        // [total][2] in/out when import_state
+  // go
+  const uint64_t* zob;
+  const uint64_t* root_hashes;  // [total][hash_stride]
+  const int32_t* root_nhash;    // [total]
+  int32_t hash_stride;
+  // outputs, indexed by global root
+  SearchResult* results;
+  int32_t max_children;
+  int32_t* child_action;
+  int32_t* child_n;
+  double* child_w;
+  int8_t* child_out;
+  int32_t* nchild;
+  int32_t* root_n;
+  double* root_w;
+  int8_t* root_out;
+  int64_t* best_action;
+};
+
+template <class G>
+struct CtxMaker;
+template <class G>
+struct CtxMaker {
+  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct CtxMaker<Go> {
+  __device__ static GoCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
+    GoCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    for (int i = 0; i < 4; ++i) c.base_filt[i] = 0;
+    for (int i = 0; i < c.n_base; ++i) {
+      const int b = GoCtx::fbit(c.base[i]);
+      c.base_filt[b >> 6] |= 1ull << (b & 63);
+    }
+    for (int i = 0; i < 4; ++i) c.filt[i] = c.base_filt[i];
+    return c;
+  }
+};
+
+template <class G, class R, int Policy>
+__global__ void k_mcts(DevArgs a) {
+  const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (lr >= a.num_roots) return;
+  const int64_t gr = a.root_base + lr;
+  uint32_t* mt0 = a.mt + lr * 2 * kMtN;
+  MtStream bot{mt0, kMtN, 0};
+  MtStream ev{mt0 + kMtN, kMtN, 0};
+  if (a.import_state) {
+    bot.idx = a.mt_pos[2 * gr];
+    bot.pre = 1;
+    ev.idx = a.mt_pos[2 * gr + 1];
+    ev.pre = 1;
+  } else {
+    mt_seed(bot.s, a.bot_seeds[gr]);
+    if (!(Policy == kPolicyNumpy && a.shared_stream)) mt_seed(ev.s, a.eval_seeds[gr]);
+  }
+  const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
+  uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
+  typename G::Ctx ctx = CtxMaker<G>::make(a, gr, glog);
+  uint32_t path[kMaxPath];
+  uint16_t actbuf[kMaxChildren];
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  SearchResult res;
+  if (Policy == kPolicyNumpy && a.shared_stream)
+    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
+                                    path, actbuf);
+  else
+    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
+                                    path, actbuf);
+  a.results[gr] = res;
+  const Node<R>& rn = nodes[0];
+  const int P0 = G::to_move(root);
+  const int nc = rn.nchild;
+  a.nchild[gr] = nc;
+  a.root_n[gr] = rn.n;
+  a.root_w[gr] = static_cast<double>(rn.w);
+  a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
+                                       : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+  const int64_t ob = gr * a.max_children;
+  for (int k = 0; k < nc && k < a.max_children; ++k) {
+    const Node<R>& c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = static_cast<double>(c.w);
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  const int b = best_child(nodes, P0);
+  a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+  if (a.import_state) {
+    bot.finalize();
+    a.mt_pos[2 * gr] = bot.idx;
+    if (!a.shared_stream) {
+      ev.finalize();
+      a.mt_pos[2 * gr + 1] = ev.idx;
+    }
+  }
+}
+
+struct RollArgs {
+  GameCfg cfg;
+  int64_t n;
+  int32_t n_rollouts;
+  const void* root;  // one G::State
+  const uint32_t* seeds;
+  uint32_t* mt;      // [n][624]
+  double* out;       // [n][2]
+  const uint64_t* zob;
+  const uint64_t* root_hashes;
+  int32_t n_root_hashes;
+};
+
+template <class G>
+struct RollCtx {
+  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct RollCtx<Go> {
+  __device__ static GoCtx make(const RollArgs& a, uint64_t* log) {
+    GoCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes;
+    c.n_base = a.n_root_hashes;
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    for (int i = 0; i < 4; ++i) c.base_filt[i] = 0;
+    for (int i = 0; i < c.n_base; ++i) {
+      const int b = GoCtx::fbit(c.base[i]);
+      c.base_filt[b >> 6] |= 1ull << (b & 63);
+    }
+    for (int i = 0; i < 4; ++i) c.filt[i] = c.base_filt[i];
+    return c;
+  }
+};
+
+template <class G>
+__global__ void k_rollouts(RollArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  MtStream ev{a.mt + i * kMtN, kMtN, 0};
+  mt_seed(ev.s, a.seeds[i]);
+  uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
+  typename G::Ctx ctx = RollCtx<G>::make(a, glog);
+  const typename G::State root = *static_cast<const typename G::State*>(a.root);
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < a.n_rollouts; ++k) {
+    ctx.reset();
+    const int r0 = rollout_ret0<G, kPolicyCpp>(root, a.cfg, ctx, ev);
+    s0 += static_cast<double>(r0);
+    s1 += static_cast<double>(-r0);
+  }
+  a.out[2 * i] = s0 / a.n_rollouts;
+  a.out[2 * i + 1] = s1 / a.n_rollouts;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Host engine
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t b) {
+    if (b <= bytes && p) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (b == 0) return 0;
+    hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return Fail(OS_ERR_DEVICE, std::string("hipMalloc(") + std::to_string(b) +
+                                     ") failed: " + hipGetErrorString(e));
+    }
+    bytes = b;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+}  // namespace
+
+struct os_engine {
+  HostGame game;
+  int device = 0;
+  // prepared run
+  os_mcts_params params{};
+  int64_t num_roots = 0;
+  int64_t chunk_roots = 0;
+  uint32_t cap = 0;
+  int node_bytes = 16;
+  int32_t max_children = 0;
+  int32_t hash_stride = 1;
+  bool import_state = false;
+  bool shared_stream = false;
+  DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
+      d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
+      d_rollout_out;
+  std::vector<SearchResult> last_results;
+  int64_t last_sims = 0;
+  ~os_engine() {
+    DevBuf* all[] = {&d_roots, &d_bseed, &d_eseed, &d_mt,  &d_arena, &d_lut,
+                     &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
+                     &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
+                     &d_rout,  &d_best,  &d_rollout_out};
+    (void)hipSetDevice(device);
+    for (DevBuf* b : all) b->release();
+  }
+};
+
+namespace {
+
+template <class G>
+using StateOf = typename G::State;
+
+// Replays a history on the host; returns false if an action is illegal.
+bool ReplayRoot(const HostGame& g, const int64_t* a, int64_t n, HostState* s,
+                std::string* err) {
+  s->game = &g;
+  StateInit(s);
+  for (int64_t i = 0; i < n; ++i) {
+    if (!StateApply(s, a[i])) {
+      *err = "illegal action " + std::to_string(a[i]) + " at ply " + std::to_string(i) +
+             " of a root history";
+      return false;
+    }
+  }
+  return true;
+}
+
+template <class G, class R, int Policy>
+int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
+  const int bs = e->params.block_size > 0 ? e->params.block_size : 64;
+  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+    a.root_base = base;
+    a.num_roots = n;
+    const unsigned grid = static_cast<unsigned>((n + bs - 1) / bs);
+    hipLaunchKernelGGL((k_mcts<G, R, Policy>), dim3(grid), dim3(bs), 0, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+      return Fail(OS_ERR_DEVICE, std::string("k_mcts launch failed: ") +
+                                     hipGetErrorString(err));
+  }
+  return OS_OK;
+}
+
+template <class G>
+int LaunchForGame(os_engine* e, const DevArgs& a, hipStream_t stream) {
+  const bool dbl = e->params.n_rollouts != 1;
+  if (e->params.policy == OS_POLICY_NUMPY) {
+    return dbl ? LaunchSearch<G, double, kPolicyNumpy>(e, a, stream)
+               : LaunchSearch<G, int32_t, kPolicyNumpy>(e, a, stream);
+  }
+  return dbl ? LaunchSearch<G, double, kPolicyCpp>(e, a, stream)
+             : LaunchSearch<G, int32_t, kPolicyCpp>(e, a, stream);
+}
+
+int CheckParams(const os_engine* e, const os_mcts_params* p) {
+  if (!p) return Fail(OS_ERR_INVALID, "null params");
+  if (p->max_simulations < 0) return Fail(OS_ERR_INVALID, "max_simulations < 0");
+  if (p->n_rollouts < 1) return Fail(OS_ERR_INVALID, "n_rollouts must be >= 1");
+  if (p->policy != OS_POLICY_CPP && p->policy != OS_POLICY_NUMPY)
+    return Fail(OS_ERR_INVALID, "unknown policy");
+  if (p->block_size < 0 || p->block_size > 1024)
+    return Fail(OS_ERR_INVALID, "block_size must be in [0, 1024]");
+  if (e->game.cfg.max_children > kMaxChildren)
+    return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxChildren");
+  if (e->game.cfg.max_game_length >= kMaxPath)
+    return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxPath");
+  return OS_OK;
+}
+
+// Uploads roots / seeds, sizes and allocates the arena and outputs.
+int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
+            const int64_t* root_actions, const int64_t* root_offsets,
+            const uint32_t* bot_seeds, const uint32_t* eval_seeds) {
+  int rc = CheckParams(e, p);
+  if (rc) return rc;
+  if (R < 0) return Fail(OS_ERR_INVALID, "num_roots < 0");
+  HIP_TRY(hipSetDevice(e->device));
+  e->params = *p;
+  e->num_roots = R;
+  const GameCfg& cfg = e->game.cfg;
+  e->max_children = cfg.max_children;
+  e->node_bytes = p->n_rollouts == 1 ? static_cast<int>(sizeof(Node<int32_t>))
+                                      : static_cast<int>(sizeof(Node<double>));
+  // Arena: exact worst case = 1 + sims * max_children (one expansion per
+  // simulation at most), unless the caller caps it.
+  int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * cfg.max_children;
+  int64_t cap = p->arena_nodes > 0 ? std::min<int64_t>(p->arena_nodes, worst) : worst;
+  if (cap < 1) cap = 1;
+  if (cap > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "arena too large per root");
+  e->cap = static_cast<uint32_t>(cap);
+  // Chunk roots so that arena + MT state stay within ~60% of free HBM.
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const size_t per_root = static_cast<size_t>(cap) * e->node_bytes + 2 * kMtN * 4;
+  size_t budget = static_cast<size_t>(free_b * 0.6);
+  int64_t chunk = per_root ? static_cast<int64_t>(budget / per_root) : R;
+  if (chunk < 1) return Fail(OS_ERR_CAPACITY, "not enough device memory for one root");
+  e->chunk_roots = std::max<int64_t>(1, std::min<int64_t>(chunk, std::max<int64_t>(R, 1)));
+
+  // Root states (+ go hash sets) on the host.
+  const int sb = e->game.state_bytes;
+  std::vector<unsigned char> roots(static_cast<size_t>(std::max<int64_t>(R, 1)) * sb);
+  const bool go = cfg.kind == kGo;
+  e->hash_stride = go ? cfg.max_game_length + 2 : 1;
+  std::vector<uint64_t> rh;
+  std::vector<int32_t> rnh;
+  if (go) {
+    rh.assign(static_cast<size_t>(std::max<int64_t>(R, 1)) * e->hash_stride, 0);
+    rnh.assign(std::max<int64_t>(R, 1), 0);
+  }
+  for (int64_t r = 0; r < R; ++r) {
+    HostState hs;
+    std::string err;
+    if (!ReplayRoot(e->game, root_actions + root_offsets[r],
+                    root_offsets[r + 1] - root_offsets[r], &hs, &err))
+      return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
+    if (StateTerminal(hs))
+      return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
+    std::memcpy(roots.data() + r * sb, hs.raw, sb);
+    if (go) {
+      const int64_t nh = static_cast<int64_t>(hs.hashes.size());
+      if (nh > e->hash_stride) return Fail(OS_ERR_CAPACITY, "go hash history too long");
+      std::memcpy(rh.data() + r * e->hash_stride, hs.hashes.data(), nh * 8);
+      rnh[r] = static_cast<int32_t>(nh);
+    }
+  }
+  const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
+  if ((rc = e->d_roots.ensure(Rz * sb))) return rc;
+  HIP_TRY(hipMemcpy(e->d_roots.p, roots.data(), Rz * sb, hipMemcpyHostToDevice));
+  if ((rc = e->d_bseed.ensure(Rz * 4)) || (rc = e->d_eseed.ensure(Rz * 4))) return rc;
+  if (R > 0) {
+    HIP_TRY(hipMemcpy(e->d_bseed.p, bot_seeds, R * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_eseed.p, eval_seeds ? eval_seeds : bot_seeds, R * 4,
+                      hipMemcpyHostToDevice));
+  }
+  if (go) {
+    if ((rc = e->d_rhash.ensure(rh.size() * 8)) || (rc = e->d_rnh.ensure(rnh.size() * 4)))
+      return rc;
+    HIP_TRY(hipMemcpy(e->d_rhash.p, rh.data(), rh.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_rnh.p, rnh.data(), rnh.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
+    HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
+                      hipMemcpyHostToDevice));
+  }
+  // log(N) LUT from the host libm, N in [0, max_simulations] (UCTValue's
+  // std::log(parent_explore_count), mcts.cc:99).
+  std::vector<double> lut(static_cast<size_t>(p->max_simulations) + 2);
+  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  if ((rc = e->d_lut.ensure(lut.size() * 8))) return rc;
+  HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice));
+  // Work buffers.
+  const size_t C = static_cast<size_t>(e->chunk_roots);
+  if ((rc = e->d_mt.ensure(C * 2 * kMtN * 4))) return rc;
+  if ((rc = e->d_arena.ensure(C * static_cast<size_t>(e->cap) * e->node_bytes))) return rc;
+  const size_t MC = Rz * e->max_children;
+  if ((rc = e->d_res.ensure(Rz * sizeof(SearchResult))) || (rc = e->d_cact.ensure(MC * 4)) ||
+      (rc = e->d_cn.ensure(MC * 4)) || (rc = e->d_cw.ensure(MC * 8)) ||
+      (rc = e->d_cout.ensure(MC)) || (rc = e->d_nch.ensure(Rz * 4)) ||
+      (rc = e->d_rn.ensure(Rz * 4)) || (rc = e->d_rw.ensure(Rz * 8)) ||
+      (rc = e->d_rout.ensure(Rz)) || (rc = e->d_best.ensure(Rz * 8)) ||
+      (rc = e->d_pos.ensure(Rz * 8)))
+    return rc;
+  e->import_state = false;
+  e->shared_stream = false;
+  return OS_OK;
+}
+
+DevArgs MakeArgs(os_engine* e) {
+  DevArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.sp.uct_c = e->params.uct_c;
+  a.sp.max_simulations = e->params.max_simulations;
+  a.sp.n_rollouts = e->params.n_rollouts;
+  a.sp.solve = e->params.solve;
+  // mcts.cc:201: max_nodes_ = (max_memory_mb << 20) / sizeof(SearchNode) + 1,
+  // with sizeof(SearchNode) == 80 on LP64 libstdc++.
+  const int64_t mn = (e->params.max_memory_mb << 20) / 80 + 1;
+  a.sp.max_nodes = static_cast<int32_t>(mn);
+  a.sp.policy = e->params.policy;
+  a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
+  a.roots = e->d_roots.p;
+  a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.eval_seeds = static_cast<const uint32_t*>(e->d_eseed.p);
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.arena = e->d_arena.p;
+  a.cap = e->cap;
+  a.import_state = e->import_state ? 1 : 0;
+  a.shared_stream = e->shared_stream ? 1 : 0;
+  a.mt_pos = static_cast<int32_t*>(e->d_pos.p);
+  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+  a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
+  a.root_nhash = static_cast<const int32_t*>(e->d_rnh.p);
+  a.hash_stride = e->hash_stride;
+  a.results = static_cast<SearchResult*>(e->d_res.p);
+  a.max_children = e->max_children;
+  a.child_action = static_cast<int32_t*>(e->d_cact.p);
+  a.child_n = static_cast<int32_t*>(e->d_cn.p);
+  a.child_w = static_cast<double*>(e->d_cw.p);
+  a.child_out = static_cast<int8_t*>(e->d_cout.p);
+  a.nchild = static_cast<int32_t*>(e->d_nch.p);
+  a.root_n = static_cast<int32_t*>(e->d_rn.p);
+  a.root_w = static_cast<double*>(e->d_rw.p);
+  a.root_out = static_cast<int8_t*>(e->d_rout.p);
+  a.best_action = static_cast<int64_t*>(e->d_best.p);
+  return a;
+}
+
+int Run(os_engine* e, hipStream_t stream) {
+  HIP_TRY(hipSetDevice(e->device));
+  if (e->num_roots == 0) return OS_OK;
+  DevArgs a = MakeArgs(e);
+  switch (e->game.cfg.kind) {
+    case kTicTacToe: return LaunchForGame<TicTacToe>(e, a, stream);
+    case kConnectFour: return LaunchForGame<ConnectFour>(e, a, stream);
+    case kBreakthrough: return LaunchForGame<Breakthrough>(e, a, stream);
+    case kHex: return LaunchForGame<Hex>(e, a, stream);
+    case kGo: return LaunchForGame<Go>(e, a, stream);
+  }
+  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+}
+
+int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
+          int32_t* child_n, double* child_w, int8_t* child_out, int32_t* nchild,
+          int32_t* root_n, double* root_w, int8_t* root_out, int64_t* best_action,
+          int32_t* nodes) {
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const int64_t R = e->num_roots;
+  if (R == 0) return OS_OK;
+  if (max_children < e->max_children)
+    return Fail(OS_ERR_INVALID, "max_children smaller than the game's bound (" +
+                                    std::to_string(e->max_children) + ")");
+  e->last_results.resize(R);
+  HIP_TRY(hipMemcpy(e->last_results.data(), e->d_res.p, R * sizeof(SearchResult),
+                    hipMemcpyDeviceToHost));
+  e->last_sims = 0;
+  for (int64_t r = 0; r < R; ++r) {
+    const SearchResult& s = e->last_results[r];
+    if (s.status != kOk) {
+      const char* why = s.status == kArenaOverflow
+                            ? "node arena overflow (raise arena_nodes)"
+                            : (s.status == kPathOverflow ? "tree path overflow"
+                                                         : "GC stack overflow");
+      return Fail(OS_ERR_CAPACITY, "root " + std::to_string(r) + ": " + why);
+    }
+    e->last_sims += s.sims;
+    if (nodes) nodes[r] = s.nodes;
+  }
+  const int mcd = e->max_children;
+  std::vector<int32_t> ca(R * mcd), cn(R * mcd);
+  std::vector<double> cw(R * mcd);
+  std::vector<int8_t> co(R * mcd);
+  HIP_TRY(hipMemcpy(ca.data(), e->d_cact.p, ca.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cn.data(), e->d_cn.p, cn.size() * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cw.data(), e->d_cw.p, cw.size() * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(co.data(), e->d_cout.p, co.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nchild, e->d_nch.p, R * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(root_n, e->d_rn.p, R * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(root_w, e->d_rw.p, R * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(root_out, e->d_rout.p, R, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(best_action, e->d_best.p, R * 8, hipMemcpyDeviceToHost));
+  for (int64_t r = 0; r < R; ++r) {
+    for (int k = 0; k < max_children; ++k) {
+      const int64_t o = r * max_children + k;
+      if (k < nchild[r] && k < mcd) {
+        child_action[o] = ca[r * mcd + k];
+        child_n[o] = cn[r * mcd + k];
+        child_w[o] = cw[r * mcd + k];
+        child_out[o] = co[r * mcd + k];
+      } else {
+        child_action[o] = -1;
+        child_n[o] = 0;
+        child_w[o] = 0.0;
+        child_out[o] = kUnsolved;
+      }
+    }
+  }
+  return OS_OK;
+}
+
+template <class G>
+int LaunchRollouts(os_engine* e, const HostState& root, int64_t n, int32_t nr,
+                   const uint32_t* seeds, double* out) {
+  int rc;
+  const size_t sb = e->game.state_bytes;
+  if ((rc = e->d_roots.ensure(sb))) return rc;
+  HIP_TRY(hipMemcpy(e->d_roots.p, root.raw, sb, hipMemcpyHostToDevice));
+  if ((rc = e->d_bseed.ensure(std::max<int64_t>(n, 1) * 4))) return rc;
+  HIP_TRY(hipMemcpy(e->d_bseed.p, seeds, n * 4, hipMemcpyHostToDevice));
+  if ((rc = e->d_mt.ensure(std::max<int64_t>(n, 1) * kMtN * 4))) return rc;
+  if ((rc = e->d_rollout_out.ensure(std::max<int64_t>(n, 1) * 16))) return rc;
+  RollArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.n = n;
+  a.n_rollouts = nr;
+  a.root = e->d_roots.p;
+  a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.out = static_cast<double*>(e->d_rollout_out.p);
+  if (e->game.cfg.kind == kGo) {
+    if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
+    HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
+                      hipMemcpyHostToDevice));
+    if ((rc = e->d_rhash.ensure(std::max<size_t>(root.hashes.size(), 1) * 8))) return rc;
+    HIP_TRY(hipMemcpy(e->d_rhash.p, root.hashes.data(), root.hashes.size() * 8,
+                      hipMemcpyHostToDevice));
+    a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+    a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
+    a.n_root_hashes = static_cast<int32_t>(root.hashes.size());
+  }
+  const int bs = 64;
+  hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
+                     dim3(bs), 0, 0, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, e->d_rollout_out.p, n * 16, hipMemcpyDeviceToHost));
+  return OS_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+extern "C" {
+
+const char* os_last_error(void) { return g_err.c_str(); }
+
+const char* os_build_info(void) {
+  return "libos_mcts: gfx950 search/rollout kernels, one lane per search, "
+         "-ffp-contract=off, lazy in-place MT19937";
+}
+
+int os_game_load(const char* game_string, os_game** out) {
+  if (!game_string || !out) return Fail(OS_ERR_INVALID, "null argument");
+  auto g = std::make_unique<os_game>();
+  bool unsupported = false;
+  std::string err = LoadHostGame(game_string, &g->g, &unsupported);
+  if (!err.empty()) return Fail(unsupported ? OS_ERR_UNSUPPORTED : OS_ERR_INVALID, err);
+  *out = g.release();
+  return OS_OK;
+}
+
+void os_game_free(os_game* game) { delete game; }
+
+int os_game_get_info(const os_game* game, os_game_info* o) {
+  if (!game || !o) return Fail(OS_ERR_INVALID, "null argument");
+  const GameCfg& c = game->g.cfg;
+  std::memset(o, 0, sizeof *o);
+  o->kind = c.kind;
+  o->num_distinct_actions = c.num_actions;
+  o->max_game_length = c.max_game_length;
+  o->num_players = 2;
+  o->max_children = c.max_children;
+  o->rows = c.rows;
+  o->cols = c.cols;
+  o->min_utility = -1.0;
+  o->max_utility = 1.0;
+  o->utility_sum = 0.0;
+  o->komi = c.komi;
+  o->handicap = c.handicap;
+  o->state_bytes = game->g.state_bytes;
+  return OS_OK;
+}
+
+static int64_t CopyOut(const std::string& s, char* buf, int64_t cap) {
+  if (buf && cap > 0) {
+    const int64_t m = std::min<int64_t>(cap - 1, static_cast<int64_t>(s.size()));
+    std::memcpy(buf, s.data(), m);
+    buf[m] = 0;
+  }
+  return static_cast<int64_t>(s.size());
+}
+
+int64_t os_game_to_string(const os_game* game, char* buf, int64_t cap) {
+  return CopyOut(game->g.canonical, buf, cap);
+}
+
+int os_state_new(const os_game* game, os_state** out) {
+  if (!game || !out) return Fail(OS_ERR_INVALID, "null argument");
+  auto s = std::make_unique<os_state>();
+  s->s.game = &game->g;
+  StateInit(&s->s);
+  *out = s.release();
+  return OS_OK;
+}
+
+int os_state_clone(const os_state* s, os_state** out) {
+  if (!s || !out) return Fail(OS_ERR_INVALID, "null argument");
+  *out = new os_state(*s);
+  return OS_OK;
+}
+
+void os_state_free(os_state* s) { delete s; }
+
+int os_state_apply(os_state* s, int64_t action) {
+  if (!s) return Fail(OS_ERR_INVALID, "null state");
+  if (!StateApply(&s->s, action))
+    return Fail(OS_ERR_INVALID, "illegal action " + std::to_string(action) +
+                                    " in state\n" + StateToString(s->s));
+  return OS_OK;
+}
+
+int32_t os_state_current_player(const os_state* s) { return StateCurrentPlayer(s->s); }
+int32_t os_state_is_terminal(const os_state* s) { return StateTerminal(s->s) ? 1 : 0; }
+int os_state_returns(const os_state* s, double* out2) {
+  StateReturns(s->s, out2);
+  return OS_OK;
+}
+int32_t os_state_legal_actions(const os_state* s, int64_t* out, int32_t cap) {
+  std::vector<int64_t> v;
+  StateLegal(s->s, &v);
+  for (int32_t i = 0; i < cap && i < static_cast<int32_t>(v.size()); ++i) out[i] = v[i];
+  return static_cast<int32_t>(v.size());
+}
+int32_t os_state_history(const os_state* s, int64_t* out, int32_t cap) {
+  const auto& h = s->s.history;
+  for (int32_t i = 0; i < cap && i < static_cast<int32_t>(h.size()); ++i) out[i] = h[i];
+  return static_cast<int32_t>(h.size());
+}
+int64_t os_state_to_string(const os_state* s, char* buf, int64_t cap) {
+  return CopyOut(StateToString(s->s), buf, cap);
+}
+int64_t os_state_action_to_string(const os_state* s, int32_t player, int64_t action,
+                                  char* buf, int64_t cap) {
+  return CopyOut(StateActionToString(s->s, player, action), buf, cap);
+}
+
+int os_engine_create(const char* game_string, int32_t device, os_engine** out) {
+  if (!game_string || !out) return Fail(OS_ERR_INVALID, "null argument");
+  auto e = std::make_unique<os_engine>();
+  bool unsupported = false;
+  std::string err = LoadHostGame(game_string, &e->game, &unsupported);
+  if (!err.empty()) return Fail(unsupported ? OS_ERR_UNSUPPORTED : OS_ERR_INVALID, err);
+  int ndev = 0;
+  hipError_t he = hipGetDeviceCount(&ndev);
+  if (he != hipSuccess || ndev == 0)
+    return Fail(OS_ERR_DEVICE, std::string("no HIP device available: ") +
+                                   (he != hipSuccess ? hipGetErrorString(he) : "0 devices"));
+  if (device < 0 || device >= ndev)
+    return Fail(OS_ERR_INVALID, "device index out of range");
+  e->device = device;
+  HIP_TRY(hipSetDevice(device));
+  *out = e.release();
+  return OS_OK;
+}
+
+int os_engine_destroy(os_engine* e) {
+  delete e;
+  return OS_OK;
+}
+
+int os_engine_prepare(os_engine* e, const os_mcts_params* p, int64_t num_roots,
+                      const int64_t* root_actions, const int64_t* root_offsets,
+                      const uint32_t* bot_seeds, const uint32_t* eval_seeds) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return Prepare(e, p, num_roots, root_actions, root_offsets, bot_seeds, eval_seeds);
+}
+
+int os_engine_run_async(os_engine* e, void* hip_stream) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return Run(e, static_cast<hipStream_t>(hip_stream));
+}
+
+int os_engine_fetch(os_engine* e, int32_t max_children, int32_t* child_action,
+                    int32_t* child_n, double* child_w, int8_t* child_out,
+                    int32_t* nchild, int32_t* root_n, double* root_w,
+                    int8_t* root_out, int64_t* best_action, int32_t* nodes) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return Fetch(e, max_children, child_action, child_n, child_w, child_out, nchild,
+               root_n, root_w, root_out, best_action, nodes);
+}
+
+int64_t os_engine_last_sims(os_engine* e) { return e ? e->last_sims : -1; }
+
+int os_mcts_batch(os_engine* e, const os_mcts_params* p, int64_t num_roots,
+                  const int64_t* root_actions, const int64_t* root_offsets,
+                  const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                  int32_t max_children, int32_t* child_action, int32_t* child_n,
+                  double* child_w, int8_t* child_out, int32_t* nchild,
+                  int32_t* root_n, double* root_w, int8_t* root_out,
+                  int64_t* best_action, int32_t* nodes) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  int rc = Prepare(e, p, num_roots, root_actions, root_offsets, bot_seeds, eval_seeds);
+  if (rc) return rc;
+  if ((rc = Run(e, nullptr))) return rc;
+  return Fetch(e, max_children, child_action, child_n, child_w, child_out, nchild,
+               root_n, root_w, root_out, best_action, nodes);
+}
+
+int os_mcts_numpy_state(os_engine* e, const os_mcts_params* p,
+                        const int64_t* root_actions, int64_t n_actions,
+                        int32_t shared, uint32_t* bot_key, int32_t* bot_pos,
+                        uint32_t* eval_key, int32_t* eval_pos,
+                        int32_t max_children, int32_t* child_action,
+                        int32_t* child_n, double* child_w, int8_t* child_out,
+                        int32_t* nchild, int32_t* root_n, double* root_w,
+                        int8_t* root_out, int64_t* best_action, int32_t* nodes) {
+  if (!e || !p || !bot_key || !bot_pos) return Fail(OS_ERR_INVALID, "null argument");
+  if (p->policy != OS_POLICY_NUMPY)
+    return Fail(OS_ERR_INVALID, "os_mcts_numpy_state needs OS_POLICY_NUMPY");
+  if (!shared && (!eval_key || !eval_pos))
+    return Fail(OS_ERR_INVALID, "separate evaluator stream needs eval_key/eval_pos");
+  int64_t offs[2] = {0, n_actions};
+  uint32_t zero = 0;
+  int rc = Prepare(e, p, 1, root_actions, offs, &zero, &zero);
+  if (rc) return rc;
+  e->import_state = true;
+  e->shared_stream = shared != 0;
+  HIP_TRY(hipMemcpy(e->d_mt.p, bot_key, kMtN * 4, hipMemcpyHostToDevice));
+  int32_t pos[2] = {*bot_pos, shared ? 0 : *eval_pos};
+  if (!shared)
+    HIP_TRY(hipMemcpy(static_cast<uint32_t*>(e->d_mt.p) + kMtN, eval_key, kMtN * 4,
+                      hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_pos.p, pos, 8, hipMemcpyHostToDevice));
+  if ((rc = Run(e, nullptr))) return rc;
+  rc = Fetch(e, max_children, child_action, child_n, child_w, child_out, nchild, root_n,
+             root_w, root_out, best_action, nodes);
+  e->import_state = false;
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy(bot_key, e->d_mt.p, kMtN * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(pos, e->d_pos.p, 8, hipMemcpyDeviceToHost));
+  *bot_pos = pos[0];
+  if (!shared) {
+    HIP_TRY(hipMemcpy(eval_key, static_cast<uint32_t*>(e->d_mt.p) + kMtN, kMtN * 4,
+                      hipMemcpyDeviceToHost));
+    *eval_pos = pos[1];
+  }
+  return OS_OK;
+}
+
+int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
+                   int32_t* n, double* w, int32_t* action, int32_t* nchild,
+                   int8_t* out0) {
+  if (!e || !count) return Fail(OS_ERR_INVALID, "null argument");
+  if (r < 0 || r >= e->num_roots || r >= static_cast<int64_t>(e->last_results.size()))
+    return Fail(OS_ERR_INVALID, "root index out of range (fetch first)");
+  if (e->num_roots > e->chunk_roots)
+    return Fail(OS_ERR_UNSUPPORTED, "tree export needs a single-chunk run");
+  const uint32_t used = e->last_results[r].used;
+  *count = used;
+  if (!first) return OS_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  const size_t nb = e->node_bytes;
+  std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
+  HIP_TRY(hipMemcpy(raw.data(),
+                    static_cast<unsigned char*>(e->d_arena.p) +
+                        static_cast<size_t>(r) * e->cap * nb,
+                    raw.size(), hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < used; ++i) {
+    if (nb == sizeof(Node<int32_t>)) {
+      const Node<int32_t>& x = reinterpret_cast<const Node<int32_t>*>(raw.data())[i];
+      first[i] = x.first; n[i] = x.n; w[i] = x.w; action[i] = x.action;
+      nchild[i] = x.nchild; out0[i] = x.out;
+    } else {
+      const Node<double>& x = reinterpret_cast<const Node<double>*>(raw.data())[i];
+      first[i] = x.first; n[i] = x.n; w[i] = x.w; action[i] = x.action;
+      nchild[i] = x.nchild; out0[i] = x.out;
+    }
+  }
+  return OS_OK;
+}
+
+int os_rollouts_batch(os_engine* e, const int64_t* root_actions, int64_t n_actions,
+                      int64_t n, int32_t n_rollouts, const uint32_t* seeds,
+                      double* out_returns) {
+  if (!e || !seeds || !out_returns) return Fail(OS_ERR_INVALID, "null argument");
+  if (n_rollouts < 1) return Fail(OS_ERR_INVALID, "n_rollouts must be >= 1");
+  HIP_TRY(hipSetDevice(e->device));
+  HostState root;
+  std::string err;
+  if (!ReplayRoot(e->game, root_actions, n_actions, &root, &err))
+    return Fail(OS_ERR_INVALID, err);
+  if (n == 0) return OS_OK;
+  switch (e->game.cfg.kind) {
+    case kTicTacToe: return LaunchRollouts<TicTacToe>(e, root, n, n_rollouts, seeds, out_returns);
+    case kConnectFour: return LaunchRollouts<ConnectFour>(e, root, n, n_rollouts, seeds, out_returns);
+    case kBreakthrough: return LaunchRollouts<Breakthrough>(e, root, n, n_rollouts, seeds, out_returns);
+    case kHex: return LaunchRollouts<Hex>(e, root, n, n_rollouts, seeds, out_returns);
+    case kGo: return LaunchRollouts<Go>(e, root, n, n_rollouts, seeds, out_returns);
+  }
+  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+}
+
+int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base,
+                      int32_t max_plies, int64_t* actions, int64_t* offsets) {
+  if (!game || num_roots < 0 || max_plies < 0)
+    return Fail(OS_ERR_INVALID, "bad argument");
+  std::vector<int64_t> all;
+  std::vector<int64_t> offs(1, 0);
+  for (int64_t i = 0; i < num_roots; ++i) {
+    std::mt19937 g(seed_base + static_cast<uint32_t>(i));
+    HostState s;
+    s.game = &game->g;
+    StateInit(&s);
+    const uint32_t k = g() % static_cast<uint32_t>(max_plies + 1);
+    std::vector<int64_t> legal;
+    for (uint32_t j = 0; j < k; ++j) {
+      StateLegal(s, &legal);
+      const int64_t a = legal[g() % legal.size()];
+      HostState t = s;
+      StateApply(&t, a);
+      if (StateTerminal(t)) break;
+      s = t;
+    }
+    all.insert(all.end(), s.history.begin(), s.history.end());
+    offs.push_back(static_cast<int64_t>(all.size()));
+  }
+  if (actions) std::memcpy(actions, all.data(), all.size() * 8);
+  if (offsets) std::memcpy(offsets, offs.data(), offs.size() * 8);
+  return static_cast<int64_t>(all.size());
+}
+
+}  // extern "C"

@@ -1,0 +1,595 @@
+// Device-side (and host-side) state machines for the five target games, as
+// SoA bitboards.  One implementation per rule set, compiled for gfx950 (the
+// search kernel) and for the host (the pyspiel-compatible State API).
+//
+// Each game G provides, with S = G::State:
+//   init(S&, cfg)                       initial position
+//   terminal(const S&, cfg)             State::IsTerminal
+//   to_move(const S&)                   CurrentPlayer() for non-terminal S
+//   Legal legal(const S&, cfg, ctx)     LegalActions() as masks: .count, kth(k)
+//   apply(S&, cfg, ctx, action)         State::DoApplyAction
+//   ret0(const S&, cfg, ctx)            Returns()[0] at a terminal state
+// Legal actions enumerate in ascending action order, exactly as the
+// reference's LegalActions() (verified against the playthrough goldens).
+//
+// Reference rules restated:
+//   tic_tac_toe   open_spiel/games/tic_tac_toe.cc:80-150
+//   connect_four  open_spiel/games/connect_four.cc:85-185
+//   breakthrough  open_spiel/games/breakthrough.cc:119-320
+//   hex           open_spiel/games/hex.cc:55-255
+//   go            open_spiel/games/go.cc:124-216, go/go_board.cc:217-597
+#ifndef OS_GAMES_H_
+#define OS_GAMES_H_
+
+#include "os_common.h"
+
+namespace osm {
+
+enum GameKind : int32_t {
+  kTicTacToe = 0,
+  kConnectFour = 1,
+  kBreakthrough = 2,
+  kHex = 3,
+  kGo = 4,
+};
+
+// Runtime game parameters plus precomputed masks.  POD: copied by value into
+// kernels.
+struct GameCfg {
+  int32_t kind;
+  int32_t rows, cols;         // breakthrough rows/cols; hex/go: n x n
+  int32_t num_actions;        // NumDistinctActions()
+  int32_t max_children;       // upper bound on |LegalActions()|
+  int32_t max_game_length;    // MaxGameLength()
+  float komi;
+  int32_t handicap;
+  uint64_t board64, notcol0_64, notcollast_64;   // breakthrough (<= 64 cells)
+  B128 board, notcol0, notcollast;               // hex / go (<= 128 cells)
+};
+
+struct NoCtx {
+  OS_HD void reset() {}
+};
+
+// ----------------------------------------------------------------------------
+// tic_tac_toe: 3x3, bit = cell, x = player 0 first.
+struct TicTacToe {
+  struct State {
+    uint16_t b[2];
+    uint8_t to_play;
+    int8_t winner;  // -1 none
+    uint8_t moves;
+    uint8_t pad;
+    static constexpr bool kNeedsLog = false;
+  };
+  using Ctx = NoCtx;
+  struct Legal {
+    uint32_t mask;
+    int count;
+    OS_HD int kth(int k) const { return select64(mask, k); }
+  };
+  OS_HD static bool line(uint32_t b) {
+    const uint32_t L[8] = {0007, 0070, 0700, 0111, 0222, 0444, 0421, 0124};
+    bool r = false;
+    for (int i = 0; i < 8; ++i) r |= (b & L[i]) == L[i];
+    return r;
+  }
+  OS_HD static void init(State& s, const GameCfg&) {
+    s.b[0] = s.b[1] = 0; s.to_play = 0; s.winner = -1; s.moves = 0; s.pad = 0;
+  }
+  OS_HD static bool terminal(const State& s, const GameCfg&) {
+    return s.winner >= 0 || s.moves == 9;
+  }
+  OS_HD static int to_move(const State& s) { return s.to_play; }
+  OS_HD static Legal legal(const State& s, const GameCfg&, Ctx&) {
+    Legal l;
+    l.mask = 0x1FFu & ~(static_cast<uint32_t>(s.b[0]) | s.b[1]);
+    l.count = popc64(l.mask);
+    return l;
+  }
+  OS_HD static void apply(State& s, const GameCfg&, Ctx&, int a) {
+    const int p = s.to_play;
+    s.b[p] = static_cast<uint16_t>(s.b[p] | (1u << a));
+    if (line(s.b[p])) s.winner = static_cast<int8_t>(p);
+    s.to_play = static_cast<uint8_t>(1 - p);
+    s.moves++;
+  }
+  OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) {
+    return s.winner == 0 ? 1 : (s.winner == 1 ? -1 : 0);
+  }
+};
+
+// ----------------------------------------------------------------------------
+// connect_four: 6 rows x 7 cols, column-major bitboard, 7 bits per column
+// (6 cells + an always-empty sentinel), bit = col * 7 + row, row 0 = bottom.
+struct ConnectFour {
+  struct State {
+    uint64_t bb[2];
+    uint8_t to_play;
+    int8_t outcome;  // -1 unknown, 0/1 winner, 2 draw
+    uint8_t moves;
+    uint8_t pad[5];
+    static constexpr bool kNeedsLog = false;
+  };
+  using Ctx = NoCtx;
+  static constexpr uint64_t kTopRow = 0x20ull | (0x20ull << 7) | (0x20ull << 14) |
+                                      (0x20ull << 21) | (0x20ull << 28) |
+                                      (0x20ull << 35) | (0x20ull << 42);
+  struct Legal {
+    uint32_t mask;  // bit c = column c playable
+    int count;
+    OS_HD int kth(int k) const { return select64(mask, k); }
+  };
+  OS_HD static bool has_four(uint64_t b) {
+    uint64_t m = b & (b >> 1);
+    if (m & (m >> 2)) return true;
+    m = b & (b >> 7);
+    if (m & (m >> 14)) return true;
+    m = b & (b >> 6);
+    if (m & (m >> 12)) return true;
+    m = b & (b >> 8);
+    if (m & (m >> 16)) return true;
+    return false;
+  }
+  OS_HD static void init(State& s, const GameCfg&) {
+    s.bb[0] = s.bb[1] = 0; s.to_play = 0; s.outcome = -1; s.moves = 0;
+    for (int i = 0; i < 5; ++i) s.pad[i] = 0;
+  }
+  OS_HD static bool terminal(const State& s, const GameCfg&) { return s.outcome >= 0; }
+  OS_HD static int to_move(const State& s) { return s.to_play; }
+  OS_HD static Legal legal(const State& s, const GameCfg&, Ctx&) {
+    const uint64_t top = (s.bb[0] | s.bb[1]) & kTopRow;
+    uint32_t m = 0;
+    for (int c = 0; c < 7; ++c) m |= static_cast<uint32_t>(((top >> (7 * c + 5)) & 1) ^ 1) << c;
+    Legal l;
+    l.mask = m;
+    l.count = popc64(m);
+    return l;
+  }
+  OS_HD static void apply(State& s, const GameCfg&, Ctx&, int col) {
+    const int p = s.to_play;
+    const uint64_t occ = s.bb[0] | s.bb[1];
+    const uint64_t colmask = 0x3Full << (7 * col);
+    const uint64_t mv = (occ + (1ull << (7 * col))) & colmask;
+    s.bb[p] |= mv;
+    s.moves++;
+    if (has_four(s.bb[p])) s.outcome = static_cast<int8_t>(p);
+    else if (s.moves == 42) s.outcome = 2;
+    s.to_play = static_cast<uint8_t>(1 - p);
+  }
+  OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) {
+    return s.outcome == 0 ? 1 : (s.outcome == 1 ? -1 : 0);
+  }
+};
+
+// ----------------------------------------------------------------------------
+// breakthrough: rows x cols <= 64, bit = r * cols + c.  Black (player 0)
+// starts on rows 0-1 and moves +row; white on the last two rows, -row.
+// Action = ((r * cols + c) * 6 + dir) * 2 + capture (mixed base, as
+// spiel_utils.cc:45-73 RankActionMixedBase over {rows, cols, 6, 2}).
+struct Breakthrough {
+  struct State {
+    uint64_t pc[2];
+    uint8_t to_play;
+    int8_t winner;  // -1 none
+    uint16_t moves;
+    uint32_t pad;
+    static constexpr bool kNeedsLog = false;
+  };
+  using Ctx = NoCtx;
+  struct Legal {
+    uint64_t L, F, R;  // source squares with a legal left/forward/right move
+    int count;
+    int player;
+    OS_HD int cnt_below(int s) const {  // actions with source < s
+      const uint64_t pre = s >= 64 ? ~0ull : ((1ull << s) - 1);
+      return popc64(L & pre) + popc64(F & pre) + popc64(R & pre);
+    }
+    OS_HD int kth(int k) const {
+      int lo = 0;
+      for (int step = 32; step >= 1; step >>= 1)
+        if (cnt_below(lo + step) <= k) lo += step;
+      int rem = k - cnt_below(lo);
+      const uint64_t bit = 1ull << lo;
+      int o;
+      if (L & bit) { if (rem == 0) { o = 0; goto done; } --rem; }
+      if (F & bit) { if (rem == 0) { o = 1; goto done; } --rem; }
+      o = 2;
+    done:
+      return ((lo * 6 + player * 3 + o) << 1) | (o != 1 ? cap_bit(lo, o) : 0);
+    }
+    uint64_t opp;
+    int cols;
+    OS_HD int cap_bit(int src, int o) const {
+      int t = player == 0 ? src + cols + (o == 0 ? -1 : 1)
+                          : src - cols + (o == 0 ? -1 : 1);
+      return static_cast<int>((opp >> t) & 1);
+    }
+  };
+  OS_HD static void init(State& s, const GameCfg& g) {
+    const bool two = g.rows >= 6;
+    uint64_t black = 0, white = 0;
+    for (int c = 0; c < g.cols; ++c) {
+      black |= 1ull << c;
+      white |= 1ull << ((g.rows - 1) * g.cols + c);
+      if (two) {
+        black |= 1ull << (g.cols + c);
+        white |= 1ull << ((g.rows - 2) * g.cols + c);
+      }
+    }
+    s.pc[0] = black; s.pc[1] = white;
+    s.to_play = 0; s.winner = -1; s.moves = 0; s.pad = 0;
+  }
+  OS_HD static bool terminal(const State& s, const GameCfg&) {
+    return s.winner >= 0 || s.pc[0] == 0 || s.pc[1] == 0;
+  }
+  OS_HD static int to_move(const State& s) { return s.to_play; }
+  OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
+    const int p = s.to_play;
+    const uint64_t own = s.pc[p], opp = s.pc[1 - p];
+    const uint64_t E = g.board64 & ~(own | opp);
+    const uint64_t EO = E | opp;
+    const int c = g.cols;
+    Legal l;
+    if (p == 0) {
+      l.L = own & g.notcol0_64 & (EO >> (c - 1));
+      l.F = own & (E >> c);
+      l.R = own & g.notcollast_64 & (EO >> (c + 1));
+    } else {
+      l.L = own & g.notcol0_64 & (EO << (c + 1));
+      l.F = own & (E << c);
+      l.R = own & g.notcollast_64 & (EO << (c - 1));
+    }
+    l.count = popc64(l.L) + popc64(l.F) + popc64(l.R);
+    l.player = p;
+    l.opp = opp;
+    l.cols = c;
+    return l;
+  }
+  OS_HD static void apply(State& s, const GameCfg& g, Ctx&, int a) {
+    const int p = s.to_play;
+    const int sq = a >> 1;
+    const int dir = sq % 6;
+    const int src = sq / 6;
+    const int dr = dir < 3 ? 1 : -1;
+    const int dc = (dir % 3) - 1;
+    const int tgt = src + dr * g.cols + dc;
+    const uint64_t tb = 1ull << tgt;
+    s.pc[1 - p] &= ~tb;
+    s.pc[p] = (s.pc[p] & ~(1ull << src)) | tb;
+    const int trow = tgt / g.cols;
+    if (p == 0 && trow == g.rows - 1) s.winner = 0;
+    else if (p == 1 && trow == 0) s.winner = 1;
+    s.to_play = static_cast<uint8_t>(1 - p);
+    s.moves++;
+  }
+  OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) {
+    if (s.winner == 0 || s.pc[1] == 0) return 1;
+    if (s.winner == 1 || s.pc[0] == 0) return -1;
+    return 0;
+  }
+};
+
+// ----------------------------------------------------------------------------
+// Hex: n x n <= 128 cells, row-major, bit = cell.  Black (player 0) joins
+// north-south, white west-east.  Per player: stones, and the stones whose
+// group touches edge A (north / west) or edge B (south / east) -- the bitboard
+// form of the reference's per-cell edge labels (hex.cc:55-134, flood :149-184).
+struct Hex {
+  struct State {
+    B128 st[2];
+    B128 ea[2];
+    B128 eb[2];
+    int16_t win_cell;  // -1 none
+    int8_t result;     // +1 black won, -1 white won, 0 running
+    uint8_t to_play;
+    uint16_t moves;
+    uint16_t pad;
+    static constexpr bool kNeedsLog = false;
+  };
+  using Ctx = NoCtx;
+  struct Legal {
+    B128 mask;
+    int count;
+    OS_HD int kth(int k) const { return select128(mask, k); }
+  };
+  OS_HD static B128 nbr6(B128 x, const GameCfg& g) {
+    const int n = g.rows;
+    B128 r = shr(x, n) | (shr(x, n - 1) & g.notcol0) | (shr(x, 1) & g.notcollast) |
+             (shl(x, 1) & g.notcol0) | (shl(x, n - 1) & g.notcollast) | shl(x, n);
+    return r & g.board;
+  }
+  OS_HD static void init(State& s, const GameCfg&) {
+    for (int p = 0; p < 2; ++p) s.st[p] = s.ea[p] = s.eb[p] = b128(0, 0);
+    s.win_cell = -1; s.result = 0; s.to_play = 0; s.moves = 0; s.pad = 0;
+  }
+  OS_HD static bool terminal(const State& s, const GameCfg&) { return s.result != 0; }
+  OS_HD static int to_move(const State& s) { return s.to_play; }
+  OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
+    Legal l;
+    l.mask = g.board & ~(s.st[0] | s.st[1]);
+    l.count = popc(l.mask);
+    return l;
+  }
+  // Edge flags the stone would get if player p played cell m (hex.cc:55-134).
+  OS_HD static void edges_if(const State& s, const GameCfg& g, int p, int m,
+                             bool* a, bool* b) {
+    const int n = g.rows;
+    bool ea, eb;
+    if (p == 0) {
+      ea = m < n;
+      eb = !ea && m >= n * (n - 1);
+    } else {
+      ea = (m % n) == 0;
+      eb = !ea && (m % n) == n - 1;
+    }
+    const B128 nb = nbr6(bit128(m), g);
+    ea |= any(nb & s.ea[p]);
+    eb |= any(nb & s.eb[p]);
+    *a = ea;
+    *b = eb;
+  }
+  OS_HD static void apply(State& s, const GameCfg& g, Ctx&, int m) {
+    const int p = s.to_play;
+    bool a, b;
+    edges_if(s, g, p, m, &a, &b);
+    const B128 mb = bit128(m);
+    s.st[p] = s.st[p] | mb;
+    if (a && b) {
+      s.result = static_cast<int8_t>(p == 0 ? 1 : -1);
+      s.win_cell = static_cast<int16_t>(m);
+    } else if (a || b) {
+      const B128 plain = s.st[p] & ~s.ea[p] & ~s.eb[p];
+      B128 comp = mb;
+      for (;;) {
+        B128 nx = comp | (nbr6(comp, g) & plain);
+        if (nx == comp) break;
+        comp = nx;
+      }
+      if (a) s.ea[p] = s.ea[p] | comp;
+      else s.eb[p] = s.eb[p] | comp;
+    }
+    s.to_play = static_cast<uint8_t>(1 - p);
+    s.moves++;
+  }
+  OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) { return s.result; }
+};
+
+// ----------------------------------------------------------------------------
+// Go: n x n <= 121 cells (board_size <= 11), row-major bit = row * n + col
+// (the concrete OpenSpiel action id), pass = n * n.  Chains are recomputed by
+// bitboard flood fills instead of the reference's pseudo-liberty chain lists;
+// on n <= 11 the reference's `in_atari` test (go_board.h:208-212) is exact
+// (no u16/u32 wrap) and equals "exactly one distinct liberty", so legality is
+// identical.  Positional superko follows go.cc:199-208 with the same Zobrist
+// hashes (chess_common.h ZobristTable, seed 2765481) compared for equality.
+struct GoCtx {
+  const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
+  const uint64_t* base;    // hashes of positions before this search's root
+  int32_t n_base;
+  uint64_t* log;           // hashes added since the root (capacity cap)
+  int32_t n_log;
+  int32_t cap;
+  uint64_t filt[4];        // 256-bit membership pre-filter (bit = hash >> 56)
+  uint64_t base_filt[4];
+
+  OS_HD void reset() {
+    n_log = 0;
+    for (int i = 0; i < 4; ++i) filt[i] = base_filt[i];
+  }
+  OS_HD static int fbit(uint64_t h) { return static_cast<int>(h >> 56); }
+  OS_HD bool filter_has(uint64_t h) const {
+    const int b = fbit(h);
+    return (filt[b >> 6] >> (b & 63)) & 1;
+  }
+  OS_HD void filter_add(uint64_t h) {
+    const int b = fbit(h);
+    filt[b >> 6] |= 1ull << (b & 63);
+  }
+  OS_HD bool contains(uint64_t h) const {
+    if (!filter_has(h)) return false;
+    for (int i = 0; i < n_base; ++i)
+      if (base[i] == h) return true;
+    for (int i = 0; i < n_log; ++i)
+      if (log[i] == h) return true;
+    return false;
+  }
+  // Returns false if the position was already present (go.cc:201-205).
+  OS_HD bool insert(uint64_t h) {
+    if (contains(h)) return false;
+    if (n_log < cap) log[n_log++] = h;
+    filter_add(h);
+    return true;
+  }
+};
+
+struct Go {
+  struct State {
+    B128 bw[2];     // black, white stones
+    uint64_t hash;  // Zobrist hash of the stones
+    int16_t ko;     // ko cell or -1
+    uint16_t moves; // history length (since the empty board)
+    uint8_t to_play;
+    uint8_t flags;  // bit0 superko, bit1 last action pass, bit2 previous pass
+    uint16_t pad;
+    static constexpr bool kNeedsLog = true;
+  };
+  using Ctx = GoCtx;
+  static constexpr uint8_t kSuperko = 1, kLastPass = 2, kPrevPass = 4;
+
+  OS_HD static B128 nbr4(B128 x, const GameCfg& g) {
+    const int n = g.rows;
+    B128 r = shl(x, n) | shr(x, n) | (shl(x, 1) & g.notcol0) | (shr(x, 1) & g.notcollast);
+    return r & g.board;
+  }
+  OS_HD static B128 flood(B128 seed, B128 within, const GameCfg& g) {
+    B128 c = seed;
+    for (;;) {
+      B128 nx = (c | nbr4(c, g)) & within;
+      if (nx == c) return c;
+      c = nx;
+    }
+  }
+  // Whether empty cell p with no empty neighbour is a legal move for player c
+  // (go_board.cc:425-440).
+  OS_HD static bool surrounded_legal(const State& s, const GameCfg& g, int p, int c,
+                                     B128 E) {
+    const B128 own = s.bw[c], opp = s.bw[1 - c];
+    B128 nb = nbr4(bit128(p), g);
+    B128 on = nb & own;
+    while (any(on)) {  // joins an own chain that keeps a liberty
+      const int q = lowest(on);
+      const B128 ch = flood(bit128(q), own, g);
+      const B128 libs = nbr4(ch, g) & E;
+      if (popc(libs) >= 2) return true;
+      on = on & ~ch;
+    }
+    B128 opn = nb & opp;
+    while (any(opn)) {  // captures an opponent chain in atari
+      const int q = lowest(opn);
+      const B128 ch = flood(bit128(q), opp, g);
+      const B128 libs = nbr4(ch, g) & E;
+      if (popc(libs) == 1) return true;
+      opn = opn & ~ch;
+    }
+    return false;
+  }
+  struct Legal {
+    B128 mask;  // legal board points (pass excluded)
+    int count;  // including pass
+    int pass_action;
+    OS_HD int kth(int k) const {
+      const int c = count - 1;
+      return k < c ? select128(mask, k) : pass_action;
+    }
+  };
+  OS_HD static void init(State& s, const GameCfg&) {
+    s.bw[0] = s.bw[1] = b128(0, 0);
+    s.hash = 0; s.ko = -1; s.moves = 0; s.to_play = 0; s.flags = 0; s.pad = 0;
+  }
+  OS_HD static bool terminal(const State& s, const GameCfg& g) {
+    if (s.moves < 2) return false;
+    return s.moves >= g.max_game_length || (s.flags & kSuperko) ||
+           ((s.flags & kLastPass) && (s.flags & kPrevPass));
+  }
+  OS_HD static int to_move(const State& s) { return s.to_play; }
+  OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
+    const int c = s.to_play;
+    const B128 E = g.board & ~(s.bw[0] | s.bw[1]);
+    B128 cand = E;
+    if (s.ko >= 0) cand = cand & ~bit128(s.ko);
+    const B128 has_lib = nbr4(E, g);
+    B128 mask = cand & has_lib;
+    B128 hard = cand & ~has_lib;
+    while (any(hard)) {
+      const int p = lowest(hard);
+      hard = hard & ~bit128(p);
+      if (surrounded_legal(s, g, p, c, E)) mask = mask | bit128(p);
+    }
+    Legal l;
+    l.mask = mask;
+    l.count = popc(mask) + 1;
+    l.pass_action = g.rows * g.cols;
+    return l;
+  }
+  OS_HD static void apply(State& s, const GameCfg& g, Ctx& ctx, int a) {
+    const int c = s.to_play;
+    const int pass = g.rows * g.cols;
+    s.flags = static_cast<uint8_t>((s.flags & kSuperko) | ((s.flags & kLastPass) ? kPrevPass : 0));
+    if (a == pass) {
+      s.ko = -1;
+      s.flags |= kLastPass;
+      // Hash unchanged: the repetition insert is a no-op for a pass.
+    } else {
+      const B128 pb = bit128(a);
+      const B128 nb = nbr4(pb, g);
+      const B128 opp0 = s.bw[1 - c];
+      const bool enemy_eye = !any(nb & ~opp0);
+      s.bw[c] = s.bw[c] | pb;
+      s.hash ^= ctx.zob[2 * a + c];
+      B128 E = g.board & ~(s.bw[0] | s.bw[1]);
+      int captured = 0;
+      int cap_pt = -1;
+      B128 on = nb & s.bw[1 - c];
+      while (any(on)) {
+        const int q = lowest(on);
+        const B128 ch = flood(bit128(q), s.bw[1 - c], g);
+        on = on & ~ch;
+        if (!any(nbr4(ch, g) & E)) {
+          s.bw[1 - c] = s.bw[1 - c] & ~ch;
+          E = E | ch;
+          captured += popc(ch);
+          cap_pt = q;
+          B128 rem = ch;
+          while (any(rem)) {
+            const int x = lowest(rem);
+            rem = rem & ~bit128(x);
+            s.hash ^= ctx.zob[2 * x + (1 - c)];
+          }
+        }
+      }
+      s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
+      if (!ctx.insert(s.hash)) s.flags |= kSuperko;
+    }
+    s.to_play = static_cast<uint8_t>(1 - c);
+    s.moves++;
+  }
+  // Tromp-Taylor score with the reference's early-abort DFS
+  // (go_board.cc:526-597): neighbour order +row, +col, -col, -row; the
+  // "marked or reached both colours" test happens only on entry.
+  OS_HD static float score(const State& s, const GameCfg& g) {
+    const int n = g.rows;
+    const B128 E = g.board & ~(s.bw[0] | s.bw[1]);
+    int delta = popc(s.bw[0]) - popc(s.bw[1]);
+    B128 marked = b128(0, 0);
+    uint8_t st_pt[128];
+    uint8_t st_d[128];
+    B128 todo = E;
+    while (any(todo)) {
+      const int p0 = lowest(todo);
+      todo = todo & ~bit128(p0);
+      if (test(marked, p0)) continue;
+      bool rb = false, rw = false;
+      int num = 1;
+      int sp = 0;
+      marked = marked | bit128(p0);
+      st_pt[0] = static_cast<uint8_t>(p0);
+      st_d[0] = 0;
+      sp = 1;
+      while (sp > 0 && !(rb && rw)) {
+        const int p = st_pt[sp - 1];
+        const int d = st_d[sp - 1];
+        if (d == 4) { --sp; continue; }
+        st_d[sp - 1] = static_cast<uint8_t>(d + 1);
+        const int r = p / n, cc = p % n;
+        int q;
+        if (d == 0) { if (r + 1 >= n) continue; q = p + n; }
+        else if (d == 1) { if (cc + 1 >= n) continue; q = p + 1; }
+        else if (d == 2) { if (cc - 1 < 0) continue; q = p - 1; }
+        else { if (r - 1 < 0) continue; q = p - n; }
+        if (test(s.bw[0], q)) { rb = true; continue; }
+        if (test(s.bw[1], q)) { rw = true; continue; }
+        if (test(marked, q)) continue;
+        marked = marked | bit128(q);
+        ++num;
+        st_pt[sp] = static_cast<uint8_t>(q);
+        st_d[sp] = 0;
+        ++sp;
+      }
+      if (rb && !rw) delta += num;
+      else if (!rb && rw) delta -= num;
+    }
+    float sc = static_cast<float>(delta) - g.komi;
+    if (g.handicap >= 2) sc -= static_cast<float>(g.handicap);
+    return sc;
+  }
+  OS_HD static int ret0(const State& s, const GameCfg& g, Ctx&) {
+    if (s.flags & kSuperko) return 0;
+    const float sc = score(s, g);
+    return sc > 0 ? 1 : (sc < 0 ? -1 : 0);
+  }
+};
+
+}  // namespace osm
+
+#endif  // OS_GAMES_H_

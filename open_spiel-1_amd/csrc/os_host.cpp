@@ -1,0 +1,530 @@
+// Host-side game loading, State API and string formatting for libos_mcts.so.
+// The rule logic itself is the shared host/device code in os_games.h.
+//
+// String formats restate the reference's ToString / ActionToString:
+//   tic_tac_toe.cc:94-99,:128-138; connect_four.cc:106-110,:160-169;
+//   breakthrough.cc:168-189,:247-266; hex.cc:189-196,:227-243;
+//   go.cc:133-144 + go_board.cc:478-506.
+#include "os_host.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <random>
+#include <sstream>
+
+namespace osm {
+namespace {
+
+bool ParseGameString(const std::string& s, std::string* name,
+                     std::map<std::string, std::string>* kv) {
+  size_t lp = s.find('(');
+  if (lp == std::string::npos) {
+    *name = s;
+    return !s.empty();
+  }
+  if (s.back() != ')') return false;
+  *name = s.substr(0, lp);
+  std::string body = s.substr(lp + 1, s.size() - lp - 2);
+  size_t pos = 0;
+  while (pos < body.size()) {
+    size_t comma = body.find(',', pos);
+    if (comma == std::string::npos) comma = body.size();
+    std::string item = body.substr(pos, comma - pos);
+    size_t eq = item.find('=');
+    if (eq == std::string::npos) return false;
+    (*kv)[item.substr(0, eq)] = item.substr(eq + 1);
+    pos = comma + 1;
+  }
+  return true;
+}
+
+bool GetInt(const std::map<std::string, std::string>& kv, const char* k,
+            int dflt, int* out) {
+  auto it = kv.find(k);
+  if (it == kv.end()) {
+    *out = dflt;
+    return true;
+  }
+  char* end = nullptr;
+  long v = std::strtol(it->second.c_str(), &end, 10);
+  if (end == it->second.c_str() || *end) return false;
+  *out = static_cast<int>(v);
+  return true;
+}
+
+bool GetDouble(const std::map<std::string, std::string>& kv, const char* k,
+               double dflt, double* out) {
+  auto it = kv.find(k);
+  if (it == kv.end()) {
+    *out = dflt;
+    return true;
+  }
+  char* end = nullptr;
+  double v = std::strtod(it->second.c_str(), &end);
+  if (end == it->second.c_str() || *end) return false;
+  *out = v;
+  return true;
+}
+
+void SquareMasks(int n, GameCfg* c) {
+  c->board = lowmask128(n * n);
+  B128 col0 = b128(0, 0), coll = b128(0, 0);
+  for (int r = 0; r < n; ++r) {
+    col0 = col0 | bit128(r * n);
+    coll = coll | bit128(r * n + n - 1);
+  }
+  c->notcol0 = c->board & ~col0;
+  c->notcollast = c->board & ~coll;
+}
+
+std::string FormatDouble(double v) {
+  std::ostringstream ss;
+  ss << v;
+  return ss.str();
+}
+
+template <class G>
+typename G::State& St(HostState& s) {
+  return *reinterpret_cast<typename G::State*>(s.raw);
+}
+template <class G>
+const typename G::State& St(const HostState& s) {
+  return *reinterpret_cast<const typename G::State*>(s.raw);
+}
+
+}  // namespace
+
+std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) {
+  *unsupported = false;
+  std::string name;
+  std::map<std::string, std::string> kv;
+  if (!ParseGameString(gs, &name, &kv)) return "cannot parse game string '" + gs + "'";
+  GameCfg c;
+  std::memset(&c, 0, sizeof c);
+  auto reject_unknown = [&](std::initializer_list<const char*> allowed) -> std::string {
+    for (auto& it : kv) {
+      bool ok = false;
+      for (const char* a : allowed) ok |= it.first == a;
+      if (!ok) return "unknown parameter '" + it.first + "' for game " + name;
+    }
+    return "";
+  };
+  if (name == "tic_tac_toe") {
+    std::string e = reject_unknown({});
+    if (!e.empty()) return e;
+    c.kind = kTicTacToe;
+    c.rows = c.cols = 3;
+    c.num_actions = 9;
+    c.max_children = 9;
+    c.max_game_length = 9;
+    g->canonical = "tic_tac_toe()";
+    g->state_bytes = sizeof(TicTacToe::State);
+  } else if (name == "connect_four") {
+    std::string e = reject_unknown({});
+    if (!e.empty()) return e;
+    c.kind = kConnectFour;
+    c.rows = 6;
+    c.cols = 7;
+    c.num_actions = 7;
+    c.max_children = 7;
+    c.max_game_length = 42;
+    g->canonical = "connect_four()";
+    g->state_bytes = sizeof(ConnectFour::State);
+  } else if (name == "breakthrough") {
+    std::string e = reject_unknown({"rows", "columns"});
+    if (!e.empty()) return e;
+    int rows, cols;
+    if (!GetInt(kv, "rows", 8, &rows) || !GetInt(kv, "columns", 8, &cols))
+      return "bad breakthrough parameter";
+    if (rows < 2 || cols < 2) return "breakthrough needs rows, columns >= 2";
+    if (rows * cols > 64) {
+      *unsupported = true;
+      return "breakthrough boards above 64 cells are not supported by this engine";
+    }
+    c.kind = kBreakthrough;
+    c.rows = rows;
+    c.cols = cols;
+    c.num_actions = rows * cols * 6 * 2;
+    c.max_game_length = 2 * (2 * rows - 3) * cols + 1;
+    c.max_children = 3 * cols * (rows >= 6 ? 2 : 1);
+    uint64_t board = rows * cols == 64 ? ~0ull : ((1ull << (rows * cols)) - 1);
+    uint64_t col0 = 0, coll = 0;
+    for (int r = 0; r < rows; ++r) {
+      col0 |= 1ull << (r * cols);
+      coll |= 1ull << (r * cols + cols - 1);
+    }
+    c.board64 = board;
+    c.notcol0_64 = board & ~col0;
+    c.notcollast_64 = board & ~coll;
+    g->canonical = (rows == 8 && cols == 8 && kv.empty())
+                       ? "breakthrough()"
+                       : "breakthrough(columns=" + std::to_string(cols) +
+                             ",rows=" + std::to_string(rows) + ")";
+    g->state_bytes = sizeof(Breakthrough::State);
+  } else if (name == "hex") {
+    std::string e = reject_unknown({"board_size"});
+    if (!e.empty()) return e;
+    int n;
+    if (!GetInt(kv, "board_size", 11, &n)) return "bad hex board_size";
+    if (n < 2 || n > 11) {
+      *unsupported = true;
+      return "hex board_size must be in [2, 11] for this engine";
+    }
+    c.kind = kHex;
+    c.rows = c.cols = n;
+    c.num_actions = n * n;
+    c.max_children = n * n;
+    c.max_game_length = n * n;
+    SquareMasks(n, &c);
+    g->canonical = kv.empty() ? "hex()" : "hex(board_size=" + std::to_string(n) + ")";
+    g->state_bytes = sizeof(Hex::State);
+  } else if (name == "go") {
+    std::string e = reject_unknown({"board_size", "komi", "handicap"});
+    if (!e.empty()) return e;
+    int n, handicap;
+    double komi;
+    if (!GetInt(kv, "board_size", 19, &n) || !GetInt(kv, "handicap", 0, &handicap) ||
+        !GetDouble(kv, "komi", 7.5, &komi))
+      return "bad go parameter";
+    if (n < 2 || n > 11) {
+      *unsupported = true;
+      return "go board_size must be in [2, 11] for this engine";
+    }
+    if (handicap >= 2) {
+      *unsupported = true;
+      return "go handicap stones (19x19 placement) are not supported by this engine";
+    }
+    c.kind = kGo;
+    c.rows = c.cols = n;
+    c.num_actions = n * n + 1;
+    c.max_children = n * n + 1;
+    c.max_game_length = 2 * n * n;
+    c.komi = static_cast<float>(komi);
+    c.handicap = handicap;
+    SquareMasks(n, &c);
+    // chess_common.h:113-154 ZobristTable<uint64_t, 441, 2>(seed 2765481),
+    // indexed by virtual point (r + 1) * 21 + (c + 1) (go_board.cc:289-299).
+    std::vector<uint64_t> vz(441 * 2);
+    std::mt19937_64 outer(2765481);
+    for (int i = 0; i < 441; ++i) {
+      std::mt19937_64 inner(outer());
+      vz[2 * i] = inner();
+      vz[2 * i + 1] = inner();
+    }
+    g->zob.assign(static_cast<size_t>(n) * n * 2, 0);
+    for (int r = 0; r < n; ++r)
+      for (int col = 0; col < n; ++col) {
+        int vp = (r + 1) * 21 + col + 1;
+        g->zob[2 * (r * n + col)] = vz[2 * vp];
+        g->zob[2 * (r * n + col) + 1] = vz[2 * vp + 1];
+      }
+    std::string canon = "go(";
+    bool first = true;
+    auto add = [&](const std::string& k, const std::string& v) {
+      canon += (first ? "" : ",") + k + "=" + v;
+      first = false;
+    };
+    for (auto& it : kv) {
+      if (it.first == "board_size") add("board_size", std::to_string(n));
+      else if (it.first == "komi") add("komi", FormatDouble(komi));
+      else if (it.first == "handicap") add("handicap", std::to_string(handicap));
+    }
+    g->canonical = canon + ")";
+    g->state_bytes = sizeof(Go::State);
+  } else {
+    *unsupported = true;
+    return "game '" + name + "' is not supported by this engine (supported: "
+           "tic_tac_toe, connect_four, breakthrough, hex, go)";
+  }
+  g->cfg = c;
+  g->name = name;
+  return "";
+}
+
+GoCtx HostGoCtx(const HostState& s, std::vector<uint64_t>* storage) {
+  GoCtx ctx;
+  std::memset(&ctx, 0, sizeof ctx);
+  const int cap = s.game->cfg.max_game_length + 4;
+  storage->assign(s.hashes.begin(), s.hashes.end());
+  storage->resize(cap);
+  ctx.zob = s.game->zob.data();
+  ctx.base = nullptr;
+  ctx.n_base = 0;
+  ctx.log = storage->data();
+  ctx.n_log = static_cast<int32_t>(s.hashes.size());
+  ctx.cap = cap;
+  for (size_t i = 0; i < s.hashes.size(); ++i) ctx.filter_add(s.hashes[i]);
+  for (int i = 0; i < 4; ++i) ctx.base_filt[i] = 0;
+  return ctx;
+}
+
+void StateInit(HostState* s) {
+  std::memset(s->raw, 0, sizeof s->raw);
+  s->history.clear();
+  s->hashes.clear();
+  const GameCfg& g = s->game->cfg;
+  switch (g.kind) {
+    case kTicTacToe: TicTacToe::init(St<TicTacToe>(*s), g); break;
+    case kConnectFour: ConnectFour::init(St<ConnectFour>(*s), g); break;
+    case kBreakthrough: Breakthrough::init(St<Breakthrough>(*s), g); break;
+    case kHex: Hex::init(St<Hex>(*s), g); break;
+    case kGo:
+      Go::init(St<Go>(*s), g);
+      s->hashes.push_back(St<Go>(*s).hash);  // go.cc:218-224 ResetBoard
+      break;
+  }
+}
+
+bool StateTerminal(const HostState& s) {
+  const GameCfg& g = s.game->cfg;
+  switch (g.kind) {
+    case kTicTacToe: return TicTacToe::terminal(St<TicTacToe>(s), g);
+    case kConnectFour: return ConnectFour::terminal(St<ConnectFour>(s), g);
+    case kBreakthrough: return Breakthrough::terminal(St<Breakthrough>(s), g);
+    case kHex: return Hex::terminal(St<Hex>(s), g);
+    case kGo: return Go::terminal(St<Go>(s), g);
+  }
+  return true;
+}
+
+int StateCurrentPlayer(const HostState& s) {
+  if (StateTerminal(s)) return -4;
+  switch (s.game->cfg.kind) {
+    case kTicTacToe: return TicTacToe::to_move(St<TicTacToe>(s));
+    case kConnectFour: return ConnectFour::to_move(St<ConnectFour>(s));
+    case kBreakthrough: return Breakthrough::to_move(St<Breakthrough>(s));
+    case kHex: return Hex::to_move(St<Hex>(s));
+    case kGo: return Go::to_move(St<Go>(s));
+  }
+  return -4;
+}
+
+namespace {
+template <class G>
+void LegalOf(const HostState& s, typename G::Ctx& ctx, std::vector<int64_t>* out) {
+  const typename G::Legal l = G::legal(St<G>(s), s.game->cfg, ctx);
+  for (int k = 0; k < l.count; ++k) out->push_back(l.kth(k));
+}
+}  // namespace
+
+void StateLegal(const HostState& s, std::vector<int64_t>* out) {
+  out->clear();
+  if (StateTerminal(s)) return;
+  NoCtx nc;
+  switch (s.game->cfg.kind) {
+    case kTicTacToe: LegalOf<TicTacToe>(s, nc, out); break;
+    case kConnectFour: LegalOf<ConnectFour>(s, nc, out); break;
+    case kBreakthrough: LegalOf<Breakthrough>(s, nc, out); break;
+    case kHex: LegalOf<Hex>(s, nc, out); break;
+    case kGo: {
+      std::vector<uint64_t> storage;
+      GoCtx ctx = HostGoCtx(s, &storage);
+      LegalOf<Go>(s, ctx, out);
+      break;
+    }
+  }
+}
+
+bool StateApply(HostState* s, int64_t a) {
+  std::vector<int64_t> legal;
+  StateLegal(*s, &legal);
+  bool ok = false;
+  for (int64_t x : legal) ok |= x == a;
+  if (!ok) return false;
+  const GameCfg& g = s->game->cfg;
+  NoCtx nc;
+  const int ai = static_cast<int>(a);
+  switch (g.kind) {
+    case kTicTacToe: TicTacToe::apply(St<TicTacToe>(*s), g, nc, ai); break;
+    case kConnectFour: ConnectFour::apply(St<ConnectFour>(*s), g, nc, ai); break;
+    case kBreakthrough: Breakthrough::apply(St<Breakthrough>(*s), g, nc, ai); break;
+    case kHex: Hex::apply(St<Hex>(*s), g, nc, ai); break;
+    case kGo: {
+      std::vector<uint64_t> storage;
+      GoCtx ctx = HostGoCtx(*s, &storage);
+      Go::apply(St<Go>(*s), g, ctx, ai);
+      s->hashes.assign(storage.begin(), storage.begin() + ctx.n_log);
+      break;
+    }
+  }
+  s->history.push_back(a);
+  return true;
+}
+
+void StateReturns(const HostState& s, double* r) {
+  r[0] = r[1] = 0.0;
+  if (!StateTerminal(s)) return;
+  const GameCfg& g = s.game->cfg;
+  NoCtx nc;
+  int r0 = 0;
+  switch (g.kind) {
+    case kTicTacToe: r0 = TicTacToe::ret0(St<TicTacToe>(s), g, nc); break;
+    case kConnectFour: r0 = ConnectFour::ret0(St<ConnectFour>(s), g, nc); break;
+    case kBreakthrough: r0 = Breakthrough::ret0(St<Breakthrough>(s), g, nc); break;
+    case kHex: r0 = Hex::ret0(St<Hex>(s), g, nc); break;
+    case kGo: {
+      std::vector<uint64_t> storage;
+      GoCtx ctx = HostGoCtx(s, &storage);
+      r0 = Go::ret0(St<Go>(s), g, ctx);
+      break;
+    }
+  }
+  r[0] = static_cast<double>(r0);
+  r[1] = static_cast<double>(-r0);
+}
+
+namespace {
+
+std::string TttString(const TicTacToe::State& s) {
+  std::string out;
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) {
+      int i = r * 3 + c;
+      out += (s.b[0] >> i) & 1 ? "x" : ((s.b[1] >> i) & 1 ? "o" : ".");
+    }
+    if (r < 2) out += "\n";
+  }
+  return out;
+}
+
+std::string C4String(const ConnectFour::State& s) {
+  std::string out;
+  for (int r = 5; r >= 0; --r) {
+    for (int c = 0; c < 7; ++c) {
+      int i = c * 7 + r;
+      out += (s.bb[0] >> i) & 1 ? "x" : ((s.bb[1] >> i) & 1 ? "o" : ".");
+    }
+    out += "\n";
+  }
+  return out;
+}
+
+std::string BtString(const Breakthrough::State& s, const GameCfg& g) {
+  std::string out;
+  for (int r = 0; r < g.rows; ++r) {
+    out += static_cast<char>('1' + (g.rows - 1 - r));
+    for (int c = 0; c < g.cols; ++c) {
+      int i = r * g.cols + c;
+      out += (s.pc[0] >> i) & 1 ? "b" : ((s.pc[1] >> i) & 1 ? "w" : ".");
+    }
+    out += "\n";
+  }
+  out += " ";
+  for (int c = 0; c < g.cols; ++c) out += static_cast<char>('a' + c);
+  out += "\n";
+  return out;
+}
+
+char HexCellChar(const Hex::State& s, int i) {
+  if (test(s.st[0], i)) {
+    if (s.win_cell == i) return 'X';
+    if (test(s.ea[0], i)) return 'y';
+    if (test(s.eb[0], i)) return 'z';
+    return 'x';
+  }
+  if (test(s.st[1], i)) {
+    if (s.win_cell == i) return 'O';
+    if (test(s.ea[1], i)) return 'p';
+    if (test(s.eb[1], i)) return 'q';
+    return 'o';
+  }
+  return '.';
+}
+
+std::string HexString(const Hex::State& s, const GameCfg& g) {
+  const int n = g.rows;
+  std::string out;
+  int line = 0;
+  for (int c = 0; c < n * n; ++c) {
+    if (c && !(c % n)) {
+      out += "\n";
+      ++line;
+      out += std::string(line, ' ');
+    }
+    out += HexCellChar(s, c);
+    out += " ";
+  }
+  return out;
+}
+
+std::string GoString(const Go::State& s, const GameCfg& g, size_t hist) {
+  std::ostringstream ss;
+  ss << "GoState(komi=" << g.komi << ", to_play=" << (s.to_play == 0 ? "B" : "W")
+     << ", history.size()=" << hist << ")\n";
+  ss << "\n";
+  const int n = g.rows;
+  for (int r = n - 1; r >= 0; --r) {
+    char buf[16];
+    std::snprintf(buf, sizeof buf, "%2d ", r + 1);
+    ss << buf;
+    for (int c = 0; c < n; ++c) {
+      int i = r * n + c;
+      ss << (test(s.bw[0], i) ? 'X' : (test(s.bw[1], i) ? 'O' : '+'));
+    }
+    ss << "\n";
+  }
+  std::string cols = "ABCDEFGHJKLMNOPQRST";
+  ss << "   " << cols.substr(0, n) << "\n";
+  return ss.str();
+}
+
+}  // namespace
+
+std::string StateToString(const HostState& s) {
+  const GameCfg& g = s.game->cfg;
+  switch (g.kind) {
+    case kTicTacToe: return TttString(St<TicTacToe>(s));
+    case kConnectFour: return C4String(St<ConnectFour>(s));
+    case kBreakthrough: return BtString(St<Breakthrough>(s), g);
+    case kHex: return HexString(St<Hex>(s), g);
+    case kGo: return GoString(St<Go>(s), g, s.history.size());
+  }
+  return "";
+}
+
+std::string StateActionToString(const HostState& s, int player, int64_t a) {
+  const GameCfg& g = s.game->cfg;
+  switch (g.kind) {
+    case kTicTacToe:
+      return std::string(player == 0 ? "x" : "o") + "(" + std::to_string(a / 3) +
+             "," + std::to_string(a % 3) + ")";
+    case kConnectFour:
+      return std::string(player == 0 ? "x" : "o") + std::to_string(a);
+    case kBreakthrough: {
+      const int cap = static_cast<int>(a & 1);
+      const int sq = static_cast<int>(a >> 1);
+      const int dir = sq % 6, src = sq / 6;
+      const int r1 = src / g.cols, c1 = src % g.cols;
+      const int r2 = r1 + (dir < 3 ? 1 : -1), c2 = c1 + (dir % 3) - 1;
+      std::string out;
+      out += static_cast<char>('a' + c1);
+      out += static_cast<char>('1' + (g.rows - 1 - r1));
+      out += static_cast<char>('a' + c2);
+      out += static_cast<char>('1' + (g.rows - 1 - r2));
+      if (cap) out += "*";
+      return out;
+    }
+    case kHex: {
+      const Hex::State& hs = St<Hex>(s);
+      bool ea, eb;
+      Hex::edges_if(hs, g, player, static_cast<int>(a), &ea, &eb);
+      char ch;
+      if (player == 0) ch = ea && eb ? 'X' : (ea ? 'y' : (eb ? 'z' : 'x'));
+      else ch = ea && eb ? 'O' : (ea ? 'p' : (eb ? 'q' : 'o'));
+      return std::string(1, ch) + "(" + std::to_string(a % g.rows) + "," +
+             std::to_string(a / g.rows) + ")";
+    }
+    case kGo: {
+      std::string out = player == 0 ? "B " : "W ";
+      if (a == g.rows * g.cols) return out + "PASS";
+      const int r = static_cast<int>(a / g.rows), c = static_cast<int>(a % g.rows);
+      char col = static_cast<char>('a' + c);
+      if (col >= 'i') ++col;
+      return out + std::string(1, col) + std::to_string(r + 1);
+    }
+  }
+  return "";
+}
+
+}  // namespace osm

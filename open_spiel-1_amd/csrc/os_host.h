@@ -1,0 +1,52 @@
+// Host-side game objects shared by the State API and the engine launcher.
+#ifndef OS_HOST_H_
+#define OS_HOST_H_
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "os_games.h"
+
+namespace osm {
+
+// Largest device state record (Hex: 6 x B128 + scalars).
+constexpr int kStateBytes = 112;
+
+struct HostGame {
+  GameCfg cfg;
+  std::string name;          // short name
+  std::string canonical;     // canonical game string
+  std::vector<uint64_t> zob; // go: [n*n][2]
+  int state_bytes = 0;
+};
+
+struct HostState {
+  const HostGame* game;
+  alignas(16) unsigned char raw[kStateBytes];
+  std::vector<int64_t> history;
+  std::vector<uint64_t> hashes;  // go: positions seen, incl. the initial one
+};
+
+// Parses and validates a game string; returns "" on success, else a message.
+// `unsupported` is set when the game/parameters are valid OpenSpiel but not
+// supported by this engine.
+std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported);
+
+void StateInit(HostState* s);
+bool StateTerminal(const HostState& s);
+int StateCurrentPlayer(const HostState& s);
+void StateLegal(const HostState& s, std::vector<int64_t>* out);
+// Returns false if the action is illegal.
+bool StateApply(HostState* s, int64_t a);
+void StateReturns(const HostState& s, double* r);
+std::string StateToString(const HostState& s);
+std::string StateActionToString(const HostState& s, int player, int64_t a);
+
+// Fills the go context for host-side use (all hashes in `log`).
+GoCtx HostGoCtx(const HostState& s, std::vector<uint64_t>* storage);
+
+}  // namespace osm
+
+#endif  // OS_HOST_H_

@@ -1,0 +1,320 @@
+// UCT MCTS with MCTS-Solver backup and random rollouts over a flat node
+// arena: the single-search engine that the gfx950 kernel runs once per lane.
+//
+// Restates open_spiel/algorithms/mcts.cc (C++ bot: MCTSBot::MCTSearch
+// :325-428, ApplyTreePolicy :255-323, UCTValue :89-100, RandomRolloutEvaluator
+// ::Evaluate :42-71, GarbageCollect :430-443) and, under kPolicyNumpy, the
+// Python twin open_spiel/python/algorithms/mcts.py:292-443 (one shared numpy
+// RandomState, no single-child early stop, no GC).
+//
+// Tree layout: node 0 is the root; the children of a node are one contiguous
+// block [first, first + nchild) in expansion (shuffled) order.  A node's
+// player is implied by its depth (all five games strictly alternate turns):
+// depth 0 -> root player P0, depth d >= 1 -> P0 ^ ((d - 1) & 1).
+// Outcomes (the reference's `outcome` vector) are stored as the player-0
+// value in {-1, 0, +1}; all five games are two-player zero-sum with returns
+// (r, -r), so outcome[p] = p == 0 ? r : -r.  kUnsolved marks an empty vector.
+#ifndef OS_MCTS_H_
+#define OS_MCTS_H_
+
+#include "os_common.h"
+#include "os_games.h"
+#include "os_rng.h"
+
+namespace osm {
+
+constexpr int8_t kUnsolved = 2;
+constexpr int kPolicyCpp = 0;     // mcts.cc: bot rng + evaluator rng
+constexpr int kPolicyNumpy = 1;   // mcts.py: one shared RandomState
+constexpr int kMaxPath = 256;     // > every supported MaxGameLength
+constexpr int kMaxChildren = 128; // >= every supported |LegalActions|
+
+enum SearchStatus : int32_t {
+  kOk = 0,
+  kArenaOverflow = 1,   // node arena capacity exceeded
+  kPathOverflow = 2,    // tree depth exceeded kMaxPath
+  kGcStackOverflow = 3, // no arena space left for the GC traversal stack
+};
+
+template <class R>
+struct Node {
+  uint32_t first;   // first child index (valid iff nchild > 0)
+  int32_t n;        // explore_count
+  R w;              // total_reward (int32 when n_rollouts == 1: exact)
+  uint16_t action;
+  uint8_t nchild;
+  int8_t out;       // player-0 outcome, or kUnsolved
+};
+
+struct SearchParams {
+  double uct_c;
+  int32_t max_simulations;
+  int32_t n_rollouts;
+  int32_t solve;
+  int32_t max_nodes;        // (max_memory_mb << 20) / sizeof(SearchNode) + 1
+  int32_t policy;           // kPolicyCpp / kPolicyNumpy
+  int32_t pad;
+  const double* log_lut;    // log(N), N in [0, max_simulations], host libm
+};
+
+struct SearchResult {
+  int32_t status;
+  int32_t sims;     // simulations run (== root explore_count)
+  int32_t nodes;    // the reference's nodes_ counter at exit
+  uint32_t used;    // arena slots used
+  int32_t gc_runs;
+  int32_t max_depth;
+};
+
+OS_HD double outcome_for(int8_t out0, int player) {
+  return static_cast<double>(player == 0 ? out0 : -out0);
+}
+
+// mcts.cc:113-123 CompareFinal(a, b) == "a < b".
+template <class R>
+OS_HD bool final_less(const Node<R>& a, int pa, const Node<R>& b, int pb) {
+  const double oa = a.out == kUnsolved ? 0.0 : outcome_for(a.out, pa);
+  const double ob = b.out == kUnsolved ? 0.0 : outcome_for(b.out, pb);
+  if (oa != ob) return oa < ob;
+  if (a.n != b.n) return a.n < b.n;
+  return static_cast<double>(a.w) < static_cast<double>(b.w);
+}
+
+// Index (within the root's children) of BestChild(): std::max_element keeps
+// the first maximum (mcts.cc:125-141; mcts.py:160-162 max() likewise).
+template <class R>
+OS_HD int best_child(const Node<R>* nodes, int child_player) {
+  const Node<R>& root = nodes[0];
+  if (root.nchild == 0) return -1;
+  int best = 0;
+  for (int k = 1; k < root.nchild; ++k)
+    if (final_less(nodes[root.first + best], child_player, nodes[root.first + k],
+                   child_player))
+      best = k;
+  return best;
+}
+
+// One random playout to the end (mcts.cc:46-55 / mcts.py:62-70).
+template <class G, int Policy, class Rng>
+OS_HD int rollout_ret0(typename G::State s, const GameCfg& g, typename G::Ctx& ctx,
+                       Rng& ev) {
+  while (!G::terminal(s, g)) {
+    const typename G::Legal l = G::legal(s, g, ctx);
+    const uint32_t k = Policy == kPolicyCpp
+                           ? AbslUniform(ev, static_cast<uint32_t>(l.count))
+                           : NpChoice(ev, static_cast<uint32_t>(l.count));
+    G::apply(s, g, ctx, l.kth(static_cast<int>(k)));
+  }
+  return G::ret0(s, g, ctx);
+}
+
+template <class R>
+struct RewardOps;
+template <>
+struct RewardOps<int32_t> {
+  OS_HD static int32_t from(int r0, int, int) { return r0; }
+};
+
+// GarbageCollect (mcts.cc:430-443): every node with children whose
+// explore_count < limit loses them; nodes_ drops by the capacity of every
+// such block, including blocks under an already-cleared ancestor (the
+// reference recurses before clearing).  Traversal order does not change the
+// result.  The DFS stack lives in the unused arena tail.
+template <class R>
+OS_HD int garbage_collect(Node<R>* nodes, uint32_t used, uint32_t cap, int limit,
+                          int* nodes_count) {
+  uint32_t* stack = reinterpret_cast<uint32_t*>(nodes + used);
+  const uint64_t stack_cap =
+      (static_cast<uint64_t>(cap - used) * sizeof(Node<R>)) / sizeof(uint32_t);
+  uint64_t sp = 0;
+  if (stack_cap < 1) return kGcStackOverflow;
+  stack[sp++] = 0;
+  while (sp > 0) {
+    const uint32_t x = stack[--sp];
+    Node<R>& nx = nodes[x];
+    const int nc = nx.nchild;
+    if (nc == 0) continue;
+    if (sp + nc > stack_cap) return kGcStackOverflow;
+    for (int k = 0; k < nc; ++k) stack[sp++] = nx.first + k;
+    if (nx.n < limit) {
+      *nodes_count -= nc;
+      nx.nchild = 0;
+    }
+  }
+  return kOk;
+}
+
+// One complete search from `root`.  `bot` and `ev` are the two MT19937
+// streams (the same object under kPolicyNumpy).  `actbuf` holds >=
+// kMaxChildren entries, `path` >= kMaxPath.
+template <class G, class R, int Policy, class Rng>
+OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
+                               const typename G::State& root,
+                               typename G::Ctx& ctx, Node<R>* nodes,
+                               uint32_t cap, Rng& bot, Rng& ev, uint32_t* path,
+                               uint16_t* actbuf) {
+  SearchResult res;
+  res.status = kOk;
+  res.sims = 0;
+  res.gc_runs = 0;
+  res.max_depth = 0;
+  const int P0 = G::to_move(root);
+  nodes[0].first = 0;
+  nodes[0].n = 0;
+  nodes[0].w = 0;
+  nodes[0].action = 0;
+  nodes[0].nchild = 0;
+  nodes[0].out = kUnsolved;
+  uint32_t used = 1;
+  int nodes_count = 1;
+  int gc_limit = 5;
+  const double inf = __builtin_huge_val();
+
+  for (int sim = 0; sim < sp.max_simulations; ++sim) {
+    typename G::State s = root;
+    ctx.reset();
+    uint32_t cur = 0;
+    int depth = 0;
+    path[0] = 0;
+    // ---- selection / expansion (ApplyTreePolicy) ----
+    while (!G::terminal(s, g) && nodes[cur].n > 0) {
+      if (nodes[cur].nchild == 0) {
+        const typename G::Legal l = G::legal(s, g, ctx);
+        const int nc = l.count;
+        for (int k = 0; k < nc; ++k) actbuf[k] = static_cast<uint16_t>(l.kth(k));
+        if (Policy == kPolicyCpp) CppShuffle(actbuf, nc, bot);
+        else NpShuffle(actbuf, nc, bot);
+        if (used + static_cast<uint32_t>(nc) > cap) {
+          res.status = kArenaOverflow;
+          goto done;
+        }
+        const uint32_t first = used;
+        used += nc;
+        for (int k = 0; k < nc; ++k) {
+          Node<R>& c = nodes[first + k];
+          c.first = 0;
+          c.n = 0;
+          c.w = 0;
+          c.action = actbuf[k];
+          c.nchild = 0;
+          c.out = kUnsolved;
+        }
+        nodes[cur].first = first;
+        nodes[cur].nchild = static_cast<uint8_t>(nc);
+        nodes_count += nc;
+      }
+      const Node<R>& pn = nodes[cur];
+      const int cp = P0 ^ (depth & 1);  // player choosing at this node
+      const double logN = sp.log_lut[pn.n];
+      double best = -inf;
+      int chosen = 0;
+      for (int k = 0; k < pn.nchild; ++k) {
+        const Node<R>& c = nodes[pn.first + k];
+        double v;
+        if (c.out != kUnsolved) {
+          v = outcome_for(c.out, cp);
+        } else if (c.n == 0) {
+          v = inf;
+        } else {
+          const double dn = static_cast<double>(c.n);
+          v = static_cast<double>(c.w) / dn + sp.uct_c * __builtin_sqrt(logN / dn);
+        }
+        if (v > best) {
+          best = v;
+          chosen = k;
+        }
+      }
+      const uint32_t nxt = pn.first + chosen;
+      G::apply(s, g, ctx, nodes[nxt].action);
+      cur = nxt;
+      if (++depth >= kMaxPath) {
+        res.status = kPathOverflow;
+        goto done;
+      }
+      path[depth] = cur;
+    }
+    if (depth > res.max_depth) res.max_depth = depth;
+    // ---- evaluation ----
+    {
+      bool solved;
+      R rv0, rv1;
+      if (G::terminal(s, g)) {
+        const int r0 = G::ret0(s, g, ctx);
+        nodes[cur].out = static_cast<int8_t>(r0);
+        solved = sp.solve != 0;
+        rv0 = static_cast<R>(r0);
+        rv1 = static_cast<R>(-r0);
+      } else {
+        solved = false;
+        if (sp.n_rollouts == 1) {
+          const int r0 = rollout_ret0<G, Policy>(s, g, ctx, ev);
+          rv0 = static_cast<R>(r0);
+          rv1 = static_cast<R>(-r0);
+        } else {
+          double s0 = 0.0, s1 = 0.0;
+          for (int k = 0; k < sp.n_rollouts; ++k) {
+            const int r0 = rollout_ret0<G, Policy>(s, g, ctx, ev);
+            s0 += static_cast<double>(r0);
+            s1 += static_cast<double>(-r0);
+          }
+          rv0 = static_cast<R>(s0 / sp.n_rollouts);
+          rv1 = static_cast<R>(s1 / sp.n_rollouts);
+        }
+      }
+      // ---- backup + MCTS-Solver (mcts.cc:351-396) ----
+      for (int d = depth; d >= 0; --d) {
+        Node<R>& nd = nodes[path[d]];
+        const int pl = d == 0 ? P0 : (P0 ^ ((d - 1) & 1));
+        nd.w += pl == 0 ? rv0 : rv1;
+        nd.n += 1;
+        if (solved && nd.nchild > 0) {
+          const int cpl = P0 ^ (d & 1);
+          int best = -1;
+          double bestv = 0.0;
+          bool all_solved = true;
+          for (int k = 0; k < nd.nchild; ++k) {
+            const Node<R>& c = nodes[nd.first + k];
+            if (c.out == kUnsolved) {
+              all_solved = false;
+            } else {
+              const double v = outcome_for(c.out, cpl);
+              if (best < 0 || v > bestv) {
+                best = k;
+                bestv = v;
+              }
+            }
+          }
+          if (best >= 0 && (all_solved || bestv == 1.0)) {
+            nd.out = nodes[nd.first + best].out;
+          } else {
+            solved = false;
+          }
+        }
+      }
+    }
+    res.sims = sim + 1;
+    if (nodes[0].out != kUnsolved) break;
+    if (Policy == kPolicyCpp) {
+      if (nodes[0].nchild == 1) break;
+      if (sp.max_nodes > 1 && nodes_count >= sp.max_nodes) {
+        const int st = garbage_collect(nodes, used, cap, gc_limit, &nodes_count);
+        if (st != kOk) {
+          res.status = st;
+          goto done;
+        }
+        res.gc_runs++;
+        gc_limit = static_cast<int>(gc_limit *
+                                    (nodes_count > sp.max_nodes / 2 ? 1.25 : 0.9));
+        if (gc_limit < 5) gc_limit = 5;
+      }
+    }
+  }
+done:
+  res.nodes = nodes_count;
+  res.used = used;
+  return res;
+}
+
+}  // namespace osm
+
+#endif  // OS_MCTS_H_

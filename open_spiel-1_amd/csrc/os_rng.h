@@ -1,0 +1,183 @@
+// Bit-exact random-number consumption of the reference MCTS path, for host and
+// gfx950:
+//   * std::mt19937 streams (mcts.h:105 evaluator rng_, mcts.h:205 bot rng_),
+//     seeded with init_genrand (== numpy RandomState legacy seeding);
+//   * absl::Uniform(rng_, 0u, actions.size())    (mcts.cc:53)   -> AbslUniform
+//   * std::shuffle(legal_actions, rng_), libstdc++ 11 (mcts.cc:275) -> CppShuffle
+//   * numpy RandomState.choice / .shuffle (python/algorithms/mcts.py:69, :320)
+//
+// The MT19937 state (624 words) lives in caller memory (HBM arena on the
+// device, a plain array on the host).  Twisting is done lazily, one word at a
+// time, in place: producing word i of a new block needs old s[i], old s[i+1]
+// and s[(i+397) mod 624], which is new exactly when the standard generator
+// uses the new value, so the output sequence is identical to std::mt19937.
+#ifndef OS_RNG_H_
+#define OS_RNG_H_
+
+#include "os_common.h"
+
+namespace osm {
+
+constexpr int kMtN = 624;
+constexpr int kMtM = 397;
+
+OS_HD void mt_seed(uint32_t* s, uint32_t seed) {
+  s[0] = seed;
+  for (int i = 1; i < kMtN; ++i)
+    s[i] = 1812433253u * (s[i - 1] ^ (s[i - 1] >> 30)) + static_cast<uint32_t>(i);
+}
+
+// A 32-bit MT19937 stream over externally owned state.
+struct MtStream {
+  uint32_t* s;
+  int idx;  // next word index within the current block; kMtN => new block
+  int pre;  // 1: the current block is already fully twisted (numpy import)
+
+  OS_HD uint32_t next() {
+    if (idx >= kMtN) {
+      idx = 0;
+      pre = 0;
+    }
+    const int i = idx;
+    if (pre) {
+      idx = i + 1;
+      return temper(s[i]);
+    }
+    const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+    const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+    uint32_t y = (s[i] & 0x80000000u) | (s[i1] & 0x7fffffffu);
+    uint32_t v = s[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    s[i] = v;
+    idx = i + 1;
+    return temper(v);
+  }
+  OS_HD static uint32_t temper(uint32_t v) {
+    v ^= v >> 11;
+    v ^= (v << 7) & 0x9d2c5680u;
+    v ^= (v << 15) & 0xefc60000u;
+    v ^= v >> 18;
+    return v;
+  }
+  // Brings the state to numpy's (key, pos) form: the whole current block
+  // twisted, `idx` words of it consumed.
+  OS_HD void finalize() {
+    if (pre || idx >= kMtN) return;
+    for (int i = idx; i < kMtN; ++i) {
+      const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+      const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+      const uint32_t y = (s[i] & 0x80000000u) | (s[i1] & 0x7fffffffu);
+      s[i] = s[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    pre = 1;
+  }
+};
+
+OS_HD uint64_t umulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return static_cast<uint64_t>((static_cast<unsigned __int128>(a) * b) >> 64);
+#endif
+}
+
+// absl::Uniform(g, 0u, n) for a 32-bit URBG with a 64-bit result type
+// (abseil 20200225 uniform_int_distribution<uint64>::Generate over
+// FastUniformBits<uint64>: two words, first in the high half; Lemire 64x64
+// with rejection).  n >= 1.
+template <class G>
+OS_HD uint32_t AbslUniform(G& g, uint32_t n) {
+  uint64_t hi = g.next();
+  uint64_t lo = g.next();
+  uint64_t bits = (hi << 32) | lo;
+  const uint64_t R = static_cast<uint64_t>(n) - 1;
+  if ((R & static_cast<uint64_t>(n)) == 0) return static_cast<uint32_t>(bits & R);
+  uint64_t plo = bits * n;
+  uint64_t phi = umulhi64(bits, n);
+  if (plo < n) {
+    const uint64_t thr = (0ull - static_cast<uint64_t>(n)) % n;
+    while (plo < thr) {
+      hi = g.next();
+      lo = g.next();
+      bits = (hi << 32) | lo;
+      plo = bits * n;
+      phi = umulhi64(bits, n);
+    }
+  }
+  return static_cast<uint32_t>(phi);
+}
+
+// libstdc++ uniform_int_distribution downscaling (_S_nd, Lemire 32x32->64).
+template <class G>
+OS_HD uint32_t Lemire32(G& g, uint32_t m) {
+  uint64_t p = static_cast<uint64_t>(g.next()) * m;
+  uint32_t low = static_cast<uint32_t>(p);
+  if (low < m) {
+    const uint32_t thr = (0u - m) % m;
+    while (low < thr) {
+      p = static_cast<uint64_t>(g.next()) * m;
+      low = static_cast<uint32_t>(p);
+    }
+  }
+  return static_cast<uint32_t>(p >> 32);
+}
+
+// std::shuffle from libstdc++ 11 (bits/stl_algo.h, "pair" path valid for
+// n <= 65535 with a 32-bit URBG).  T is any swappable element type.
+template <class T, class G>
+OS_HD void CppShuffle(T* a, int n, G& g) {
+  if (n <= 1) return;
+  int i = 1;
+  if ((n & 1) == 0) {
+    uint32_t j = Lemire32(g, 2u);
+    T t = a[1]; a[1] = a[j]; a[j] = t;
+    i = 2;
+  }
+  while (i != n) {
+    const uint32_t b0 = static_cast<uint32_t>(i) + 1u;
+    const uint32_t b1 = b0 + 1u;
+    const uint32_t x = Lemire32(g, b0 * b1);
+    const uint32_t p0 = x / b1, p1 = x % b1;
+    T t = a[i]; a[i] = a[p0]; a[p0] = t;
+    t = a[i + 1]; a[i + 1] = a[p1]; a[p1] = t;
+    i += 2;
+  }
+}
+
+OS_HD uint32_t np_mask(uint32_t m) {
+  m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
+  return m;
+}
+
+// numpy legacy random_interval(max) (32-bit masked rejection).
+template <class G>
+OS_HD uint32_t NpRandomInterval(G& g, uint32_t max) {
+  if (max == 0) return 0;
+  const uint32_t mask = np_mask(max);
+  uint32_t v;
+  do { v = g.next() & mask; } while (v > max);
+  return v;
+}
+
+// numpy legacy RandomState.choice(seq of n) -> index (no draw when n == 1).
+template <class G>
+OS_HD uint32_t NpChoice(G& g, uint32_t n) {
+  const uint32_t rng = n - 1;
+  if (rng == 0) return 0;
+  const uint32_t mask = np_mask(rng);
+  uint32_t v;
+  do { v = g.next() & mask; } while (v > rng);
+  return v;
+}
+
+// numpy RandomState.shuffle(list): Fisher-Yates from the end.
+template <class T, class G>
+OS_HD void NpShuffle(T* a, int n, G& g) {
+  for (int i = n - 1; i >= 1; --i) {
+    uint32_t j = NpRandomInterval(g, static_cast<uint32_t>(i));
+    T t = a[i]; a[i] = a[j]; a[j] = t;
+  }
+}
+
+}  // namespace osm
+
+#endif  // OS_RNG_H_

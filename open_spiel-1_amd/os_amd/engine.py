@@ -1,0 +1,208 @@
+"""Batched MCTS engine on one MI355X (gfx950): Python face of libos_mcts.so.
+
+`Engine(game_string, device)` replaces a population of the reference's
+`algorithms::MCTSBot` + `RandomRolloutEvaluator` pairs
+(open_spiel/algorithms/mcts.h:92-159): `mcts_batch` runs one independent
+`MCTSBot::MCTSearch` (mcts.cc:325-428) per root on the GPU, one lane per
+search, bit-exact with the reference for the same seeds.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+OUTPUT_KEYS = ("child_action", "child_n", "child_w", "child_out", "nchild",
+               "root_n", "root_w", "root_out", "best_action", "nodes")
+UNSOLVED = 2
+
+
+def make_params(uct_c=2.0, max_simulations=1000, n_rollouts=1,
+                max_memory_mb=1000, solve=True, policy=_lib.POLICY_CPP,
+                block_size=0, arena_nodes=0):
+  p = _lib.MctsParams()
+  p.uct_c = float(uct_c)
+  p.max_simulations = int(max_simulations)
+  p.n_rollouts = int(n_rollouts)
+  p.max_memory_mb = int(max_memory_mb)
+  p.solve = 1 if solve else 0
+  p.policy = int(policy)
+  p.block_size = int(block_size)
+  p.arena_nodes = int(arena_nodes)
+  return p
+
+
+def _alloc_outputs(R, mc):
+  return dict(
+      child_action=np.zeros((R, mc), np.int32),
+      child_n=np.zeros((R, mc), np.int32),
+      child_w=np.zeros((R, mc), np.float64),
+      child_out=np.zeros((R, mc), np.int8),
+      nchild=np.zeros(R, np.int32),
+      root_n=np.zeros(R, np.int32),
+      root_w=np.zeros(R, np.float64),
+      root_out=np.zeros(R, np.int8),
+      best_action=np.zeros(R, np.int64),
+      nodes=np.zeros(R, np.int32))
+
+
+def _out_ptrs(o):
+  return [ptr(o[k]) for k in OUTPUT_KEYS]
+
+
+def roots_from_histories(histories):
+  """[[a0, a1, ...], ...] -> (actions int64[], offsets int64[R+1])."""
+  offs = np.zeros(len(histories) + 1, np.int64)
+  for i, h in enumerate(histories):
+    offs[i + 1] = offs[i] + len(h)
+  acts = np.zeros(int(offs[-1]), np.int64)
+  for i, h in enumerate(histories):
+    acts[offs[i]:offs[i + 1]] = h
+  return acts, offs
+
+
+class Engine:
+  """One engine per device (C-ABI os_engine)."""
+
+  def __init__(self, game_string, device=0):
+    h = ctypes.c_void_p()
+    check(lib.os_engine_create(game_string.encode(), int(device), ctypes.byref(h)))
+    self._h = h
+    self.game_string = game_string
+    self.device = device
+    g = ctypes.c_void_p()
+    check(lib.os_game_load(game_string.encode(), ctypes.byref(g)))
+    info = _lib.GameInfo()
+    check(lib.os_game_get_info(g, ctypes.byref(info)))
+    lib.os_game_free(g)
+    self.num_distinct_actions = info.num_distinct_actions
+    self.max_children = info.max_children
+    self.max_game_length = info.max_game_length
+
+  def close(self):
+    if getattr(self, "_h", None) and self._h.value:
+      lib.os_engine_destroy(self._h)
+      self._h = ctypes.c_void_p()
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:  # interpreter shutdown
+      pass
+
+  def mcts_batch(self, root_actions, root_offsets, bot_seeds, eval_seeds=None,
+                 **params):
+    """Independent searches; returns dict of numpy arrays (child order)."""
+    p = make_params(**params)
+    acts = _lib.i64(root_actions)
+    offs = _lib.i64(root_offsets)
+    R = len(offs) - 1
+    bs = _lib.u32(bot_seeds)
+    es = _lib.u32(eval_seeds if eval_seeds is not None else bot_seeds)
+    assert len(bs) == R and len(es) == R
+    mc = self.max_children
+    o = _alloc_outputs(R, mc)
+    check(lib.os_mcts_batch(self._h, ctypes.byref(p), R, ptr(acts), ptr(offs),
+                            ptr(bs), ptr(es), mc, *_out_ptrs(o)))
+    return o
+
+  def mcts_numpy_state(self, history, bot_state, eval_state=None, **params):
+    """python/algorithms/mcts.py search driven by numpy RandomState states.
+
+    bot_state / eval_state: (key uint32[624], pos) pairs, updated in place
+    semantics returned as new tuples.  eval_state None => one shared stream.
+    """
+    params = dict(params)
+    params["policy"] = _lib.POLICY_NUMPY
+    p = make_params(**params)
+    acts = _lib.i64(history)
+    bkey = np.array(bot_state[0], dtype=np.uint32).copy()
+    bpos = np.array([bot_state[1]], dtype=np.int32)
+    shared = eval_state is None
+    if shared:
+      ekey, epos = None, None
+    else:
+      ekey = np.array(eval_state[0], dtype=np.uint32).copy()
+      epos = np.array([eval_state[1]], dtype=np.int32)
+    mc = self.max_children
+    o = _alloc_outputs(1, mc)
+    check(lib.os_mcts_numpy_state(self._h, ctypes.byref(p), ptr(acts), len(acts),
+                                  1 if shared else 0, ptr(bkey), ptr(bpos),
+                                  ptr(ekey), ptr(epos), mc, *_out_ptrs(o)))
+    new_eval = None if shared else (ekey, int(epos[0]))
+    return o, (bkey, int(bpos[0])), new_eval
+
+  def tree(self, r=0):
+    """Flat tree of root r of the last search: dict of node arrays."""
+    cnt = ctypes.c_int64()
+    check(lib.os_engine_tree(self._h, r, ctypes.addressof(cnt), None, None, None,
+                             None, None, None))
+    n = cnt.value
+    t = dict(first=np.zeros(n, np.uint32), n=np.zeros(n, np.int32),
+             w=np.zeros(n, np.float64), action=np.zeros(n, np.int32),
+             nchild=np.zeros(n, np.int32), out0=np.zeros(n, np.int8))
+    check(lib.os_engine_tree(self._h, r, ctypes.addressof(cnt), ptr(t["first"]),
+                             ptr(t["n"]), ptr(t["w"]), ptr(t["action"]),
+                             ptr(t["nchild"]), ptr(t["out0"])))
+    return t
+
+  def rollouts(self, history, seeds, n_rollouts=1):
+    """RandomRolloutEvaluator(n_rollouts, seed).Evaluate(root) per seed."""
+    acts = _lib.i64(history)
+    s = _lib.u32(seeds)
+    out = np.zeros((len(s), 2), np.float64)
+    check(lib.os_rollouts_batch(self._h, ptr(acts), len(acts), len(s),
+                                int(n_rollouts), ptr(s), ptr(out)))
+    return out
+
+  # ---- device-resident pipeline (bench) ----
+  def prepare(self, root_actions, root_offsets, bot_seeds, eval_seeds=None,
+              **params):
+    self._prep_params = make_params(**params)
+    self._prep = (_lib.i64(root_actions), _lib.i64(root_offsets),
+                  _lib.u32(bot_seeds),
+                  _lib.u32(eval_seeds if eval_seeds is not None else bot_seeds))
+    acts, offs, bs, es = self._prep
+    self._prep_R = len(offs) - 1
+    check(lib.os_engine_prepare(self._h, ctypes.byref(self._prep_params),
+                                self._prep_R, ptr(acts), ptr(offs), ptr(bs),
+                                ptr(es)))
+
+  def run_async(self, stream=None):
+    """Launches the search kernel(s) on a hipStream_t (int handle) or NULL."""
+    check(lib.os_engine_run_async(self._h, stream))
+
+  def fetch(self):
+    o = _alloc_outputs(self._prep_R, self.max_children)
+    check(lib.os_engine_fetch(self._h, self.max_children, *_out_ptrs(o)))
+    return o
+
+  def last_sims(self):
+    return int(lib.os_engine_last_sims(self._h))
+
+
+def make_roots(game_string, num_roots, seed_base=1000, max_plies=8):
+  """Benchmark roots: see os_make_roots in include/os_mcts.h."""
+  g = ctypes.c_void_p()
+  check(lib.os_game_load(game_string.encode(), ctypes.byref(g)))
+  try:
+    total = lib.os_make_roots(g, num_roots, seed_base, max_plies, None, None)
+    if total < 0:
+      check(int(total))
+    acts = np.zeros(max(int(total), 1), np.int64)
+    offs = np.zeros(num_roots + 1, np.int64)
+    lib.os_make_roots(g, num_roots, seed_base, max_plies, ptr(acts), ptr(offs))
+    return acts[:int(total)].copy(), offs
+  finally:
+    lib.os_game_free(g)
+
+
+def action_indexed_visits(out, num_actions):
+  """[R][A] visit counts from child-ordered outputs (root-parallel reduce)."""
+  R = out["nchild"].shape[0]
+  v = np.zeros((R, num_actions), np.int64)
+  for r in range(R):
+    nc = out["nchild"][r]
+    np.add.at(v[r], out["child_action"][r, :nc], out["child_n"][r, :nc])
+  return v

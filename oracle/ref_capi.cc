@@ -58,6 +58,12 @@ void FillOut(const SearchNode& root, int max_children, int64_t r,
              const SearchStats& st, const RootOut& o) {
   int nc = static_cast<int>(root.children.size());
   o.nchild[r] = nc;
+  for (int k = nc; k < max_children; ++k) {  // padding, as the C-ABI fills it
+    o.child_action[r * max_children + k] = -1;
+    o.child_n[r * max_children + k] = 0;
+    o.child_w[r * max_children + k] = 0.0;
+    o.child_out[r * max_children + k] = 2;
+  }
   for (int k = 0; k < nc && k < max_children; ++k) {
     const SearchNode& c = root.children[k];
     o.child_action[r * max_children + k] = static_cast<int32_t>(c.action);

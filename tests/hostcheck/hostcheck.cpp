@@ -1,0 +1,206 @@
+// TEST INFRASTRUCTURE ONLY — the product's search engine (csrc/os_mcts.h) and
+// game state machines compiled for the host CPU with g++, so the CPU test
+// suite can check the exact engine logic the gfx950 kernel runs against the
+// oracle without a GPU.  Never shipped, never used by bench.py or the C-ABI.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "os_host.h"
+#include "os_mcts.h"
+
+using namespace osm;
+
+namespace {
+thread_local std::string g_err;
+
+template <class G, class R, int Policy>
+int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
+           uint32_t bot_seed, uint32_t eval_seed, uint32_t cap, int32_t max_children,
+           int32_t* child_action, int32_t* child_n, double* child_w,
+           int8_t* child_out, int32_t* nchild, int32_t* root_n, double* root_w,
+           int8_t* root_out, int64_t* best_action, int32_t* nodes_out) {
+  std::vector<Node<R>> nodes(cap);
+  std::vector<uint32_t> mt(2 * kMtN);
+  MtStream bot{mt.data(), kMtN, 0}, ev{mt.data() + kMtN, kMtN, 0};
+  mt_seed(bot.s, bot_seed);
+  mt_seed(ev.s, eval_seed);
+  uint32_t path[kMaxPath];
+  uint16_t actbuf[kMaxChildren];
+  typename G::Ctx ctx;
+  std::vector<uint64_t> storage;
+  std::vector<uint64_t> logbuf(256);
+  if constexpr (G::State::kNeedsLog) {
+    std::memset(&ctx, 0, sizeof ctx);
+    ctx.zob = game.zob.data();
+    ctx.base = root.hashes.data();
+    ctx.n_base = static_cast<int32_t>(root.hashes.size());
+    ctx.log = logbuf.data();
+    ctx.cap = 256;
+    for (uint64_t h : root.hashes) {
+      const int b = GoCtx::fbit(h);
+      ctx.base_filt[b >> 6] |= 1ull << (b & 63);
+    }
+  }
+  const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
+  SearchResult res = mcts_search<G, R, Policy>(game.cfg, sp, rs, ctx, nodes.data(), cap,
+                                               bot, ev, path, actbuf);
+  if (res.status != kOk) {
+    g_err = "search status " + std::to_string(res.status);
+    return -4;
+  }
+  const int P0 = G::to_move(rs);
+  const Node<R>& rn = nodes[0];
+  *nchild = rn.nchild;
+  for (int k = 0; k < rn.nchild && k < max_children; ++k) {
+    const Node<R>& c = nodes[rn.first + k];
+    child_action[k] = c.action;
+    child_n[k] = c.n;
+    child_w[k] = static_cast<double>(c.w);
+    child_out[k] = c.out == kUnsolved ? kUnsolved : (P0 == 0 ? c.out : -c.out);
+  }
+  *root_n = rn.n;
+  *root_w = static_cast<double>(rn.w);
+  *root_out = rn.out == kUnsolved ? kUnsolved : (P0 == 0 ? rn.out : -rn.out);
+  const int b = best_child(nodes.data(), P0);
+  *best_action = b < 0 ? -1 : nodes[rn.first + b].action;
+  *nodes_out = res.nodes;
+  return 0;
+}
+
+template <class G>
+int Dispatch(const HostGame& game, const HostState& root, const SearchParams& sp,
+             int policy, uint32_t bs, uint32_t es, uint32_t cap, int32_t mc, int32_t* ca,
+             int32_t* cn, double* cw, int8_t* co, int32_t* nch, int32_t* rn,
+             double* rw, int8_t* ro, int64_t* ba, int32_t* nd) {
+  if (sp.n_rollouts == 1) {
+    if (policy == kPolicyCpp)
+      return RunOne<G, int32_t, kPolicyCpp>(game, root, sp, bs, es, cap, mc, ca, cn, cw,
+                                            co, nch, rn, rw, ro, ba, nd);
+    return RunOne<G, int32_t, kPolicyNumpy>(game, root, sp, bs, es, cap, mc, ca, cn, cw,
+                                            co, nch, rn, rw, ro, ba, nd);
+  }
+  if (policy == kPolicyCpp)
+    return RunOne<G, double, kPolicyCpp>(game, root, sp, bs, es, cap, mc, ca, cn, cw, co,
+                                         nch, rn, rw, ro, ba, nd);
+  return RunOne<G, double, kPolicyNumpy>(game, root, sp, bs, es, cap, mc, ca, cn, cw, co,
+                                         nch, rn, rw, ro, ba, nd);
+}
+}  // namespace
+
+extern "C" {
+
+const char* hc_last_error() { return g_err.c_str(); }
+
+// Same output layout as oref_mcts_batch.
+int hc_mcts_batch(const char* game_string, int64_t num_roots,
+                  const int64_t* root_actions, const int64_t* root_offsets,
+                  double uct_c, int32_t max_simulations, int32_t n_rollouts,
+                  int64_t max_memory_mb, int32_t solve, int32_t policy,
+                  const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                  int32_t max_children, int32_t* child_action, int32_t* child_n,
+                  double* child_w, int8_t* child_out, int32_t* nchild,
+                  int32_t* root_n, double* root_w, int8_t* root_out,
+                  int64_t* best_action, int32_t* nodes) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty()) {
+    g_err = err;
+    return -1;
+  }
+  std::vector<double> lut(max_simulations + 2);
+  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  SearchParams sp;
+  std::memset(&sp, 0, sizeof sp);
+  sp.uct_c = uct_c;
+  sp.max_simulations = max_simulations;
+  sp.n_rollouts = n_rollouts;
+  sp.solve = solve;
+  sp.max_nodes = static_cast<int32_t>((max_memory_mb << 20) / 80 + 1);
+  sp.policy = policy;
+  sp.log_lut = lut.data();
+  const uint32_t cap = 1 + static_cast<uint32_t>(max_simulations) * game.cfg.max_children;
+  for (int64_t r = 0; r < num_roots; ++r) {
+    HostState hs;
+    hs.game = &game;
+    StateInit(&hs);
+    for (int64_t i = root_offsets[r]; i < root_offsets[r + 1]; ++i) {
+      if (!StateApply(&hs, root_actions[i])) {
+        g_err = "illegal root action";
+        return -1;
+      }
+    }
+    const int64_t o = r * max_children;
+    int rc = 0;
+    const uint32_t es = eval_seeds[r], bs = bot_seeds[r];
+    switch (game.cfg.kind) {
+#define HC_CASE(K, G)                                                              \
+  case K:                                                                          \
+    rc = Dispatch<G>(game, hs, sp, policy, bs, es, cap, max_children,              \
+                     child_action + o, child_n + o, child_w + o, child_out + o,    \
+                     nchild + r, root_n + r, root_w + r, root_out + r,             \
+                     best_action + r, nodes + r);                                  \
+    break;
+      HC_CASE(kTicTacToe, TicTacToe)
+      HC_CASE(kConnectFour, ConnectFour)
+      HC_CASE(kBreakthrough, Breakthrough)
+      HC_CASE(kHex, Hex)
+      HC_CASE(kGo, Go)
+#undef HC_CASE
+    }
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// Product rollouts on the host: RandomRolloutEvaluator::Evaluate per seed.
+int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actions,
+                int64_t n, const uint32_t* seeds, double* out) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty()) {
+    g_err = err;
+    return -1;
+  }
+  HostState hs;
+  hs.game = &game;
+  StateInit(&hs);
+  for (int64_t i = 0; i < n_actions; ++i) StateApply(&hs, actions[i]);
+  std::vector<uint32_t> mt(kMtN);
+  std::vector<uint64_t> logbuf(256);
+  for (int64_t i = 0; i < n; ++i) {
+    MtStream ev{mt.data(), kMtN, 0};
+    mt_seed(ev.s, seeds[i]);
+    int r0 = 0;
+    switch (game.cfg.kind) {
+      case kTicTacToe: { NoCtx c; r0 = rollout_ret0<TicTacToe, kPolicyCpp>(*reinterpret_cast<TicTacToe::State*>(hs.raw), game.cfg, c, ev); break; }
+      case kConnectFour: { NoCtx c; r0 = rollout_ret0<ConnectFour, kPolicyCpp>(*reinterpret_cast<ConnectFour::State*>(hs.raw), game.cfg, c, ev); break; }
+      case kBreakthrough: { NoCtx c; r0 = rollout_ret0<Breakthrough, kPolicyCpp>(*reinterpret_cast<Breakthrough::State*>(hs.raw), game.cfg, c, ev); break; }
+      case kHex: { NoCtx c; r0 = rollout_ret0<Hex, kPolicyCpp>(*reinterpret_cast<Hex::State*>(hs.raw), game.cfg, c, ev); break; }
+      case kGo: {
+        GoCtx c;
+        std::memset(&c, 0, sizeof c);
+        c.zob = game.zob.data();
+        c.base = hs.hashes.data();
+        c.n_base = static_cast<int32_t>(hs.hashes.size());
+        c.log = logbuf.data();
+        c.cap = 256;
+        for (uint64_t h : hs.hashes) {
+          const int b = GoCtx::fbit(h);
+          c.base_filt[b >> 6] |= 1ull << (b & 63);
+        }
+        c.reset();
+        r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg, c, ev);
+        break;
+      }
+    }
+    out[2 * i] = r0;
+    out[2 * i + 1] = -r0;
+  }
+  return 0;
+}
+
+}  // extern "C"
