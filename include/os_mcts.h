@@ -109,7 +109,7 @@ typedef struct {
  * root, bot seed bot_seeds[r], evaluator seed eval_seeds[r].  Bit-exact with
  * the reference given the same seeds.  Under OS_POLICY_NUMPY the two seeds
  * seed numpy-style streams (equal seeds => the test's shared RandomState is
- * NOT modelled; use os_mcts_numpy_state for a shared stream). */
+ * NOT modelled; use os_mcts_stateful for a shared stream). */
 int os_mcts_batch(os_engine* e, const os_mcts_params* p, int64_t num_roots,
                   const int64_t* root_actions, const int64_t* root_offsets,
                   const uint32_t* bot_seeds, const uint32_t* eval_seeds,
@@ -118,12 +118,15 @@ int os_mcts_batch(os_engine* e, const os_mcts_params* p, int64_t num_roots,
                   int32_t* nchild, int32_t* root_n, double* root_w,
                   int8_t* root_out, int64_t* best_action, int32_t* nodes);
 
-/* One search under OS_POLICY_NUMPY driven by caller-provided MT19937 states in
- * numpy's legacy (key[624], pos) form, updated in place on return — the
+/* One search whose MT19937 streams persist across calls: the state is passed
+ * in numpy's legacy (key[624], pos) form (== libstdc++ mersenne_twister
+ * _M_x/_M_p) and updated in place on return.  OS_POLICY_CPP: a stateful
+ * MCTSBot (rng_ is never reseeded between MCTSearch calls, mcts.cc:325-333)
+ * and its RandomRolloutEvaluator; OS_POLICY_NUMPY: the
  * python/algorithms/mcts.py path with np.random.RandomState objects.
- * shared != 0: one stream (bot_key) serves bot and evaluator
+ * shared != 0 (numpy only): one stream (bot_key) serves bot and evaluator
  * (mcts_test.py:41-54); else eval_key/eval_pos is the evaluator's. */
-int os_mcts_numpy_state(os_engine* e, const os_mcts_params* p,
+int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
                         const int64_t* root_actions, int64_t n_actions,
                         int32_t shared, uint32_t* bot_key, int32_t* bot_pos,
                         uint32_t* eval_key, int32_t* eval_pos,
@@ -160,6 +163,15 @@ int os_engine_fetch(os_engine* e, int32_t max_children, int32_t* child_action,
                     int8_t* root_out, int64_t* best_action, int32_t* nodes);
 /* Summed simulations over the prepared roots of the last run (after fetch). */
 int64_t os_engine_last_sims(os_engine* e);
+/* Instrumentation of the last fetched run, summed over roots:
+ * out[0] sims, [1] children scanned by UCT selection, [2] nodes backed up,
+ * [3] children expanded, [4] children scanned by the solver backup,
+ * [5] MT19937 words drawn, [6] reference nodes_ counter, [7] arena slots
+ * used, [8] max tree depth, [9] GC runs.  out has 10 entries. */
+int os_engine_stats(os_engine* e, int64_t* out);
+/* Bytes per arena node (16 for n_rollouts == 1, else 24) and per root state. */
+int32_t os_engine_node_bytes(os_engine* e);
+int32_t os_engine_state_bytes(os_engine* e);
 
 /* Deterministic benchmark roots: root i = initial state plus
  * k_i = g() % (max_plies + 1) uniformly random legal plies drawn from

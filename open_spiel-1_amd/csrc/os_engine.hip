@@ -144,6 +144,7 @@ __global__ void k_mcts(DevArgs a) {
   else
     res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
                                     path, actbuf);
+  res.rng_words = bot.words + ((Policy == kPolicyNumpy && a.shared_stream) ? 0u : ev.words);
   a.results[gr] = res;
   const Node<R>& rn = nodes[0];
   const int P0 = G::to_move(root);
@@ -372,6 +373,10 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   // Arena: exact worst case = 1 + sims * max_children (one expansion per
   // simulation at most), unless the caller caps it.
   int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * cfg.max_children;
+  // GC (mcts.cc:402-424) can fire only if the node budget can be reached; its
+  // DFS stack then lives in the arena tail, so reserve room for it.
+  const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+  if (max_nodes > 1 && worst >= max_nodes) worst += GcStackReserve(cfg.max_children);
   int64_t cap = p->arena_nodes > 0 ? std::min<int64_t>(p->arena_nodes, worst) : worst;
   if (cap < 1) cap = 1;
   if (cap > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "arena too large per root");
@@ -762,6 +767,27 @@ int os_engine_fetch(os_engine* e, int32_t max_children, int32_t* child_action,
 
 int64_t os_engine_last_sims(os_engine* e) { return e ? e->last_sims : -1; }
 
+int os_engine_stats(os_engine* e, int64_t* out) {
+  if (!e || !out) return Fail(OS_ERR_INVALID, "null argument");
+  for (int i = 0; i < 10; ++i) out[i] = 0;
+  for (const SearchResult& s : e->last_results) {
+    out[0] += s.sims;
+    out[1] += s.scanned;
+    out[2] += s.backed;
+    out[3] += s.expanded;
+    out[4] += s.solver_scanned;
+    out[5] += s.rng_words;
+    out[6] += s.nodes;
+    out[7] += s.used;
+    out[8] = std::max<int64_t>(out[8], s.max_depth);
+    out[9] += s.gc_runs;
+  }
+  return OS_OK;
+}
+
+int32_t os_engine_node_bytes(os_engine* e) { return e ? e->node_bytes : -1; }
+int32_t os_engine_state_bytes(os_engine* e) { return e ? e->game.state_bytes : -1; }
+
 int os_mcts_batch(os_engine* e, const os_mcts_params* p, int64_t num_roots,
                   const int64_t* root_actions, const int64_t* root_offsets,
                   const uint32_t* bot_seeds, const uint32_t* eval_seeds,
@@ -777,7 +803,7 @@ int os_mcts_batch(os_engine* e, const os_mcts_params* p, int64_t num_roots,
                root_n, root_w, root_out, best_action, nodes);
 }
 
-int os_mcts_numpy_state(os_engine* e, const os_mcts_params* p,
+int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
                         const int64_t* root_actions, int64_t n_actions,
                         int32_t shared, uint32_t* bot_key, int32_t* bot_pos,
                         uint32_t* eval_key, int32_t* eval_pos,
@@ -786,8 +812,8 @@ int os_mcts_numpy_state(os_engine* e, const os_mcts_params* p,
                         int32_t* nchild, int32_t* root_n, double* root_w,
                         int8_t* root_out, int64_t* best_action, int32_t* nodes) {
   if (!e || !p || !bot_key || !bot_pos) return Fail(OS_ERR_INVALID, "null argument");
-  if (p->policy != OS_POLICY_NUMPY)
-    return Fail(OS_ERR_INVALID, "os_mcts_numpy_state needs OS_POLICY_NUMPY");
+  if (shared && p->policy != OS_POLICY_NUMPY)
+    return Fail(OS_ERR_INVALID, "a shared stream needs OS_POLICY_NUMPY");
   if (!shared && (!eval_key || !eval_pos))
     return Fail(OS_ERR_INVALID, "separate evaluator stream needs eval_key/eval_pos");
   int64_t offs[2] = {0, n_actions};

@@ -45,6 +45,10 @@ struct GameCfg {
   int32_t handicap;
   uint64_t board64, notcol0_64, notcollast_64;   // breakthrough (<= 64 cells)
   B128 board, notcol0, notcollast;               // hex / go (<= 128 cells)
+  // Hex side-neighbour masks.  Equal to notcol0 / notcollast except on n = 2,
+  // where the reference's wrap filter (hex.cc:206-222) also drops the genuine
+  // left/right and diagonal neighbours, leaving only up/down.
+  B128 hex_a, hex_b;
 };
 
 struct NoCtx {
@@ -295,8 +299,8 @@ struct Hex {
   };
   OS_HD static B128 nbr6(B128 x, const GameCfg& g) {
     const int n = g.rows;
-    B128 r = shr(x, n) | (shr(x, n - 1) & g.notcol0) | (shr(x, 1) & g.notcollast) |
-             (shl(x, 1) & g.notcol0) | (shl(x, n - 1) & g.notcollast) | shl(x, n);
+    B128 r = shr(x, n) | (shr(x, n - 1) & g.hex_a) | (shr(x, 1) & g.hex_b) |
+             (shl(x, 1) & g.hex_a) | (shl(x, n - 1) & g.hex_b) | shl(x, n);
     return r & g.board;
   }
   OS_HD static void init(State& s, const GameCfg&) {

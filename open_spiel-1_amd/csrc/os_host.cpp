@@ -76,6 +76,9 @@ void SquareMasks(int n, GameCfg* c) {
   }
   c->notcol0 = c->board & ~col0;
   c->notcollast = c->board & ~coll;
+  const bool n2 = n == 2;
+  c->hex_a = n2 ? b128(0, 0) : c->notcol0;
+  c->hex_b = n2 ? b128(0, 0) : c->notcollast;
 }
 
 std::string FormatDouble(double v) {

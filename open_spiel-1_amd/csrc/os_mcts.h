@@ -64,6 +64,13 @@ struct SearchResult {
   uint32_t used;    // arena slots used
   int32_t gc_runs;
   int32_t max_depth;
+  // Instrumentation for the algorithmic-bytes model:
+  uint32_t scanned;    // child nodes read by UCT selection
+  uint32_t backed;     // nodes updated by backup
+  uint32_t expanded;   // child nodes written by expansion
+  uint32_t solver_scanned;  // child nodes read by the MCTS-Solver backup
+  uint32_t rng_words;  // MT19937 words drawn (set by the caller)
+  uint32_t pad;
 };
 
 OS_HD double outcome_for(int8_t out0, int player) {
@@ -115,6 +122,12 @@ struct RewardOps<int32_t> {
   OS_HD static int32_t from(int r0, int, int) { return r0; }
 };
 
+// Arena nodes to reserve for the GC traversal stack (u32 entries; the stack
+// never holds more than depth x max_children entries).
+OS_HD int64_t GcStackReserve(int max_children) {
+  return (static_cast<int64_t>(kMaxPath) * max_children * 4) / 16 + 64;
+}
+
 // GarbageCollect (mcts.cc:430-443): every node with children whose
 // explore_count < limit loses them; nodes_ drops by the capacity of every
 // such block, including blocks under an already-cleared ancestor (the
@@ -158,6 +171,7 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
   res.sims = 0;
   res.gc_runs = 0;
   res.max_depth = 0;
+  res.scanned = res.backed = res.expanded = res.solver_scanned = 0;
   const int P0 = G::to_move(root);
   nodes[0].first = 0;
   nodes[0].n = 0;
@@ -202,12 +216,14 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         nodes[cur].first = first;
         nodes[cur].nchild = static_cast<uint8_t>(nc);
         nodes_count += nc;
+        res.expanded += nc;
       }
       const Node<R>& pn = nodes[cur];
       const int cp = P0 ^ (depth & 1);  // player choosing at this node
       const double logN = sp.log_lut[pn.n];
       double best = -inf;
       int chosen = 0;
+      res.scanned += pn.nchild;
       for (int k = 0; k < pn.nchild; ++k) {
         const Node<R>& c = nodes[pn.first + k];
         double v;
@@ -267,8 +283,10 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         const int pl = d == 0 ? P0 : (P0 ^ ((d - 1) & 1));
         nd.w += pl == 0 ? rv0 : rv1;
         nd.n += 1;
+        res.backed += 1;
         if (solved && nd.nchild > 0) {
           const int cpl = P0 ^ (d & 1);
+          res.solver_scanned += nd.nchild;
           int best = -1;
           double bestv = 0.0;
           bool all_solved = true;

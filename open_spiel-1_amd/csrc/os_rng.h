@@ -32,8 +32,10 @@ struct MtStream {
   uint32_t* s;
   int idx;  // next word index within the current block; kMtN => new block
   int pre;  // 1: the current block is already fully twisted (numpy import)
+  uint32_t words;  // words drawn (instrumentation for algorithmic bytes)
 
   OS_HD uint32_t next() {
+    ++words;
     if (idx >= kMtN) {
       idx = 0;
       pre = 0;

@@ -82,7 +82,7 @@ _sig("os_engine_destroy", ctypes.c_int, [_vp])
 _sig("os_mcts_batch", ctypes.c_int,
      [_vp, ctypes.POINTER(MctsParams), _i64, _P, _P, _P, _P, _i32, _P, _P, _P, _P,
       _P, _P, _P, _P, _P, _P])
-_sig("os_mcts_numpy_state", ctypes.c_int,
+_sig("os_mcts_stateful", ctypes.c_int,
      [_vp, ctypes.POINTER(MctsParams), _P, _i64, _i32, _P, _P, _P, _P, _i32, _P,
       _P, _P, _P, _P, _P, _P, _P, _P, _P])
 _sig("os_engine_tree", ctypes.c_int, [_vp, _i64, _P, _P, _P, _P, _P, _P, _P])
@@ -93,6 +93,9 @@ _sig("os_engine_run_async", ctypes.c_int, [_vp, _vp])
 _sig("os_engine_fetch", ctypes.c_int,
      [_vp, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P])
 _sig("os_engine_last_sims", _i64, [_vp])
+_sig("os_engine_stats", ctypes.c_int, [_vp, _P])
+_sig("os_engine_node_bytes", _i32, [_vp])
+_sig("os_engine_state_bytes", _i32, [_vp])
 _sig("os_make_roots", _i64, [_vp, _i64, _u32, _i32, _P, _P])
 
 

@@ -107,14 +107,13 @@ class Engine:
                             ptr(bs), ptr(es), mc, *_out_ptrs(o)))
     return o
 
-  def mcts_numpy_state(self, history, bot_state, eval_state=None, **params):
-    """python/algorithms/mcts.py search driven by numpy RandomState states.
+  def mcts_stateful(self, history, bot_state, eval_state=None, **params):
+    """One search continuing caller-owned MT19937 streams.
 
-    bot_state / eval_state: (key uint32[624], pos) pairs, updated in place
-    semantics returned as new tuples.  eval_state None => one shared stream.
+    bot_state / eval_state: (key uint32[624], pos) pairs (numpy legacy
+    RandomState form); the advanced states are returned.  eval_state None =>
+    one shared stream (numpy policy only).
     """
-    params = dict(params)
-    params["policy"] = _lib.POLICY_NUMPY
     p = make_params(**params)
     acts = _lib.i64(history)
     bkey = np.array(bot_state[0], dtype=np.uint32).copy()
@@ -127,7 +126,7 @@ class Engine:
       epos = np.array([eval_state[1]], dtype=np.int32)
     mc = self.max_children
     o = _alloc_outputs(1, mc)
-    check(lib.os_mcts_numpy_state(self._h, ctypes.byref(p), ptr(acts), len(acts),
+    check(lib.os_mcts_stateful(self._h, ctypes.byref(p), ptr(acts), len(acts),
                                   1 if shared else 0, ptr(bkey), ptr(bpos),
                                   ptr(ekey), ptr(epos), mc, *_out_ptrs(o)))
     new_eval = None if shared else (ekey, int(epos[0]))
@@ -180,6 +179,32 @@ class Engine:
 
   def last_sims(self):
     return int(lib.os_engine_last_sims(self._h))
+
+  STAT_KEYS = ("sims", "scanned", "backed", "expanded", "solver_scanned",
+               "rng_words", "nodes", "used", "max_depth", "gc_runs")
+
+  def stats(self):
+    """Instrumentation counters of the last fetched run (summed over roots)."""
+    out = np.zeros(10, np.int64)
+    check(lib.os_engine_stats(self._h, ptr(out)))
+    d = {k: int(v) for k, v in zip(self.STAT_KEYS, out)}
+    d["node_bytes"] = int(lib.os_engine_node_bytes(self._h))
+    d["state_bytes"] = int(lib.os_engine_state_bytes(self._h))
+    return d
+
+  def algorithmic_bytes(self, num_roots):
+    """HBM bytes the search must move, from the instrumentation.
+
+    Per simulation the algorithm reads every child scanned by UCT selection,
+    reads+writes each backed-up node, writes each expanded child, reads the
+    children the solver backup inspects, and reads+writes one MT19937 state
+    word per word drawn; plus one root state read per search.
+    """
+    s = self.stats()
+    nb = s["node_bytes"]
+    return (s["scanned"] * nb + s["backed"] * 2 * nb + s["expanded"] * nb +
+            s["solver_scanned"] * nb + s["rng_words"] * 8 +
+            num_roots * s["state_bytes"])
 
 
 def make_roots(game_string, num_roots, seed_base=1000, max_plies=8):

@@ -1,0 +1,318 @@
+"""Drop-in for open_spiel/python/algorithms/mcts.py, GPU-backed.
+
+Public names and signatures follow the reference module (Evaluator :29-43,
+RandomRolloutEvaluator :46-82, SearchNode :85-196, MCTSBot :199-443).
+
+`MCTSBot.mcts_search` runs on the MI355X whenever the search is the hot path
+the engine implements — a `RandomRolloutEvaluator`, UCT child selection, no
+Dirichlet noise, one of the five supported games — continuing the bot's and
+the evaluator's `np.random.RandomState` streams in place, bit-exact with the
+reference module (one shared RandomState, as in mcts_test.py:41-54, or two).
+Searches the engine does not implement (user evaluators, custom
+`child_selection_fn`, Dirichlet noise) run the generic host loop below; pass
+`backend="hip"` to forbid that and fail loudly instead.
+"""
+import math
+import time
+
+import numpy as np
+
+from . import _lib
+from . import pyspiel
+
+
+class Evaluator(object):
+  """Evaluation function interface (mcts.py:29-43)."""
+
+  def evaluate(self, state):
+    raise NotImplementedError
+
+  def prior(self, state):
+    raise NotImplementedError
+
+
+class RandomRolloutEvaluator(Evaluator):
+  """Average outcome of n_rollouts uniformly random playouts (mcts.py:46-82).
+
+  On the GPU path its RandomState is advanced by the kernel; `evaluate` is
+  also available on the host for direct calls.
+  """
+
+  def __init__(self, n_rollouts=1, random_state=None):
+    self.n_rollouts = n_rollouts
+    self._random_state = random_state or np.random.RandomState()
+
+  def evaluate(self, state):
+    total = None
+    for _ in range(self.n_rollouts):
+      playout = state.clone()
+      while not playout.is_terminal():
+        if playout.is_chance_node():
+          acts, probs = zip(*playout.chance_outcomes())
+          playout.apply_action(self._random_state.choice(acts, p=probs))
+        else:
+          playout.apply_action(self._random_state.choice(playout.legal_actions()))
+      r = np.array(playout.returns())
+      total = r if total is None else total + r
+    return total / self.n_rollouts
+
+  def prior(self, state):
+    if state.is_chance_node():
+      return state.chance_outcomes()
+    legal = state.legal_actions(state.current_player())
+    p = 1.0 / len(legal)
+    return [(a, p) for a in legal]
+
+
+class SearchNode(object):
+  """Search tree node (mcts.py:85-196; C++ mcts.h:109-137)."""
+
+  __slots__ = ["action", "player", "prior", "explore_count", "total_reward",
+               "outcome", "children"]
+
+  def __init__(self, action, player, prior):
+    self.action = action
+    self.player = player
+    self.prior = prior
+    self.explore_count = 0
+    self.total_reward = 0.0
+    self.outcome = None
+    self.children = []
+
+  def uct_value(self, parent_explore_count, uct_c):
+    """UCT (mcts.py:124-133 / mcts.cc:89-100)."""
+    if self.outcome is not None:
+      return self.outcome[self.player]
+    if self.explore_count == 0:
+      return float("inf")
+    n = self.explore_count
+    return self.total_reward / n + uct_c * math.sqrt(
+        math.log(parent_explore_count) / n)
+
+  def puct_value(self, parent_explore_count, uct_c):
+    """PUCT (mcts.py:135-142 / mcts.cc:102-111)."""
+    if self.outcome is not None:
+      return self.outcome[self.player]
+    q = self.total_reward / self.explore_count if self.explore_count else 0
+    return q + uct_c * self.prior * math.sqrt(parent_explore_count) / (
+        self.explore_count + 1)
+
+  def sort_key(self):
+    """Proven value, then visits, then reward (mcts.py:144-158)."""
+    proven = 0 if self.outcome is None else self.outcome[self.player]
+    return (proven, self.explore_count, self.total_reward)
+
+  def best_child(self):
+    return max(self.children, key=SearchNode.sort_key)
+
+  def children_str(self, state=None):
+    ordered = sorted(self.children, key=SearchNode.sort_key)
+    return "\n".join(c.to_str(state) for c in reversed(ordered))
+
+  def to_str(self, state=None):
+    if state is not None and self.action is not None:
+      name = state.action_to_string(state.current_player(), self.action)
+    else:
+      name = str(self.action)
+    mean = self.explore_count and self.total_reward / self.explore_count
+    solved = ("{:4.1f}".format(self.outcome[self.player])
+              if self.outcome else "none")
+    return ("{:>6}: player: {}, prior: {:5.3f}, value: {:6.3f}, sims: {:5d}, "
+            "outcome: {}, {:3d} children").format(
+                name, self.player, self.prior, mean, self.explore_count, solved,
+                len(self.children))
+
+  def __str__(self):
+    return self.to_str(None)
+
+
+def tree_to_search_nodes(flat, state, game, root_action=None):
+  """Materialises the engine's flat arena (os_engine_tree) as SearchNodes.
+
+  Node players follow from depth (the five games alternate turns); priors are
+  the uniform 1/|legal| of RandomRolloutEvaluator.prior; outcomes are
+  [v, -v] vectors as the reference stores Returns().
+  """
+  first, n, w = flat["first"], flat["n"], flat["w"]
+  action, nchild, out0 = flat["action"], flat["nchild"], flat["out0"]
+  p0 = state.current_player()
+  root = SearchNode(root_action, p0, 1)
+  stack = [(0, root, 0)]
+  while stack:
+    idx, node, depth = stack.pop()
+    node.explore_count = int(n[idx])
+    node.total_reward = float(w[idx])
+    if out0[idx] != 2:
+      v = float(out0[idx])
+      node.outcome = [v, -v]
+    nc = int(nchild[idx])
+    if nc:
+      child_player = p0 ^ (depth & 1)
+      prior = 1.0 / nc
+      base = int(first[idx])
+      node.children = [SearchNode(int(action[base + k]), child_player, prior)
+                       for k in range(nc)]
+      for k, c in enumerate(node.children):
+        stack.append((base + k, c, depth + 1))
+  return root
+
+
+class MCTSBot(pyspiel.Bot):
+  """MCTS bot (mcts.py:199-443) whose hot path runs on the MI355X."""
+
+  def __init__(self, game, uct_c, max_simulations, evaluator, solve=True,
+               random_state=None, child_selection_fn=SearchNode.uct_value,
+               dirichlet_noise=None, verbose=False, backend="auto"):
+    pyspiel.Bot.__init__(self)
+    gt = game.get_type()
+    if gt.reward_model != pyspiel.GameType.RewardModel.TERMINAL:
+      raise ValueError("Game must have terminal rewards.")
+    if gt.dynamics != pyspiel.GameType.Dynamics.SEQUENTIAL:
+      raise ValueError("Game must have sequential turns.")
+    if backend not in ("auto", "hip", "host"):
+      raise ValueError("backend must be 'auto', 'hip' or 'host'")
+    self._game = game
+    self.uct_c = uct_c
+    self.max_simulations = max_simulations
+    self.evaluator = evaluator
+    self.verbose = verbose
+    self.solve = solve
+    self.max_utility = game.max_utility()
+    self._dirichlet_noise = dirichlet_noise
+    self._random_state = random_state or np.random.RandomState()
+    self._child_selection_fn = child_selection_fn
+    self.backend = backend
+    if backend == "hip" and not self._gpu_eligible():
+      raise ValueError("backend='hip' needs RandomRolloutEvaluator, UCT child "
+                       "selection, no Dirichlet noise and a supported game")
+
+  def _gpu_eligible(self):
+    return (type(self.evaluator) is RandomRolloutEvaluator and
+            self._child_selection_fn is SearchNode.uct_value and
+            not self._dirichlet_noise and
+            isinstance(self._game, pyspiel.Game))
+
+  def restart_at(self, state):
+    pass
+
+  def step_with_policy(self, state):
+    t0 = time.time()
+    root = self.mcts_search(state)
+    best = root.best_child()
+    if self.verbose:
+      secs = time.time() - t0
+      print("Finished {} sims in {:.3f} secs, {:.1f} sims/s".format(
+          root.explore_count, secs, root.explore_count / secs))
+      print("Root:")
+      print(root.to_str(state))
+      print("Children:")
+      print(root.children_str(state))
+      if best.children:
+        nxt = state.clone()
+        nxt.apply_action(best.action)
+        print("Children of chosen:")
+        print(best.children_str(nxt))
+    chosen = best.action
+    policy = [(a, 1.0 if a == chosen else 0.0)
+              for a in state.legal_actions(state.current_player())]
+    return policy, chosen
+
+  def step(self, state):
+    return self.step_with_policy(state)[1]
+
+  def mcts_search(self, state):
+    use_gpu = self.backend == "hip" or (self.backend == "auto" and
+                                        self._gpu_eligible())
+    if use_gpu:
+      return self._search_gpu(state)
+    return self._search_host(state)
+
+  # ---- GPU path -------------------------------------------------------------
+  def _search_gpu(self, state):
+    eng = pyspiel._engine_for(self._game)
+    bot_rs = self._random_state
+    ev_rs = self.evaluator._random_state
+    shared = ev_rs is bot_rs
+    b = bot_rs.get_state()
+    e = None if shared else ev_rs.get_state()
+    _, nb, ne = eng.mcts_stateful(
+        state.history(), (b[1], b[2]), None if shared else (e[1], e[2]),
+        uct_c=self.uct_c, max_simulations=self.max_simulations,
+        n_rollouts=self.evaluator.n_rollouts, solve=self.solve,
+        max_memory_mb=0, policy=_lib.POLICY_NUMPY)
+    bot_rs.set_state(("MT19937", nb[0], nb[1], b[3], b[4]))
+    if not shared:
+      ev_rs.set_state(("MT19937", ne[0], ne[1], e[3], e[4]))
+    return tree_to_search_nodes(eng.tree(0), state, self._game)
+
+  # ---- generic host path (user evaluators / selection functions) ------------
+  def _descend(self, root, state):
+    path = [root]
+    node = root
+    working = state.clone()
+    while not working.is_terminal() and node.explore_count > 0:
+      if not node.children:
+        priors = self.evaluator.prior(working)
+        if node is root and self._dirichlet_noise:
+          eps, alpha = self._dirichlet_noise
+          noise = self._random_state.dirichlet([alpha] * len(priors))
+          priors = [(a, (1 - eps) * p + eps * z)
+                    for (a, p), z in zip(priors, noise)]
+        self._random_state.shuffle(priors)
+        mover = working.current_player()
+        node.children = [SearchNode(a, mover, p) for a, p in priors]
+      if working.is_chance_node():
+        acts, probs = zip(*working.chance_outcomes())
+        pick = self._random_state.choice(acts, p=probs)
+        node = next(c for c in node.children if c.action == pick)
+      else:
+        parent_n = node.explore_count
+        node = max(node.children,
+                   key=lambda c: self._child_selection_fn(c, parent_n, self.uct_c))
+      working.apply_action(node.action)
+      path.append(node)
+    return path, working
+
+  def _backup(self, path, returns, root_player, solved):
+    for node in reversed(path):
+      who = root_player if node.player == pyspiel.PlayerId.CHANCE else node.player
+      node.total_reward += returns[who]
+      node.explore_count += 1
+      if not (solved and node.children):
+        continue
+      mover = node.children[0].player
+      if mover == pyspiel.PlayerId.CHANCE:
+        first = node.children[0].outcome
+        if first is not None and all(np.array_equal(c.outcome, first)
+                                     for c in node.children):
+          node.outcome = first
+        else:
+          solved = False
+        continue
+      proven = [c for c in node.children if c.outcome is not None]
+      best = None
+      for c in proven:
+        if best is None or c.outcome[mover] > best.outcome[mover]:
+          best = c
+      if best is not None and (len(proven) == len(node.children) or
+                               best.outcome[mover] == self.max_utility):
+        node.outcome = best.outcome
+      else:
+        solved = False
+
+  def _search_host(self, state):
+    root_player = state.current_player()
+    root = SearchNode(None, root_player, 1)
+    for _ in range(self.max_simulations):
+      path, working = self._descend(root, state)
+      if working.is_terminal():
+        returns = working.returns()
+        path[-1].outcome = returns
+        solved = self.solve
+      else:
+        returns = self.evaluator.evaluate(working)
+        solved = False
+      self._backup(path, returns, root_player, solved)
+      if root.outcome is not None:
+        break
+    return root

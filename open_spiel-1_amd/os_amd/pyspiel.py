@@ -1,0 +1,457 @@
+"""`pyspiel`-compatible surface for the five target games.
+
+Mirrors the subset of open_spiel/python/pybind11/pyspiel.cc the Python MCTS
+bot path uses (load_game :675-684, State :292-360, Game :362-390, GameType
+:215-284, PlayerId :277-281, Bot :487-497, RandomRolloutEvaluator / MCTSBot
+:499-524).  Game rules run in libos_mcts.so (the same state machines the
+gfx950 kernel runs); `MCTSBot.step` / `.mcts_search` run on the GPU.
+
+Errors follow the reference: SpielFatalError conditions raise RuntimeError
+(`SpielError`), unsupported games raise ValueError.
+"""
+import ctypes
+import enum
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, get_string, lib
+
+SpielError = _lib.SpielError
+INVALID_ACTION = -1
+
+
+class PlayerId(enum.IntEnum):
+  """spiel.h:40-49."""
+  INVALID = -3
+  TERMINAL = -4
+  CHANCE = -1
+  SIMULTANEOUS = -2
+
+
+class TensorLayout(enum.IntEnum):
+  HWC = 0
+  CHW = 1
+
+
+class GameType:
+  """spiel.h:61-143 (read-only record)."""
+
+  class Dynamics(enum.IntEnum):
+    SIMULTANEOUS = 0
+    SEQUENTIAL = 1
+
+  class ChanceMode(enum.IntEnum):
+    DETERMINISTIC = 0
+    EXPLICIT_STOCHASTIC = 1
+    SAMPLED_STOCHASTIC = 2
+
+  class Information(enum.IntEnum):
+    ONE_SHOT = 0
+    PERFECT_INFORMATION = 1
+    IMPERFECT_INFORMATION = 2
+
+  class Utility(enum.IntEnum):
+    ZERO_SUM = 0
+    CONSTANT_SUM = 1
+    GENERAL_SUM = 2
+    IDENTICAL = 3
+
+  class RewardModel(enum.IntEnum):
+    REWARDS = 0
+    TERMINAL = 1
+
+  def __init__(self, short_name, long_name, parameter_specification,
+               provides_information_state_string=True):
+    self.short_name = short_name
+    self.long_name = long_name
+    self.dynamics = GameType.Dynamics.SEQUENTIAL
+    self.chance_mode = GameType.ChanceMode.DETERMINISTIC
+    self.information = GameType.Information.PERFECT_INFORMATION
+    self.utility = GameType.Utility.ZERO_SUM
+    self.reward_model = GameType.RewardModel.TERMINAL
+    self.max_num_players = 2
+    self.min_num_players = 2
+    self.provides_information_state_string = provides_information_state_string
+    self.provides_information_state_tensor = False
+    self.provides_observation_string = True
+    self.provides_observation_tensor = True
+    self.parameter_specification = parameter_specification
+    self.default_loadable = True
+
+  def __repr__(self):
+    return "<GameType '%s'>" % self.short_name
+
+
+_TYPES = {
+    0: GameType("tic_tac_toe", "Tic Tac Toe", {}),
+    1: GameType("connect_four", "Connect Four", {}),
+    2: GameType("breakthrough", "Breakthrough", {"rows": 8, "columns": 8},
+                provides_information_state_string=False),
+    3: GameType("hex", "Hex", {"board_size": 11}),
+    4: GameType("go", "Go", {"komi": 7.5, "board_size": 19, "handicap": 0}),
+}
+
+
+def _game_string(name, params):
+  if not params:
+    return name
+  return "%s(%s)" % (name, ",".join("%s=%s" % (k, params[k]) for k in sorted(params)))
+
+
+class Game:
+  """Game (spiel.h:601-750) backed by libos_mcts.so."""
+
+  def __init__(self, game_string):
+    h = ctypes.c_void_p()
+    check(lib.os_game_load(game_string.encode(), ctypes.byref(h)))
+    self._h = h
+    self._info = _lib.GameInfo()
+    check(lib.os_game_get_info(h, ctypes.byref(self._info)))
+    self._string = get_string(lib.os_game_to_string, h)
+    self.game_string = game_string
+
+  def __del__(self):
+    if getattr(self, "_h", None) and self._h.value:
+      lib.os_game_free(self._h)
+
+  def new_initial_state(self):
+    return State(self)
+
+  def num_distinct_actions(self):
+    return self._info.num_distinct_actions
+
+  def policy_tensor_shape(self):
+    return [self._info.num_distinct_actions]
+
+  def max_chance_outcomes(self):
+    return 0
+
+  def num_players(self):
+    return 2
+
+  def min_utility(self):
+    return self._info.min_utility
+
+  def max_utility(self):
+    return self._info.max_utility
+
+  def utility_sum(self):
+    return self._info.utility_sum
+
+  def max_game_length(self):
+    return self._info.max_game_length
+
+  def get_type(self):
+    return _TYPES[self._info.kind]
+
+  def get_parameters(self):
+    k = self._info.kind
+    if k == 2:
+      return {"columns": self._info.cols, "rows": self._info.rows}
+    if k == 3:
+      return {"board_size": self._info.rows}
+    if k == 4:
+      return {"board_size": self._info.rows, "handicap": self._info.handicap,
+              "komi": self._info.komi}
+    return {}
+
+  def deserialize_state(self, s):
+    """Inverse of State.serialize() (history form, spiel.cc:375-420)."""
+    st = self.new_initial_state()
+    for line in s.split("\n"):
+      if line:
+        st.apply_action(int(line))
+    return st
+
+  def __str__(self):
+    return self._string
+
+  def __eq__(self, other):
+    return isinstance(other, Game) and str(self) == str(other)
+
+  def __hash__(self):
+    return hash(self._string)
+
+  def __reduce__(self):
+    return (load_game, (self.game_string,))
+
+
+def load_game(name, params=None):
+  """pyspiel.load_game(name[, params]) (pyspiel.cc:675-684)."""
+  return Game(_game_string(name, params) if params else name)
+
+
+class State:
+  """State (spiel.h:173-592) backed by libos_mcts.so host state machines."""
+
+  __slots__ = ("_game", "_h")
+
+  def __init__(self, game, handle=None):
+    self._game = game
+    if handle is None:
+      handle = ctypes.c_void_p()
+      check(lib.os_state_new(game._h, ctypes.byref(handle)))
+    self._h = handle
+
+  def __del__(self):
+    h = getattr(self, "_h", None)
+    if h is not None and h.value:
+      lib.os_state_free(h)
+
+  def clone(self):
+    h = ctypes.c_void_p()
+    check(lib.os_state_clone(self._h, ctypes.byref(h)))
+    return State(self._game, h)
+
+  def __deepcopy__(self, memo):
+    return self.clone()
+
+  def __copy__(self):
+    return self.clone()
+
+  def child(self, action):
+    c = self.clone()
+    c.apply_action(action)
+    return c
+
+  def current_player(self):
+    return int(lib.os_state_current_player(self._h))
+
+  def is_terminal(self):
+    return bool(lib.os_state_is_terminal(self._h))
+
+  def is_chance_node(self):
+    return False
+
+  def is_simultaneous_node(self):
+    return False
+
+  def is_player_node(self):
+    return not self.is_terminal()
+
+  def apply_action(self, action):
+    check(lib.os_state_apply(self._h, int(action)))
+
+  def legal_actions(self, player=None):
+    if player is not None and player != self.current_player():
+      return []
+    buf = np.zeros(256, np.int64)
+    n = lib.os_state_legal_actions(self._h, buf.ctypes.data, 256)
+    return [int(a) for a in buf[:n]]
+
+  def legal_actions_mask(self, player=None):
+    mask = [0] * self._game.num_distinct_actions()
+    for a in self.legal_actions(player):
+      mask[a] = 1
+    return mask
+
+  def action_to_string(self, arg0, arg1=None):
+    if arg1 is None:
+      player, action = self.current_player(), arg0
+    else:
+      player, action = arg0, arg1
+    return get_string(lib.os_state_action_to_string, self._h, int(player),
+                      int(action))
+
+  def string_to_action(self, arg0, arg1=None):
+    if arg1 is None:
+      player, s = self.current_player(), arg0
+    else:
+      player, s = arg0, arg1
+    for a in self.legal_actions():
+      if self.action_to_string(player, a) == s:
+        return a
+    raise SpielError("Illegal move: %s" % s)
+
+  def returns(self):
+    r = np.zeros(2, np.float64)
+    lib.os_state_returns(self._h, r.ctypes.data)
+    return [float(r[0]), float(r[1])]
+
+  def rewards(self):
+    return self.returns() if self.is_terminal() else [0.0, 0.0]
+
+  def player_return(self, player):
+    return self.returns()[player]
+
+  def player_reward(self, player):
+    return self.rewards()[player]
+
+  def history(self):
+    buf = np.zeros(512, np.int64)
+    n = lib.os_state_history(self._h, buf.ctypes.data, 512)
+    if n > 512:
+      buf = np.zeros(n, np.int64)
+      lib.os_state_history(self._h, buf.ctypes.data, n)
+    return [int(a) for a in buf[:n]]
+
+  def history_str(self):
+    return " ".join(str(a) for a in self.history())
+
+  def information_state_string(self, player=None):
+    return self.history_str()
+
+  def observation_string(self, player=None):
+    return str(self)
+
+  def chance_outcomes(self):
+    return []
+
+  def num_distinct_actions(self):
+    return self._game.num_distinct_actions()
+
+  def num_players(self):
+    return 2
+
+  def get_game(self):
+    return self._game
+
+  def get_type(self):
+    return self._game.get_type()
+
+  def serialize(self):
+    h = self.history()
+    return "".join("%d\n" % a for a in h)
+
+  def __str__(self):
+    return get_string(lib.os_state_to_string, self._h)
+
+  def __reduce__(self):
+    return (_restore_state, (self._game.game_string, self.history()))
+
+
+def _restore_state(game_string, history):
+  st = load_game(game_string).new_initial_state()
+  for a in history:
+    st.apply_action(a)
+  return st
+
+
+class Bot:
+  """pyspiel.Bot (spiel_bots.h; pybind trampoline pyspiel.cc:82-178)."""
+
+  def __init__(self):
+    pass
+
+  def step(self, state):
+    raise NotImplementedError
+
+  def step_with_policy(self, state):
+    a = self.step(state)
+    return [(a, 1.0)], a
+
+  def restart(self):
+    pass
+
+  def restart_at(self, state):
+    pass
+
+  def inform_action(self, state, player_id, action):
+    pass
+
+  def provides_force_action(self):
+    return False
+
+  def force_action(self, state, action):
+    raise SpielError("force_action not implemented")
+
+  def provides_policy(self):
+    return False
+
+  def get_policy(self, state):
+    raise SpielError("get_policy not implemented")
+
+
+class ChildSelectionPolicy(enum.IntEnum):
+  UCT = 0
+  PUCT = 1
+
+
+def _mt_key(seed):
+  """std::mt19937(seed) state as (key[624], pos=624) (== numpy legacy)."""
+  st = np.random.RandomState(seed & 0xFFFFFFFF).get_state()
+  return np.array(st[1], dtype=np.uint32), int(st[2])
+
+
+class Evaluator:
+  """pyspiel.Evaluator (no Python trampoline in the reference either)."""
+
+
+class RandomRolloutEvaluator(Evaluator):
+  """RandomRolloutEvaluator(n_rollouts, seed) (mcts.h:92-106).
+
+  Holds its std::mt19937 stream; a bot using it advances the stream on the GPU
+  and writes it back, so an evaluator shared by several bots interleaves its
+  random numbers in call order exactly as in the reference (mcts_test.cc:39).
+  """
+
+  def __init__(self, n_rollouts, seed):
+    self.n_rollouts = int(n_rollouts)
+    self._state = _mt_key(seed)
+
+
+_ENGINES = {}
+
+
+def _engine_for(game):
+  from .engine import Engine
+  key = str(game)
+  eng = _ENGINES.get(key)
+  if eng is None:
+    eng = Engine(game.game_string, device=0)
+    _ENGINES[key] = eng
+  return eng
+
+
+class MCTSBot(Bot):
+  """pyspiel.MCTSBot (mcts.h:139-208; pyspiel.cc:512-524) on the GPU.
+
+  Every `step` / `mcts_search` runs MCTSBot::MCTSearch (mcts.cc:325-428) in
+  the gfx950 kernel, continuing this bot's and its evaluator's MT19937
+  streams, so a sequence of calls is bit-exact with the C++ bot.
+  """
+
+  def __init__(self, game, evaluator, uct_c, max_simulations, max_memory_mb,
+               solve, seed, verbose,
+               child_selection_policy=ChildSelectionPolicy.UCT):
+    Bot.__init__(self)
+    if not isinstance(evaluator, RandomRolloutEvaluator):
+      raise ValueError("the GPU MCTSBot supports RandomRolloutEvaluator only "
+                       "(pyspiel.Evaluator has no Python trampoline either)")
+    if child_selection_policy != ChildSelectionPolicy.UCT:
+      raise ValueError("PUCT child selection is not supported by this engine")
+    gt = game.get_type()
+    if gt.reward_model != GameType.RewardModel.TERMINAL:
+      raise SpielError("Game must have terminal rewards.")
+    if gt.dynamics != GameType.Dynamics.SEQUENTIAL:
+      raise SpielError("Game must have sequential turns.")
+    self._game = game
+    self._evaluator = evaluator
+    self.uct_c = float(uct_c)
+    self.max_simulations = int(max_simulations)
+    self.max_memory_mb = int(max_memory_mb)
+    self.solve = bool(solve)
+    self.verbose = bool(verbose)
+    self._state = _mt_key(seed)
+
+  def mcts_search(self, state):
+    from .mcts import SearchNode, tree_to_search_nodes
+    eng = _engine_for(self._game)
+    o, self._state, self._evaluator._state = eng.mcts_stateful(
+        state.history(), self._state, self._evaluator._state,
+        uct_c=self.uct_c, max_simulations=self.max_simulations,
+        n_rollouts=self._evaluator.n_rollouts, max_memory_mb=self.max_memory_mb,
+        solve=self.solve, policy=_lib.POLICY_CPP)
+    del o, SearchNode
+    return tree_to_search_nodes(eng.tree(0), state, self._game, root_action=-1)
+
+  def step(self, state):
+    root = self.mcts_search(state)
+    if not root.children:
+      raise SpielError("MCTSBot: root has no children")
+    return root.best_child().action
+
+  def step_with_policy(self, state):
+    a = self.step(state)
+    return [(a, 1.0)], a

@@ -121,7 +121,8 @@ int hc_mcts_batch(const char* game_string, int64_t num_roots,
   sp.max_nodes = static_cast<int32_t>((max_memory_mb << 20) / 80 + 1);
   sp.policy = policy;
   sp.log_lut = lut.data();
-  const uint32_t cap = 1 + static_cast<uint32_t>(max_simulations) * game.cfg.max_children;
+  const uint32_t cap = 1 + static_cast<uint32_t>(max_simulations) * game.cfg.max_children +
+                       static_cast<uint32_t>(GcStackReserve(game.cfg.max_children));
   for (int64_t r = 0; r < num_roots; ++r) {
     HostState hs;
     hs.game = &game;
@@ -153,6 +154,49 @@ int hc_mcts_batch(const char* game_string, int64_t num_roots,
     if (rc) return rc;
   }
   return 0;
+}
+
+// Product RNG primitives (csrc/os_rng.h) on the host, for known-answer tests.
+void hc_mt_words(uint32_t seed, int64_t n, uint32_t* out) {
+  std::vector<uint32_t> s(kMtN);
+  mt_seed(s.data(), seed);
+  MtStream g{s.data(), kMtN, 0, 0};
+  for (int64_t i = 0; i < n; ++i) out[i] = g.next();
+}
+void hc_absl_uniform(uint32_t seed, uint32_t n, int64_t k, uint64_t* out) {
+  std::vector<uint32_t> s(kMtN);
+  mt_seed(s.data(), seed);
+  MtStream g{s.data(), kMtN, 0, 0};
+  for (int64_t i = 0; i < k; ++i) out[i] = AbslUniform(g, n);
+}
+void hc_cpp_shuffle(uint32_t seed, int32_t n, int32_t* out) {
+  std::vector<uint32_t> s(kMtN);
+  mt_seed(s.data(), seed);
+  MtStream g{s.data(), kMtN, 0, 0};
+  std::vector<int32_t> a(n);
+  for (int i = 0; i < n; ++i) a[i] = i;
+  CppShuffle(a.data(), n, g);
+  for (int i = 0; i < n; ++i) out[i] = a[i];
+}
+// numpy RandomState(seed): k choice(range(n)) draws then one shuffle of n.
+void hc_np_ops(uint32_t seed, uint32_t n, int64_t k, uint32_t* choices,
+               int32_t* perm, uint32_t* next_word) {
+  std::vector<uint32_t> s(kMtN);
+  mt_seed(s.data(), seed);
+  MtStream g{s.data(), kMtN, 0, 0};
+  for (int64_t i = 0; i < k; ++i) choices[i] = NpChoice(g, n);
+  std::vector<int32_t> a(n);
+  for (uint32_t i = 0; i < n; ++i) a[i] = static_cast<int32_t>(i);
+  NpShuffle(a.data(), static_cast<int>(n), g);
+  for (uint32_t i = 0; i < n; ++i) perm[i] = a[i];
+  *next_word = g.next();
+}
+// Import a numpy (key, pos) state, draw k words, export back (finalize).
+void hc_mt_roundtrip(uint32_t* key, int32_t* pos, int64_t k, uint32_t* out) {
+  MtStream g{key, *pos, 1, 0};
+  for (int64_t i = 0; i < k; ++i) out[i] = g.next();
+  g.finalize();
+  *pos = g.idx;
 }
 
 // Product rollouts on the host: RandomRolloutEvaluator::Evaluate per seed.

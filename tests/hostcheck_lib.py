@@ -1,0 +1,112 @@
+"""ctypes wrapper for tests/hostcheck (product engine compiled for the host).
+
+TEST INFRASTRUCTURE ONLY: lets the CPU suite check the exact search logic the
+gfx950 kernel runs (csrc/os_mcts.h, os_games.h, os_rng.h) against the oracle.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+_PATH = os.path.join(_ROOT, "hostcheck", "build", "libhostcheck.so")
+_lib = None
+
+
+def lib():
+  global _lib
+  if _lib is None:
+    L = ctypes.CDLL(_PATH)
+    L.hc_last_error.restype = ctypes.c_char_p
+    vp = ctypes.c_void_p
+    L.hc_mcts_batch.argtypes = [ctypes.c_char_p, ctypes.c_int64, vp, vp,
+                                ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                vp, vp, ctypes.c_int32] + [vp] * 10
+    L.hc_rollouts.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.c_int64,
+                              vp, vp]
+    L.hc_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
+    L.hc_absl_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp]
+    L.hc_cpp_shuffle.argtypes = [ctypes.c_uint32, ctypes.c_int32, vp]
+    L.hc_np_ops.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp, vp,
+                            vp]
+    L.hc_mt_roundtrip.argtypes = [vp, vp, ctypes.c_int64, vp]
+    _lib = L
+  return _lib
+
+
+KEYS = ("child_action", "child_n", "child_w", "child_out", "nchild", "root_n",
+        "root_w", "root_out", "best_action", "nodes")
+
+
+def mcts_batch(game_string, acts, offs, bot_seeds, eval_seeds, max_children,
+               uct_c=2.0, max_simulations=1000, n_rollouts=1, max_memory_mb=1000,
+               solve=True, policy=0):
+  R = len(offs) - 1
+  mc = max_children
+  o = dict(child_action=np.zeros((R, mc), np.int32),
+           child_n=np.zeros((R, mc), np.int32),
+           child_w=np.zeros((R, mc), np.float64),
+           child_out=np.zeros((R, mc), np.int8),
+           nchild=np.zeros(R, np.int32), root_n=np.zeros(R, np.int32),
+           root_w=np.zeros(R, np.float64), root_out=np.zeros(R, np.int8),
+           best_action=np.zeros(R, np.int64), nodes=np.zeros(R, np.int32))
+  # padding convention of the C-ABI
+  o["child_action"][:] = -1
+  o["child_out"][:] = 2
+  acts = np.ascontiguousarray(acts, np.int64)
+  offs = np.ascontiguousarray(offs, np.int64)
+  bs = np.ascontiguousarray(bot_seeds, np.uint32)
+  es = np.ascontiguousarray(eval_seeds, np.uint32)
+  rc = lib().hc_mcts_batch(game_string.encode(), R, acts.ctypes.data,
+                           offs.ctypes.data, uct_c, max_simulations, n_rollouts,
+                           max_memory_mb, int(solve), policy, bs.ctypes.data,
+                           es.ctypes.data, mc, *[o[k].ctypes.data for k in KEYS])
+  if rc:
+    raise RuntimeError(lib().hc_last_error().decode())
+  return o
+
+
+def rollouts(game_string, history, seeds):
+  a = np.ascontiguousarray(history, np.int64)
+  s = np.ascontiguousarray(seeds, np.uint32)
+  out = np.zeros((len(s), 2), np.float64)
+  rc = lib().hc_rollouts(game_string.encode(), a.ctypes.data, len(a), len(s),
+                         s.ctypes.data, out.ctypes.data)
+  if rc:
+    raise RuntimeError(lib().hc_last_error().decode())
+  return out
+
+
+def mt_words(seed, n):
+  out = np.zeros(n, np.uint32)
+  lib().hc_mt_words(seed, n, out.ctypes.data)
+  return out
+
+
+def absl_uniform(seed, n, k):
+  out = np.zeros(k, np.uint64)
+  lib().hc_absl_uniform(seed, n, k, out.ctypes.data)
+  return out
+
+
+def cpp_shuffle(seed, n):
+  out = np.zeros(n, np.int32)
+  lib().hc_cpp_shuffle(seed, n, out.ctypes.data)
+  return out
+
+
+def np_ops(seed, n, k):
+  ch = np.zeros(k, np.uint32)
+  perm = np.zeros(n, np.int32)
+  nw = np.zeros(1, np.uint32)
+  lib().hc_np_ops(seed, n, k, ch.ctypes.data, perm.ctypes.data, nw.ctypes.data)
+  return ch, perm, int(nw[0])
+
+
+def mt_roundtrip(key, pos, k):
+  key = np.array(key, dtype=np.uint32).copy()
+  p = np.array([pos], dtype=np.int32)
+  out = np.zeros(k, np.uint32)
+  lib().hc_mt_roundtrip(key.ctypes.data, p.ctypes.data, k, out.ctypes.data)
+  return out, key, int(p[0])

@@ -1,0 +1,51 @@
+"""The C-ABI library loads without a GPU and exports every symbol that
+include/os_mcts.h declares; error paths report through os_last_error."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "os_mcts.h")
+SO = os.path.join(ROOT, "open_spiel-1_amd", "os_amd", "libos_mcts.so")
+
+
+def declared_symbols():
+  text = open(HDR).read()
+  text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+  names = re.findall(r"\b(os_[a-z0-9_]+)\s*\(", text)
+  return sorted(set(names))
+
+
+def test_header_declares_entry_points():
+  names = declared_symbols()
+  for must in ("os_game_load", "os_state_apply", "os_engine_create",
+               "os_mcts_batch", "os_rollouts_batch", "os_mcts_stateful",
+               "os_engine_run_async", "os_last_error"):
+    assert must in names
+
+
+@pytest.mark.parametrize("name", declared_symbols())
+def test_symbol_exported(name):
+  lib = ctypes.CDLL(SO)
+  assert hasattr(lib, name), name
+
+
+def test_errors_surface():
+  from os_amd import _lib
+  h = ctypes.c_void_p()
+  rc = _lib.lib.os_game_load(b"not_a_game", ctypes.byref(h))
+  assert rc == _lib.OS_ERR_UNSUPPORTED
+  assert b"not supported" in _lib.lib.os_last_error()
+  rc = _lib.lib.os_game_load(b"hex(board_size=x)", ctypes.byref(h))
+  assert rc == _lib.OS_ERR_INVALID
+
+
+def test_engine_without_gpu_fails_loudly():
+  import torch
+  if torch.cuda.is_available():
+    pytest.skip("GPU present")
+  from os_amd import engine
+  with pytest.raises(RuntimeError):
+    engine.Engine("connect_four")

@@ -1,0 +1,52 @@
+"""Product RNG primitives (csrc/os_rng.h, host-compiled) against libstdc++
+(through the oracle) and the container's numpy legacy RandomState."""
+import numpy as np
+import pytest
+
+import hostcheck_lib as H
+import oracle_lib as O
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, 5489, 2**32 - 1])
+def test_mt_stream_matches_std_mt19937(seed):
+  # Crosses several lazy in-place twists.
+  assert np.array_equal(H.mt_words(seed, 3000), O.mt19937(seed, 3000))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 48, 82, 121, 768])
+def test_absl_uniform_matches_oracle(n):
+  for seed in (3, 99):
+    assert np.array_equal(H.absl_uniform(seed, n, 500), O.absl_uniform(seed, n, 500))
+
+
+@pytest.mark.parametrize("n", list(range(1, 40)) + [48, 82, 121, 122])
+def test_cpp_shuffle_matches_libstdcxx(n):
+  for seed in (1, 17, 123456):
+    assert np.array_equal(H.cpp_shuffle(seed, n), O.std_shuffle(seed, n))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 9, 16, 17, 82, 121])
+def test_numpy_choice_and_shuffle(n):
+  for seed in (0, 42, 77):
+    rs = np.random.RandomState(seed)
+    ch = [rs.choice(list(range(n))) for _ in range(50)]
+    lst = list(range(n))
+    rs.shuffle(lst)
+    nxt = int(rs.randint(0, 2**32, dtype=np.uint64))
+    hch, hperm, hnext = H.np_ops(seed, n, 50)
+    assert list(hch) == ch
+    assert list(hperm) == lst
+    assert hnext == nxt
+
+
+@pytest.mark.parametrize("k", [0, 1, 100, 623, 624, 625, 1500])
+def test_numpy_state_roundtrip(k):
+  rs = np.random.RandomState(9)
+  rs.randint(0, 2**32, size=37, dtype=np.uint64)  # mid-block position
+  st = rs.get_state()
+  out, key, pos = H.mt_roundtrip(st[1], st[2], k)
+  ref = rs.randint(0, 2**32, size=k, dtype=np.uint64).astype(np.uint32)
+  assert np.array_equal(out, ref)
+  st2 = rs.get_state()
+  assert pos == st2[2]
+  assert np.array_equal(key, st2[1])
