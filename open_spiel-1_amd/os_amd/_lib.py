@@ -26,6 +26,30 @@ if not os.path.exists(LIB_PATH):
       "libos_mcts.so not found at %s: run `python -c \"import __graft_entry__ as g;"
       " g.build()\"` to compile the HIP engine (no CPU fallback exists)" % LIB_PATH)
 
+def _share_torch_hip_runtime():
+  """Makes libos_mcts.so bind to the HIP/HSA runtime PyTorch ships, if any.
+
+  A process must hold ONE HIP runtime: PyTorch-ROCm bundles its own
+  libamdhip64 / libhsa-runtime64 (same SONAMEs as /opt/rocm's), and a second
+  copy loaded beside it cannot open the device.  Preloading torch's copies
+  RTLD_GLOBAL (without importing torch) lets the dynamic loader resolve our
+  NEEDED entries by SONAME to them, whichever of torch / os_amd is imported
+  first.  Set OS_AMD_HIP_RUNTIME=system to skip (processes without torch).
+  """
+  if os.environ.get("OS_AMD_HIP_RUNTIME", "torch") == "system":
+    return
+  import importlib.util
+  spec = importlib.util.find_spec("torch")
+  if spec is None or not spec.submodule_search_locations:
+    return
+  tlib = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+  for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+    p = os.path.join(tlib, name)
+    if os.path.exists(p):
+      ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+
+
+_share_torch_hip_runtime()
 lib = ctypes.CDLL(LIB_PATH)
 
 _vp = ctypes.c_void_p
