@@ -66,6 +66,8 @@ struct DevArgs {
   uint32_t* mt;           // [num_roots][2][624]
   void* arena;            // [num_roots][cap] Node<R>
   uint32_t cap;
+  int32_t path_cap;       // >= MaxGameLength + 1 (LDS path slice per lane)
+  int32_t child_cap;      // >= max |LegalActions| (LDS expansion slice)
   int32_t import_state;   // numpy (key, pos) import / export
   int32_t shared_stream;  // numpy: one RandomState for bot + evaluator
   int32_t* mt_pos;        // [total][2] in/out when import_state
@@ -119,31 +121,46 @@ __global__ void k_mcts(DevArgs a) {
   const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (lr >= a.num_roots) return;
   const int64_t gr = a.root_base + lr;
-  uint32_t* mt0 = a.mt + lr * 2 * kMtN;
+  // Per-lane LDS slices: [blockDim][2][624] MT19937 words, then
+  // [blockDim][path_cap] u32 visit path, then [blockDim][child_cap] u16
+  // expansion buffer.  Every per-simulation random word and path entry is an
+  // LDS access (~tens of cycles) instead of a dependent HBM/L2 round trip.
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int nb = blockDim.x;
+  const int lane = threadIdx.x;
+  uint32_t* mt0 = reinterpret_cast<uint32_t*>(smem) + lane * 2 * kMtN;
+  PathEnt<R>* path =
+      reinterpret_cast<PathEnt<R>*>(smem + static_cast<size_t>(nb) * 2 * kMtN * 4) +
+      lane * a.path_cap;
+  uint16_t* actbuf =
+      reinterpret_cast<uint16_t*>(
+          smem + static_cast<size_t>(nb) * (2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>))) +
+      lane * a.child_cap;
   MtStream bot{mt0, kMtN, 0};
   MtStream ev{mt0 + kMtN, kMtN, 0};
+  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
   if (a.import_state) {
+    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = 0; i < 2 * kMtN; ++i) mt0[i] = g0[i];
     bot.idx = a.mt_pos[2 * gr];
     bot.pre = 1;
     ev.idx = a.mt_pos[2 * gr + 1];
     ev.pre = 1;
   } else {
     mt_seed(bot.s, a.bot_seeds[gr]);
-    if (!(Policy == kPolicyNumpy && a.shared_stream)) mt_seed(ev.s, a.eval_seeds[gr]);
+    if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
   }
   const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
   uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
   typename G::Ctx ctx = CtxMaker<G>::make(a, gr, glog);
-  uint32_t path[kMaxPath];
-  uint16_t actbuf[kMaxChildren];
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   SearchResult res;
   if (Policy == kPolicyNumpy && a.shared_stream)
     res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
-                                    path, actbuf);
+                                    path, actbuf, a.path_cap);
   else
     res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
-                                    path, actbuf);
+                                    path, actbuf, a.path_cap);
   res.rng_words = bot.words + ((Policy == kPolicyNumpy && a.shared_stream) ? 0u : ev.words);
   a.results[gr] = res;
   const Node<R>& rn = nodes[0];
@@ -172,6 +189,8 @@ __global__ void k_mcts(DevArgs a) {
       ev.finalize();
       a.mt_pos[2 * gr + 1] = ev.idx;
     }
+    uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = 0; i < 2 * kMtN; ++i) g0[i] = mt0[i];
   }
 }
 
@@ -313,15 +332,31 @@ bool ReplayRoot(const HostGame& g, const int64_t* a, int64_t n, HostState* s,
   return true;
 }
 
+constexpr size_t kLdsBytes = 160 * 1024;  // LDS per CU on gfx950
+constexpr int kDefaultBlock = 16;           // searches (lanes) per workgroup
+
+template <class R>
+size_t LdsPerLane(int path_cap, int child_cap) {
+  return static_cast<size_t>(2 * kMtN * 4) + path_cap * sizeof(PathEnt<R>) +
+         static_cast<size_t>(child_cap) * 2;
+}
+
 template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
-  const int bs = e->params.block_size > 0 ? e->params.block_size : 64;
+  int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
+  const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
+  if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
+  if (bs < 1) return Fail(OS_ERR_CAPACITY, "per-lane LDS slice exceeds the CU's LDS");
+  const size_t lds = per_lane * bs;
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mcts<G, R, Policy>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)));
   for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
     a.root_base = base;
     a.num_roots = n;
     const unsigned grid = static_cast<unsigned>((n + bs - 1) / bs);
-    hipLaunchKernelGGL((k_mcts<G, R, Policy>), dim3(grid), dim3(bs), 0, stream, a);
+    hipLaunchKernelGGL((k_mcts<G, R, Policy>), dim3(grid), dim3(bs), lds, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess)
       return Fail(OS_ERR_DEVICE, std::string("k_mcts launch failed: ") +
@@ -478,6 +513,9 @@ DevArgs MakeArgs(os_engine* e) {
   a.mt = static_cast<uint32_t*>(e->d_mt.p);
   a.arena = e->d_arena.p;
   a.cap = e->cap;
+  // Paths hold depth + 1 <= MaxGameLength + 1 nodes; keep slices 4-byte even.
+  a.path_cap = e->game.cfg.max_game_length + 2;
+  a.child_cap = (e->game.cfg.max_children + 1) & ~1;
   a.import_state = e->import_state ? 1 : 0;
   a.shared_stream = e->shared_stream ? 1 : 0;
   a.mt_pos = static_cast<int32_t*>(e->d_pos.p);

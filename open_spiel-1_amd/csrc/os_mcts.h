@@ -157,15 +157,28 @@ OS_HD int garbage_collect(Node<R>* nodes, uint32_t used, uint32_t cap, int limit
   return kOk;
 }
 
+// One entry of the current simulation's visit path (mcts.cc visit_path).
+// Selection records each visited node's statistics as it reads them while
+// scanning the parent's children, so backup only stores (no dependent global
+// loads), and entry 0 (the root) persists across simulations.
+template <class R>
+struct PathEnt {
+  uint32_t idx;    // arena index
+  uint32_t first;  // first child (valid iff nc > 0)
+  int32_t n;       // explore_count before this simulation's backup
+  int32_t nc;      // nchild
+  R w;             // total_reward before this simulation's backup
+};
+
 // One complete search from `root`.  `bot` and `ev` are the two MT19937
 // streams (the same object under kPolicyNumpy).  `actbuf` holds >=
-// kMaxChildren entries, `path` >= kMaxPath.
+// max_children entries, `path` >= path_cap >= MaxGameLength + 1 entries.
 template <class G, class R, int Policy, class Rng>
 OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
                                const typename G::State& root,
                                typename G::Ctx& ctx, Node<R>* nodes,
-                               uint32_t cap, Rng& bot, Rng& ev, uint32_t* path,
-                               uint16_t* actbuf) {
+                               uint32_t cap, Rng& bot, Rng& ev, PathEnt<R>* path,
+                               uint16_t* actbuf, int path_cap) {
   SearchResult res;
   res.status = kOk;
   res.sims = 0;
@@ -179,6 +192,12 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
   nodes[0].action = 0;
   nodes[0].nchild = 0;
   nodes[0].out = kUnsolved;
+  path[0].idx = 0;
+  path[0].first = 0;
+  path[0].n = 0;
+  path[0].nc = 0;
+  path[0].w = 0;
+  int8_t root_out = kUnsolved;
   uint32_t used = 1;
   int nodes_count = 1;
   int gc_limit = 5;
@@ -187,12 +206,21 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
   for (int sim = 0; sim < sp.max_simulations; ++sim) {
     typename G::State s = root;
     ctx.reset();
-    uint32_t cur = 0;
+    // Current node, carried from the parent's child scan.
+    uint32_t cur_idx = 0;
+    uint32_t cur_first = path[0].first;
+    int32_t cur_n = path[0].n;
+    int cur_nc = path[0].nc;
     int depth = 0;
-    path[0] = 0;
-    // ---- selection / expansion (ApplyTreePolicy) ----
-    while (!G::terminal(s, g) && nodes[cur].n > 0) {
-      if (nodes[cur].nchild == 0) {
+    // ---- selection / expansion (ApplyTreePolicy, mcts.cc:255-323) ----
+    while (!G::terminal(s, g) && cur_n > 0) {
+      int chosen;
+      uint16_t c_action;
+      uint32_t c_first;
+      int32_t c_n;
+      int c_nc;
+      R c_w;
+      if (cur_nc == 0) {
         const typename G::Legal l = G::legal(s, g, ctx);
         const int nc = l.count;
         for (int k = 0; k < nc; ++k) actbuf[k] = static_cast<uint16_t>(l.kth(k));
@@ -213,41 +241,67 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
           c.nchild = 0;
           c.out = kUnsolved;
         }
-        nodes[cur].first = first;
-        nodes[cur].nchild = static_cast<uint8_t>(nc);
+        nodes[cur_idx].first = first;
+        nodes[cur_idx].nchild = static_cast<uint8_t>(nc);
+        path[depth].first = first;
+        path[depth].nc = nc;
         nodes_count += nc;
         res.expanded += nc;
-      }
-      const Node<R>& pn = nodes[cur];
-      const int cp = P0 ^ (depth & 1);  // player choosing at this node
-      const double logN = sp.log_lut[pn.n];
-      double best = -inf;
-      int chosen = 0;
-      res.scanned += pn.nchild;
-      for (int k = 0; k < pn.nchild; ++k) {
-        const Node<R>& c = nodes[pn.first + k];
-        double v;
-        if (c.out != kUnsolved) {
-          v = outcome_for(c.out, cp);
-        } else if (c.n == 0) {
-          v = inf;
-        } else {
-          const double dn = static_cast<double>(c.n);
-          v = static_cast<double>(c.w) / dn + sp.uct_c * __builtin_sqrt(logN / dn);
+        cur_first = first;
+        cur_nc = nc;
+        // Every fresh child is unvisited and unsolved (UCT +inf), so the
+        // strict '>' scan of mcts.cc:310 picks the first one.
+        chosen = 0;
+        c_action = actbuf[0];
+        c_first = 0;
+        c_n = 0;
+        c_nc = 0;
+        c_w = 0;
+      } else {
+        const int cp = P0 ^ (depth & 1);  // player choosing at this node
+        const double logN = sp.log_lut[cur_n];
+        double best = -inf;
+        chosen = 0;
+        res.scanned += cur_nc;
+        Node<R> bc = nodes[cur_first];
+        for (int k = 0; k < cur_nc; ++k) {
+          const Node<R> c = nodes[cur_first + k];
+          double v;
+          if (c.out != kUnsolved) {
+            v = outcome_for(c.out, cp);
+          } else if (c.n == 0) {
+            v = inf;
+          } else {
+            const double dn = static_cast<double>(c.n);
+            v = static_cast<double>(c.w) / dn + sp.uct_c * __builtin_sqrt(logN / dn);
+          }
+          if (v > best) {
+            best = v;
+            chosen = k;
+            bc = c;
+          }
         }
-        if (v > best) {
-          best = v;
-          chosen = k;
-        }
+        c_action = bc.action;
+        c_first = bc.first;
+        c_n = bc.n;
+        c_nc = bc.nchild;
+        c_w = bc.w;
       }
-      const uint32_t nxt = pn.first + chosen;
-      G::apply(s, g, ctx, nodes[nxt].action);
-      cur = nxt;
-      if (++depth >= kMaxPath) {
+      G::apply(s, g, ctx, c_action);
+      if (++depth >= path_cap) {
         res.status = kPathOverflow;
         goto done;
       }
-      path[depth] = cur;
+      cur_idx = cur_first + chosen;
+      cur_first = c_first;
+      cur_n = c_n;
+      cur_nc = c_nc;
+      PathEnt<R>& pe = path[depth];
+      pe.idx = cur_idx;
+      pe.first = c_first;
+      pe.n = c_n;
+      pe.nc = c_nc;
+      pe.w = c_w;
     }
     if (depth > res.max_depth) res.max_depth = depth;
     // ---- evaluation ----
@@ -256,7 +310,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
       R rv0, rv1;
       if (G::terminal(s, g)) {
         const int r0 = G::ret0(s, g, ctx);
-        nodes[cur].out = static_cast<int8_t>(r0);
+        nodes[cur_idx].out = static_cast<int8_t>(r0);
+        if (depth == 0) root_out = static_cast<int8_t>(r0);
         solved = sp.solve != 0;
         rv0 = static_cast<R>(r0);
         rv1 = static_cast<R>(-r0);
@@ -279,31 +334,37 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
       }
       // ---- backup + MCTS-Solver (mcts.cc:351-396) ----
       for (int d = depth; d >= 0; --d) {
-        Node<R>& nd = nodes[path[d]];
+        PathEnt<R>& pe = path[d];
         const int pl = d == 0 ? P0 : (P0 ^ ((d - 1) & 1));
-        nd.w += pl == 0 ? rv0 : rv1;
-        nd.n += 1;
+        pe.w += pl == 0 ? rv0 : rv1;
+        pe.n += 1;
+        Node<R>& nd = nodes[pe.idx];
+        nd.n = pe.n;
+        nd.w = pe.w;
         res.backed += 1;
-        if (solved && nd.nchild > 0) {
+        if (solved && pe.nc > 0) {
           const int cpl = P0 ^ (d & 1);
-          res.solver_scanned += nd.nchild;
+          res.solver_scanned += pe.nc;
           int best = -1;
+          int8_t best_out = kUnsolved;
           double bestv = 0.0;
           bool all_solved = true;
-          for (int k = 0; k < nd.nchild; ++k) {
-            const Node<R>& c = nodes[nd.first + k];
-            if (c.out == kUnsolved) {
+          for (int k = 0; k < pe.nc; ++k) {
+            const int8_t co = nodes[pe.first + k].out;
+            if (co == kUnsolved) {
               all_solved = false;
             } else {
-              const double v = outcome_for(c.out, cpl);
+              const double v = outcome_for(co, cpl);
               if (best < 0 || v > bestv) {
                 best = k;
                 bestv = v;
+                best_out = co;
               }
             }
           }
           if (best >= 0 && (all_solved || bestv == 1.0)) {
-            nd.out = nodes[nd.first + best].out;
+            nd.out = best_out;
+            if (d == 0) root_out = best_out;
           } else {
             solved = false;
           }
@@ -311,9 +372,9 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
       }
     }
     res.sims = sim + 1;
-    if (nodes[0].out != kUnsolved) break;
+    if (root_out != kUnsolved) break;
     if (Policy == kPolicyCpp) {
-      if (nodes[0].nchild == 1) break;
+      if (path[0].nc == 1) break;
       if (sp.max_nodes > 1 && nodes_count >= sp.max_nodes) {
         const int st = garbage_collect(nodes, used, cap, gc_limit, &nodes_count);
         if (st != kOk) {
@@ -324,6 +385,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         gc_limit = static_cast<int>(gc_limit *
                                     (nodes_count > sp.max_nodes / 2 ? 1.25 : 0.9));
         if (gc_limit < 5) gc_limit = 5;
+        path[0].nc = nodes[0].nchild;  // the root may have lost its children
+        path[0].first = nodes[0].first;
       }
     }
   }
@@ -332,6 +395,7 @@ done:
   res.used = used;
   return res;
 }
+
 
 }  // namespace osm
 

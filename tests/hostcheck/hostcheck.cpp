@@ -26,7 +26,7 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
   MtStream bot{mt.data(), kMtN, 0}, ev{mt.data() + kMtN, kMtN, 0};
   mt_seed(bot.s, bot_seed);
   mt_seed(ev.s, eval_seed);
-  uint32_t path[kMaxPath];
+  PathEnt<R> path[kMaxPath];
   uint16_t actbuf[kMaxChildren];
   typename G::Ctx ctx;
   std::vector<uint64_t> storage;
@@ -45,7 +45,7 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
   }
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
   SearchResult res = mcts_search<G, R, Policy>(game.cfg, sp, rs, ctx, nodes.data(), cap,
-                                               bot, ev, path, actbuf);
+                                               bot, ev, path, actbuf, kMaxPath);
   if (res.status != kOk) {
     g_err = "search status " + std::to_string(res.status);
     return -4;
