@@ -32,6 +32,10 @@ CONFIGS = {
 }
 
 
+LAYOUTS = {}
+KERNEL = {"wave": "k_wsearch", "lane": "k_mcts"}
+
+
 def parse():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
@@ -42,6 +46,8 @@ def parse():
   ap.add_argument("--sims", type=int, default=0, help="override simulations")
   ap.add_argument("--block", type=int, default=0, help="lanes per workgroup")
   ap.add_argument("--arena-nodes", type=int, default=0)
+  ap.add_argument("--layout", default="wave", choices=("wave", "lane"),
+                  help="search kernel: one wave per search / one lane per search")
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
                   help="target CPU-baseline sample duration")
@@ -54,6 +60,8 @@ def main():
   import torch
   import torch.distributed as dist
   from os_amd import engine as E
+  from os_amd import _lib
+  LAYOUTS.update(wave=_lib.LAYOUT_WAVE, lane=_lib.LAYOUT_LANE)
 
   world = int(os.environ.get("WORLD_SIZE", "1"))
   rank = int(os.environ.get("RANK", "0"))
@@ -69,7 +77,7 @@ def main():
   sims = args.sims or sims
   params = dict(uct_c=2.0, max_simulations=sims, n_rollouts=1,
                 max_memory_mb=1000, solve=True, block_size=args.block,
-                arena_nodes=args.arena_nodes)
+                arena_nodes=args.arena_nodes, layout=LAYOUTS[args.layout])
   base = rank * R  # global root ids of this rank
   acts, offs = E.make_roots(game, R, seed_base=1000 + base, max_plies=plies)
   gid = np.arange(base, base + R, dtype=np.uint32)
@@ -134,7 +142,7 @@ def main():
 
   if rank == 0:
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
-    traffic = pmc_traffic()
+    traffic = pmc_traffic(KERNEL[args.layout], game)
     line = {
         "metric": "MCTS simulations/sec (random rollout) on connect_four at "
                   "1/2/4/8 MI355X" if args.config == "c2" else
@@ -157,7 +165,8 @@ def main():
             "uct_c": 2.0, "n_rollouts": 1, "solve": True,
             "max_memory_mb": 1000, "root_plies": "k~U[0,%d] from mt19937(1000+i)" % plies,
             "parallelism": "dp%d (independent roots, no collective)" % world,
-            "block_size": args.block or 64,
+            "layout": args.layout,
+            "block_size": args.block or (64 if args.layout == "wave" else 16),
             "sims_per_step_per_gpu": sims_per_step,
         },
         "roofline": {
@@ -167,7 +176,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "k_mcts",
+            "kernel": KERNEL[args.layout],
             "kernel_ms_per_launch": kernel_ms,
             "algorithmic_bytes_per_launch": alg_bytes,
             "algorithmic_bytes_per_sim": alg_bytes / max(sims_per_step, 1),
@@ -205,14 +214,15 @@ def cpu_baseline(game, acts, offs, bot_seeds, eval_seeds, sims, seconds):
                     (want, R, sims, n, secs, threads)}
 
 
-def pmc_traffic():
-  """HBM bytes per k_mcts launch from the committed rocprofv3 PMC summary."""
-  path = os.path.join(ROOT, "profiles", "pmc_k_mcts.json")
+def pmc_traffic(kernel, game):
+  """HBM bytes per launch of `kernel` on `game` from the committed rocprofv3
+  PMC summary (profiles/pmc_traffic.json, written by tools/pmc_summary.py)."""
+  path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
   if not os.path.exists(path):
     return None
   with open(path) as f:
     d = json.load(f)
-  return d.get("hbm_bytes_per_launch")
+  return d.get("%s/%s" % (kernel, game), {}).get("hbm_bytes_per_launch")
 
 
 if __name__ == "__main__":

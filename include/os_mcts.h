@@ -90,6 +90,11 @@ int64_t os_state_action_to_string(const os_state* s, int32_t player,
 int os_engine_create(const char* game_string, int32_t device, os_engine** out);
 int os_engine_destroy(os_engine* e);
 
+/* Kernel layouts: one 64-lane wavefront per search (lanes scan children, twist
+ * MT19937, back up the path in parallel), or one lane per search. */
+#define OS_LAYOUT_WAVE 0
+#define OS_LAYOUT_LANE 1
+
 #define OS_POLICY_CPP 0    /* mcts.cc: std::mt19937 bot + evaluator streams   */
 #define OS_POLICY_NUMPY 1  /* mcts.py: numpy RandomState (shared or separate) */
 
@@ -100,8 +105,8 @@ typedef struct {
   int64_t max_memory_mb;        /* MCTSBot max_memory_mb (drives GC, mcts.cc:402) */
   int32_t solve;                /* MCTSBot solve (MCTS-Solver backup) */
   int32_t policy;               /* OS_POLICY_* */
-  int32_t block_size;           /* 0 = default; lanes per workgroup */
-  int32_t pad;
+  int32_t block_size;           /* OS_LAYOUT_LANE only: lanes per workgroup (0 = default) */
+  int32_t layout;               /* OS_LAYOUT_WAVE (default) or OS_LAYOUT_LANE */
   int64_t arena_nodes;          /* 0 = exact worst case; else nodes per root */
 } os_mcts_params;
 
@@ -147,6 +152,9 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
 int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
                       int64_t n_actions, int64_t n, int32_t n_rollouts,
                       const uint32_t* seeds, double* out_returns);
+/* Kernel layout for os_rollouts_batch: OS_LAYOUT_WAVE (default: one wave per
+ * evaluator, uniform game code) or OS_LAYOUT_LANE (one lane per evaluator). */
+int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
 
 /* ---- Device-resident pipeline (inputs already in HBM; for benchmarks) ---
  * prepare: upload roots + seeds and size the arena; run: launch the search
@@ -183,6 +191,13 @@ int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base
 
 /* Library/kernel build info string (arch, build flags). */
 const char* os_build_info(void);
+
+/* Diagnostic (no reference counterpart): shader-clock cycles per search phase
+ * of the wave-layout kernel summed over all waves since the last call
+ * (select, expand, rollout, backup, solver, tail, mt-twist, total), then reset.
+ * Returns the number of phases written; OS_ERR_UNSUPPORTED unless the library
+ * was built with -DOS_PHASE_TIMING=1. */
+int os_debug_phase_cycles(uint64_t* out, int32_t n);
 
 #ifdef __cplusplus
 }

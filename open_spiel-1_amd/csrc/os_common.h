@@ -54,6 +54,21 @@ OS_HD int select64(uint64_t x, int k) {
   return base;
 }
 
+// Player-indexed pairs without dynamic indexing: a[p] with a runtime p would
+// force the whole state into private (scratch) memory on the GPU; selects keep
+// it in registers (SGPRs when the player is wave-uniform).
+template <class T>
+OS_HD T pick(const T* a, int i) {
+  return i ? a[1] : a[0];
+}
+template <class T>
+OS_HD void put(T* a, int i, T v) {
+  const T v0 = i ? a[0] : v;
+  const T v1 = i ? v : a[1];
+  a[0] = v0;
+  a[1] = v1;
+}
+
 // 128-bit bitboard (two u64 words).  Bit i = cell i.
 struct B128 {
   uint64_t lo, hi;

@@ -22,6 +22,7 @@
 #include "../../include/os_mcts.h"
 #include "os_host.h"
 #include "os_mcts.h"
+#include "os_wave.h"
 
 using namespace osm;
 
@@ -54,6 +55,10 @@ struct os_state {
 namespace {
 
 constexpr int kGoLogCap = 248;  // >= 2 * 11 * 11 + 4
+
+#if OS_PHASE_TIMING
+__device__ uint64_t g_phase_cycles[kNumPhases];  // diagnostic build only
+#endif
 
 struct DevArgs {
   GameCfg cfg;
@@ -106,12 +111,7 @@ struct CtxMaker<Go> {
     c.log = log;
     c.n_log = 0;
     c.cap = kGoLogCap;
-    for (int i = 0; i < 4; ++i) c.base_filt[i] = 0;
-    for (int i = 0; i < c.n_base; ++i) {
-      const int b = GoCtx::fbit(c.base[i]);
-      c.base_filt[b >> 6] |= 1ull << (b & 63);
-    }
-    for (int i = 0; i < 4; ++i) c.filt[i] = c.base_filt[i];
+    c.init_filters();
     return c;
   }
 };
@@ -194,6 +194,115 @@ __global__ void k_mcts(DevArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-search kernel (default layout): one 64-lane workgroup per search.
+template <class G>
+struct WaveCtxMaker {
+  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct WaveCtxMaker<Go> {
+  __device__ static GoWaveCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+
+template <class G, class R>
+__host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
+  return static_cast<size_t>(2 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
+}
+
+template <class G, class R, int Policy>
+__global__ __launch_bounds__(64) void k_wsearch(DevArgs a) {
+  const int64_t lr = blockIdx.x;
+  if (lr >= a.num_roots) return;
+  const int64_t gr = a.root_base + lr;
+  const int l = lane_id();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4);
+  uint64_t* glog = reinterpret_cast<uint64_t*>(
+      smem + ((2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
+  WaveMt bot, ev;
+  bot.s = mt;
+  ev.s = mt + kMtN;
+  if (a.import_state) {
+    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = l; i < 2 * kMtN; i += 64) mt[i] = g0[i];
+    __syncthreads();
+    bot.init_import(a.mt_pos[2 * gr]);
+    ev.init_import(a.mt_pos[2 * gr + 1]);
+  } else {
+    if (l == 0) {
+      mt_seed(bot.s, a.bot_seeds[gr]);
+      if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
+    }
+    __syncthreads();
+    bot.init_seeded();
+    ev.init_seeded();
+  }
+  const typename G::State root =
+      make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
+  typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr, glog);
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  PhaseCycles ph = {};
+  SearchResult res = shared
+      ? wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
+                                  a.path_cap, ph)
+      : wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                                  a.path_cap, ph);
+  res.rng_words = bot.words + (shared ? 0u : ev.words);
+#if OS_PHASE_TIMING
+  ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);
+  if (l == 0)
+    for (int i = 0; i < kNumPhases; ++i)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&g_phase_cycles[i]),
+                static_cast<unsigned long long>(ph.c[i]));
+#endif
+  __threadfence_block();
+  const Node<R> rn = nodes[0];
+  const int P0 = G::to_move(root);
+  const int nc = rn.nchild;
+  const int64_t ob = gr * a.max_children;
+  for (int k = l; k < nc && k < a.max_children; k += 64) {
+    const Node<R> c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = static_cast<double>(c.w);
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  if (l == 0) {
+    a.results[gr] = res;
+    a.nchild[gr] = nc;
+    a.root_n[gr] = rn.n;
+    a.root_w[gr] = static_cast<double>(rn.w);
+    a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
+                                         : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+    const int b = best_child(nodes, P0);
+    a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+  }
+  if (a.import_state) {
+    if (l == 0) {
+      a.mt_pos[2 * gr] = bot.export_pos();
+      if (!shared) a.mt_pos[2 * gr + 1] = ev.export_pos();
+    }
+    __syncthreads();
+    uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = l; i < 2 * kMtN; i += 64) g0[i] = mt[i];
+  }
+}
+
 struct RollArgs {
   GameCfg cfg;
   int64_t n;
@@ -221,15 +330,56 @@ struct RollCtx<Go> {
     c.log = log;
     c.n_log = 0;
     c.cap = kGoLogCap;
-    for (int i = 0; i < 4; ++i) c.base_filt[i] = 0;
-    for (int i = 0; i < c.n_base; ++i) {
-      const int b = GoCtx::fbit(c.base[i]);
-      c.base_filt[b >> 6] |= 1ull << (b & 63);
-    }
-    for (int i = 0; i < 4; ++i) c.filt[i] = c.base_filt[i];
+    c.init_filters();
     return c;
   }
 };
+
+template <class G>
+struct WaveRollCtx {
+  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct WaveRollCtx<Go> {
+  __device__ static GoWaveCtx make(const RollArgs& a, uint64_t* log) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes;
+    c.n_base = a.n_root_hashes;
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+
+// One wave per RandomRolloutEvaluator (n_rollouts playouts from the root).
+template <class G>
+__global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
+  const int64_t i = blockIdx.x;
+  if (i >= a.n) return;
+  __shared__ uint32_t mt[kMtN];
+  __shared__ uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
+  WaveMt ev;
+  ev.s = mt;
+  if (lane_id() == 0) mt_seed(mt, a.seeds[i]);
+  __syncthreads();
+  ev.init_seeded();
+  typename WaveCtxOf<G>::type ctx = WaveRollCtx<G>::make(a, glog);
+  const typename G::State root = make_uniform(*static_cast<const typename G::State*>(a.root));
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < a.n_rollouts; ++k) {
+    ctx.reset();
+    const int r0 = wave_rollout<G, kPolicyCpp>(root, a.cfg, ctx, ev);
+    s0 += static_cast<double>(r0);
+    s1 += static_cast<double>(-r0);
+  }
+  if (lane_id() == 0) {
+    a.out[2 * i] = s0 / a.n_rollouts;
+    a.out[2 * i + 1] = s1 / a.n_rollouts;
+  }
+}
 
 template <class G>
 __global__ void k_rollouts(RollArgs a) {
@@ -297,6 +447,7 @@ struct os_engine {
   int32_t hash_stride = 1;
   bool import_state = false;
   bool shared_stream = false;
+  int32_t rollout_layout = OS_LAYOUT_WAVE;
   DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out;
@@ -342,7 +493,29 @@ size_t LdsPerLane(int path_cap, int child_cap) {
 }
 
 template <class G, class R, int Policy>
+int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
+  const size_t lds = WaveLdsBytes<G, R>(a.path_cap);
+  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsearch<G, R, Policy>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)));
+  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+    a.root_base = base;
+    a.num_roots = n;
+    hipLaunchKernelGGL((k_wsearch<G, R, Policy>), dim3(static_cast<unsigned>(n)), dim3(64),
+                       lds, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+      return Fail(OS_ERR_DEVICE, std::string("k_wsearch launch failed: ") +
+                                     hipGetErrorString(err));
+  }
+  return OS_OK;
+}
+
+template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
+  if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
   const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
   if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
@@ -384,6 +557,8 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
     return Fail(OS_ERR_INVALID, "unknown policy");
   if (p->block_size < 0 || p->block_size > 1024)
     return Fail(OS_ERR_INVALID, "block_size must be in [0, 1024]");
+  if (p->layout != OS_LAYOUT_WAVE && p->layout != OS_LAYOUT_LANE)
+    return Fail(OS_ERR_INVALID, "unknown layout");
   if (e->game.cfg.max_children > kMaxChildren)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxChildren");
   if (e->game.cfg.max_game_length >= kMaxPath)
@@ -641,9 +816,13 @@ int LaunchRollouts(os_engine* e, const HostState& root, int64_t n, int32_t nr,
     a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
     a.n_root_hashes = static_cast<int32_t>(root.hashes.size());
   }
-  const int bs = 64;
-  hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                     dim3(bs), 0, 0, a);
+  if (e->rollout_layout == OS_LAYOUT_WAVE) {
+    hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, 0, a);
+  } else {
+    const int bs = 64;
+    hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
+                       dim3(bs), 0, 0, a);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, e->d_rollout_out.p, n * 16, hipMemcpyDeviceToHost));
@@ -657,6 +836,22 @@ int LaunchRollouts(os_engine* e, const HostState& root, int64_t n, int32_t nr,
 extern "C" {
 
 const char* os_last_error(void) { return g_err.c_str(); }
+
+int os_debug_phase_cycles(uint64_t* out, int32_t n) {
+#if OS_PHASE_TIMING
+  if (!out || n < kNumPhases) return Fail(OS_ERR_INVALID, "need kNumPhases slots");
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(uint64_t) * kNumPhases));
+  std::vector<uint64_t> zero(kNumPhases, 0);
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero.data(),
+                            sizeof(uint64_t) * kNumPhases));
+  return kNumPhases;
+#else
+  (void)out;
+  (void)n;
+  return Fail(OS_ERR_UNSUPPORTED, "built without -DOS_PHASE_TIMING=1");
+#endif
+}
 
 const char* os_build_info(void) {
   return "libos_mcts: gfx950 search/rollout kernels, one lane per search, "
@@ -804,6 +999,14 @@ int os_engine_fetch(os_engine* e, int32_t max_children, int32_t* child_action,
 }
 
 int64_t os_engine_last_sims(os_engine* e) { return e ? e->last_sims : -1; }
+
+int os_engine_set_rollout_layout(os_engine* e, int32_t layout) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (layout != OS_LAYOUT_WAVE && layout != OS_LAYOUT_LANE)
+    return Fail(OS_ERR_INVALID, "unknown layout");
+  e->rollout_layout = layout;
+  return OS_OK;
+}
 
 int os_engine_stats(os_engine* e, int64_t* out) {
   if (!e || !out) return Fail(OS_ERR_INVALID, "null argument");

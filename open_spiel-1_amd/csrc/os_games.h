@@ -93,8 +93,9 @@ struct TicTacToe {
   }
   OS_HD static void apply(State& s, const GameCfg&, Ctx&, int a) {
     const int p = s.to_play;
-    s.b[p] = static_cast<uint16_t>(s.b[p] | (1u << a));
-    if (line(s.b[p])) s.winner = static_cast<int8_t>(p);
+    const uint16_t mine = static_cast<uint16_t>(pick(s.b, p) | (1u << a));
+    put(s.b, p, mine);
+    if (line(mine)) s.winner = static_cast<int8_t>(p);
     s.to_play = static_cast<uint8_t>(1 - p);
     s.moves++;
   }
@@ -155,9 +156,10 @@ struct ConnectFour {
     const uint64_t occ = s.bb[0] | s.bb[1];
     const uint64_t colmask = 0x3Full << (7 * col);
     const uint64_t mv = (occ + (1ull << (7 * col))) & colmask;
-    s.bb[p] |= mv;
+    const uint64_t mine = pick(s.bb, p) | mv;
+    put(s.bb, p, mine);
     s.moves++;
-    if (has_four(s.bb[p])) s.outcome = static_cast<int8_t>(p);
+    if (has_four(mine)) s.outcome = static_cast<int8_t>(p);
     else if (s.moves == 42) s.outcome = 2;
     s.to_play = static_cast<uint8_t>(1 - p);
   }
@@ -230,7 +232,7 @@ struct Breakthrough {
   OS_HD static int to_move(const State& s) { return s.to_play; }
   OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
     const int p = s.to_play;
-    const uint64_t own = s.pc[p], opp = s.pc[1 - p];
+    const uint64_t own = pick(s.pc, p), opp = pick(s.pc, 1 - p);
     const uint64_t E = g.board64 & ~(own | opp);
     const uint64_t EO = E | opp;
     const int c = g.cols;
@@ -259,8 +261,10 @@ struct Breakthrough {
     const int dc = (dir % 3) - 1;
     const int tgt = src + dr * g.cols + dc;
     const uint64_t tb = 1ull << tgt;
-    s.pc[1 - p] &= ~tb;
-    s.pc[p] = (s.pc[p] & ~(1ull << src)) | tb;
+    const uint64_t own = (pick(s.pc, p) & ~(1ull << src)) | tb;
+    const uint64_t opp = pick(s.pc, 1 - p) & ~tb;
+    s.pc[0] = p ? opp : own;
+    s.pc[1] = p ? own : opp;
     const int trow = tgt / g.cols;
     if (p == 0 && trow == g.rows - 1) s.winner = 0;
     else if (p == 1 && trow == 0) s.winner = 1;
@@ -304,7 +308,8 @@ struct Hex {
     return r & g.board;
   }
   OS_HD static void init(State& s, const GameCfg&) {
-    for (int p = 0; p < 2; ++p) s.st[p] = s.ea[p] = s.eb[p] = b128(0, 0);
+    s.st[0] = s.ea[0] = s.eb[0] = b128(0, 0);
+    s.st[1] = s.ea[1] = s.eb[1] = b128(0, 0);
     s.win_cell = -1; s.result = 0; s.to_play = 0; s.moves = 0; s.pad = 0;
   }
   OS_HD static bool terminal(const State& s, const GameCfg&) { return s.result != 0; }
@@ -328,8 +333,8 @@ struct Hex {
       eb = !ea && (m % n) == n - 1;
     }
     const B128 nb = nbr6(bit128(m), g);
-    ea |= any(nb & s.ea[p]);
-    eb |= any(nb & s.eb[p]);
+    ea |= any(nb & pick(s.ea, p));
+    eb |= any(nb & pick(s.eb, p));
     *a = ea;
     *b = eb;
   }
@@ -338,20 +343,22 @@ struct Hex {
     bool a, b;
     edges_if(s, g, p, m, &a, &b);
     const B128 mb = bit128(m);
-    s.st[p] = s.st[p] | mb;
+    const B128 st = pick(s.st, p) | mb;
+    put(s.st, p, st);
     if (a && b) {
       s.result = static_cast<int8_t>(p == 0 ? 1 : -1);
       s.win_cell = static_cast<int16_t>(m);
     } else if (a || b) {
-      const B128 plain = s.st[p] & ~s.ea[p] & ~s.eb[p];
+      const B128 ea = pick(s.ea, p), eb = pick(s.eb, p);
+      const B128 plain = st & ~ea & ~eb;
       B128 comp = mb;
       for (;;) {
         B128 nx = comp | (nbr6(comp, g) & plain);
         if (nx == comp) break;
         comp = nx;
       }
-      if (a) s.ea[p] = s.ea[p] | comp;
-      else s.eb[p] = s.eb[p] | comp;
+      if (a) put(s.ea, p, ea | comp);
+      else put(s.eb, p, eb | comp);
     }
     s.to_play = static_cast<uint8_t>(1 - p);
     s.moves++;
@@ -367,6 +374,26 @@ struct Hex {
 // (no u16/u32 wrap) and equals "exactly one distinct liberty", so legality is
 // identical.  Positional superko follows go.cc:199-208 with the same Zobrist
 // hashes (chess_common.h ZobristTable, seed 2765481) compared for equality.
+// 256-bit membership pre-filter (bit = hash >> 56), kept in four named words
+// so it stays in registers.
+struct Filter256 {
+  uint64_t w0, w1, w2, w3;
+  OS_HD void clear() { w0 = w1 = w2 = w3 = 0; }
+  OS_HD bool has(int b) const {
+    const int q = b >> 6;
+    const uint64_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+    return (w >> (b & 63)) & 1;
+  }
+  OS_HD void add(int b) {
+    const int q = b >> 6;
+    const uint64_t m = 1ull << (b & 63);
+    w0 |= q == 0 ? m : 0;
+    w1 |= q == 1 ? m : 0;
+    w2 |= q == 2 ? m : 0;
+    w3 |= q == 3 ? m : 0;
+  }
+};
+
 struct GoCtx {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
   const uint64_t* base;    // hashes of positions before this search's root
@@ -374,22 +401,22 @@ struct GoCtx {
   uint64_t* log;           // hashes added since the root (capacity cap)
   int32_t n_log;
   int32_t cap;
-  uint64_t filt[4];        // 256-bit membership pre-filter (bit = hash >> 56)
-  uint64_t base_filt[4];
+  Filter256 filt;          // all hashes (base + log)
+  Filter256 base_filt;     // base hashes only
 
   OS_HD void reset() {
     n_log = 0;
-    for (int i = 0; i < 4; ++i) filt[i] = base_filt[i];
+    filt = base_filt;
+  }
+  // Builds base_filt from base[0, n_base) and resets.
+  OS_HD void init_filters() {
+    base_filt.clear();
+    for (int i = 0; i < n_base; ++i) base_filt.add(fbit(base[i]));
+    reset();
   }
   OS_HD static int fbit(uint64_t h) { return static_cast<int>(h >> 56); }
-  OS_HD bool filter_has(uint64_t h) const {
-    const int b = fbit(h);
-    return (filt[b >> 6] >> (b & 63)) & 1;
-  }
-  OS_HD void filter_add(uint64_t h) {
-    const int b = fbit(h);
-    filt[b >> 6] |= 1ull << (b & 63);
-  }
+  OS_HD bool filter_has(uint64_t h) const { return filt.has(fbit(h)); }
+  OS_HD void filter_add(uint64_t h) { filt.add(fbit(h)); }
   OS_HD bool contains(uint64_t h) const {
     if (!filter_has(h)) return false;
     for (int i = 0; i < n_base; ++i)
@@ -438,7 +465,7 @@ struct Go {
   // (go_board.cc:425-440).
   OS_HD static bool surrounded_legal(const State& s, const GameCfg& g, int p, int c,
                                      B128 E) {
-    const B128 own = s.bw[c], opp = s.bw[1 - c];
+    const B128 own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
     B128 nb = nbr4(bit128(p), g);
     B128 on = nb & own;
     while (any(on)) {  // joins an own chain that keeps a liberty
@@ -477,7 +504,8 @@ struct Go {
            ((s.flags & kLastPass) && (s.flags & kPrevPass));
   }
   OS_HD static int to_move(const State& s) { return s.to_play; }
-  OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
+  template <class C>
+  OS_HD static Legal legal(const State& s, const GameCfg& g, C&) {
     const int c = s.to_play;
     const B128 E = g.board & ~(s.bw[0] | s.bw[1]);
     B128 cand = E;
@@ -496,7 +524,10 @@ struct Go {
     l.pass_action = g.rows * g.cols;
     return l;
   }
-  OS_HD static void apply(State& s, const GameCfg& g, Ctx& ctx, int a) {
+  // C: GoCtx (one search per lane) or a wave-parallel context with the same
+  // zob / insert() interface (os_wave.h).
+  template <class C>
+  OS_HD static void apply(State& s, const GameCfg& g, C& ctx, int a) {
     const int c = s.to_play;
     const int pass = g.rows * g.cols;
     s.flags = static_cast<uint8_t>((s.flags & kSuperko) | ((s.flags & kLastPass) ? kPrevPass : 0));
@@ -507,20 +538,20 @@ struct Go {
     } else {
       const B128 pb = bit128(a);
       const B128 nb = nbr4(pb, g);
-      const B128 opp0 = s.bw[1 - c];
-      const bool enemy_eye = !any(nb & ~opp0);
-      s.bw[c] = s.bw[c] | pb;
+      B128 own = pick(s.bw, c) | pb;
+      B128 opp = pick(s.bw, 1 - c);
+      const bool enemy_eye = !any(nb & ~opp);
       s.hash ^= ctx.zob[2 * a + c];
-      B128 E = g.board & ~(s.bw[0] | s.bw[1]);
+      B128 E = g.board & ~(own | opp);
       int captured = 0;
       int cap_pt = -1;
-      B128 on = nb & s.bw[1 - c];
+      B128 on = nb & opp;
       while (any(on)) {
         const int q = lowest(on);
-        const B128 ch = flood(bit128(q), s.bw[1 - c], g);
+        const B128 ch = flood(bit128(q), opp, g);
         on = on & ~ch;
         if (!any(nbr4(ch, g) & E)) {
-          s.bw[1 - c] = s.bw[1 - c] & ~ch;
+          opp = opp & ~ch;
           E = E | ch;
           captured += popc(ch);
           cap_pt = q;
@@ -532,6 +563,8 @@ struct Go {
           }
         }
       }
+      s.bw[0] = c ? opp : own;
+      s.bw[1] = c ? own : opp;
       s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
       if (!ctx.insert(s.hash)) s.flags |= kSuperko;
     }
@@ -587,7 +620,8 @@ struct Go {
     if (g.handicap >= 2) sc -= static_cast<float>(g.handicap);
     return sc;
   }
-  OS_HD static int ret0(const State& s, const GameCfg& g, Ctx&) {
+  template <class C>
+  OS_HD static int ret0(const State& s, const GameCfg& g, C&) {
     if (s.flags & kSuperko) return 0;
     const float sc = score(s, g);
     return sc > 0 ? 1 : (sc < 0 ? -1 : 0);

@@ -257,8 +257,9 @@ GoCtx HostGoCtx(const HostState& s, std::vector<uint64_t>* storage) {
   ctx.log = storage->data();
   ctx.n_log = static_cast<int32_t>(s.hashes.size());
   ctx.cap = cap;
+  ctx.base_filt.clear();
+  ctx.filt.clear();
   for (size_t i = 0; i < s.hashes.size(); ++i) ctx.filter_add(s.hashes[i]);
-  for (int i = 0; i < 4; ++i) ctx.base_filt[i] = 0;
   return ctx;
 }
 

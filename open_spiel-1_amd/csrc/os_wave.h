@@ -1,0 +1,617 @@
+// Wave-per-search execution of the MCTS engine on gfx950 (device only).
+//
+// One 64-lane wavefront runs one independent search.  The game state, the
+// tree walk and the random rollout are wave-uniform (SGPRs, scalar 64-bit
+// bitboard ops); the lanes are used where the algorithm has data
+// parallelism:
+//   * MT19937: the 624-word block is twisted cooperatively in LDS (64 words
+//     per step), tempered in parallel, and drawn with v_readlane;
+//   * selection: lane k loads child k (coalesced) and evaluates its UCT value;
+//     a wave argmax (max value, lowest index on ties == mcts.cc's strict '>'
+//     scan) picks the child;
+//   * expansion: lane k computes the k-th legal action; the libstdc++ /
+//     numpy shuffle runs on the lane-distributed array; lane k writes child k;
+//   * backup: lane d updates path node d (mcts.cc:351-357) in one step; the
+//     MCTS-Solver max^n backup (:359-395) walks up serially, each level's
+//     children outcomes read and reduced across lanes;
+//   * go superko: the hash history lives in LDS and is compared 64 at a time.
+// The semantics are those of os_mcts.h::mcts_search (checked bit-exact
+// against the oracle by tests/test_gpu_parity.py).
+#ifndef OS_WAVE_H_
+#define OS_WAVE_H_
+
+#include "os_mcts.h"
+
+// Re-assert wave-uniformity of the playout state each rollout ply / of the
+// walk state each selection step (A/B switches; measured on MI355X, C4 4096x1024:
+// ROLL=0,SEL=1 25.6 ms; 0,0 25.8; 1,1 27.8; 1,0 28.5 — profiles/r01/ab_uniform.txt).
+#ifndef OS_UNI_ROLL
+#define OS_UNI_ROLL 0
+#endif
+#ifndef OS_UNI_SEL
+#define OS_UNI_SEL 1
+#endif
+// Diagnostic build (-DOS_PHASE_TIMING=1): per-phase shader-clock cycles of the
+// wave search, summed over waves into PhaseCycles (os_debug_phase_cycles).
+#ifndef OS_PHASE_TIMING
+#define OS_PHASE_TIMING 0
+#endif
+
+namespace osm {
+
+enum PhaseId { kPhSelect = 0, kPhExpand, kPhRollout, kPhBackup, kPhSolver, kPhTail,
+               kPhTwist, kPhTotal, kNumPhases };
+struct PhaseCycles {
+  uint64_t c[kNumPhases];
+};
+#if OS_PHASE_TIMING
+#define OS_PH_NOW() __builtin_amdgcn_s_memtime()
+#define OS_PH_ADD(acc, t0) ((acc) += __builtin_amdgcn_s_memtime() - (t0))
+#else
+#define OS_PH_NOW() 0ull
+#define OS_PH_ADD(acc, t0) ((void)(t0))
+#endif
+
+__device__ __forceinline__ int lane_id() { return static_cast<int>(threadIdx.x & 63); }
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), lane));
+}
+__device__ __forceinline__ int32_t rli(int32_t v, int lane) {
+  return __builtin_amdgcn_readlane(v, lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
+  const uint32_t lo = rl32(static_cast<uint32_t>(v), lane);
+  const uint32_t hi = rl32(static_cast<uint32_t>(v >> 32), lane);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ double rld(double v, int lane) {
+  return __longlong_as_double(static_cast<long long>(
+      rl64(static_cast<uint64_t>(__double_as_longlong(v)), lane)));
+}
+__device__ __forceinline__ uint32_t wl32(uint32_t v, int lane, uint32_t old) {
+  return lane_id() == lane ? v : old;  // v_cmp + v_cndmask
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// Marks a trivially-copyable value as wave-uniform (v_readfirstlane per
+// dword) so the compiler keeps it, and everything computed from it, in SGPRs
+// and runs the game logic on the scalar unit.
+template <class T>
+__device__ __forceinline__ T make_uniform(const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "dword-sized state expected");
+  T out;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+  for (int i = 0; i < static_cast<int>(sizeof(T) / 4); ++i)
+    dst[i] = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(src[i])));
+  return out;
+}
+
+// MT19937 stream whose 624-word state lives in LDS, shared by the wave.
+// Draws are wave-uniform.  `cur` holds 64 tempered words of the current block
+// (word base + lane in lane `lane`).
+struct WaveMt {
+  uint32_t* s;     // LDS, 624 words
+  uint32_t cur;    // per lane
+  int base;        // first word index held in cur; kMtN => block exhausted
+  int valid;       // words held in cur
+  int pos;         // next word (offset in cur)
+  uint32_t words;  // draws (instrumentation)
+#if OS_PHASE_TIMING
+  uint64_t twist_cycles;
+#endif
+
+  __device__ void init_seeded() {  // state = init_genrand output, untwisted
+    base = kMtN;
+    valid = 0;
+    pos = 0;
+    words = 0;
+#if OS_PHASE_TIMING
+    twist_cycles = 0;
+#endif
+  }
+  // numpy legacy (key, p): key is a fully twisted block, p words consumed.
+  __device__ void init_import(int p) {
+    words = 0;
+#if OS_PHASE_TIMING
+    twist_cycles = 0;
+#endif
+    if (p >= kMtN) {
+      base = kMtN;
+      valid = 0;
+      pos = 0;
+      return;
+    }
+    base = p & ~63;
+    valid = kMtN - base < 64 ? kMtN - base : 64;
+    const int i = base + lane_id();
+    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    pos = p - base;
+  }
+  __device__ int export_pos() const { return base >= kMtN ? kMtN : base + pos; }
+
+  // Cooperative in-place twist of the whole block (same result as 624 serial
+  // steps: word i reads old s[i], old s[i+1] and s[(i+397) % 624], which is
+  // new exactly for i >= 227, and every such word lies >= 3 chunks back).
+  __device__ void twist() {
+    const int l = lane_id();
+#if OS_PHASE_TIMING
+    const uint64_t t0 = OS_PH_NOW();
+#endif
+    for (int c = 0; c < kMtN; c += 64) {
+      const int i = c + l;
+      uint32_t v = 0;
+      const bool act = i < kMtN;
+      if (act) {
+        const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+        const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+        const uint32_t y = (s[i] & 0x80000000u) | (s[i1] & 0x7fffffffu);
+        v = s[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (act) s[i] = v;
+      __builtin_amdgcn_wave_barrier();
+    }
+#if OS_PHASE_TIMING
+    OS_PH_ADD(twist_cycles, t0);
+#endif
+  }
+  __device__ void refill() {
+    int nb = base + valid;
+    if (base >= kMtN || nb >= kMtN) {
+      twist();
+      nb = 0;
+    }
+    base = nb;
+    valid = kMtN - base < 64 ? kMtN - base : 64;
+    const int i = base + lane_id();
+    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    pos = 0;
+  }
+  __device__ uint32_t next() {
+    if (pos >= valid) refill();
+    const uint32_t w = rl32(cur, pos);
+    ++pos;
+    ++words;
+    return w;
+  }
+};
+
+// Go superko context for one search per wave: the per-simulation hash log in
+// LDS, compared 64 entries at a time.
+struct GoWaveCtx {
+  const uint64_t* zob;
+  const uint64_t* base;   // hashes before the root (global)
+  int32_t n_base;
+  uint64_t* log;          // LDS
+  int32_t n_log;
+  int32_t cap;
+  Filter256 filt;
+  Filter256 base_filt;
+
+  __device__ void reset() {
+    n_log = 0;
+    filt = base_filt;
+  }
+  __device__ void init_filters() {
+    base_filt.clear();
+    for (int i = 0; i < n_base; ++i) base_filt.add(GoCtx::fbit(base[i]));
+    reset();
+  }
+  __device__ bool contains(uint64_t h) const {
+    if (!filt.has(GoCtx::fbit(h))) return false;
+    const int l = lane_id();
+    for (int i = 0; i < n_base; i += 64) {
+      const bool hit = i + l < n_base && base[i + l] == h;
+      if (ballot(hit)) return true;
+    }
+    for (int i = 0; i < n_log; i += 64) {
+      const bool hit = i + l < n_log && log[i + l] == h;
+      if (ballot(hit)) return true;
+    }
+    return false;
+  }
+  __device__ bool insert(uint64_t h) {
+    if (contains(h)) return false;
+    if (n_log < cap) {
+      if (lane_id() == 0) log[n_log] = h;
+      __builtin_amdgcn_wave_barrier();
+      ++n_log;
+    }
+    filt.add(GoCtx::fbit(h));
+    return true;
+  }
+};
+
+template <class G>
+struct WaveCtxOf {
+  using type = NoCtx;
+};
+template <>
+struct WaveCtxOf<Go> {
+  using type = GoWaveCtx;
+};
+
+// Lane-distributed array of up to 128 u16 actions: element i in lane i % 64 of
+// slot i / 64.
+struct LaneArr {
+  uint32_t a0, a1;
+  __device__ uint32_t get(int i) const { return i < 64 ? rl32(a0, i) : rl32(a1, i - 64); }
+  __device__ void set(int i, uint32_t v) {
+    if (i < 64) a0 = wl32(v, i, a0);
+    else a1 = wl32(v, i - 64, a1);
+  }
+  __device__ void swap(int i, int j) {
+    if (i == j) return;
+    const uint32_t x = get(i), y = get(j);
+    set(i, y);
+    set(j, x);
+  }
+};
+
+template <int Policy, class Rng>
+__device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
+  if (Policy == kPolicyCpp) {  // libstdc++ 11 std::shuffle, pair path
+    if (n <= 1) return;
+    int i = 1;
+    if ((n & 1) == 0) {
+      a.swap(1, static_cast<int>(Lemire32(g, 2u)));
+      i = 2;
+    }
+    while (i != n) {
+      const uint32_t b0 = static_cast<uint32_t>(i) + 1u, b1 = b0 + 1u;
+      const uint32_t x = Lemire32(g, b0 * b1);
+      a.swap(i, static_cast<int>(x / b1));
+      a.swap(i + 1, static_cast<int>(x % b1));
+      i += 2;
+    }
+  } else {  // numpy RandomState.shuffle
+    for (int i = n - 1; i >= 1; --i)
+      a.swap(i, static_cast<int>(NpRandomInterval(g, static_cast<uint32_t>(i))));
+  }
+}
+
+// Wave argmax: max v, lowest index among equal maxima (== first maximum of a
+// strict '>' scan in index order).  Returns the index (uniform).
+__device__ __forceinline__ int wave_argmax(double v, int idx) {
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const int oi = __shfl_xor(idx, off);
+    if (ov > v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+  return rli(idx, 0);
+}
+
+template <class G, int Policy, class Rng, class C>
+__device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
+  for (;;) {
+#if OS_UNI_ROLL
+    s = make_uniform(s);  // keep the playout on the scalar unit
+#endif
+    if (G::terminal(s, g)) break;
+    const typename G::Legal l = G::legal(s, g, ctx);
+    const uint32_t k = Policy == kPolicyCpp
+                           ? AbslUniform(ev, static_cast<uint32_t>(l.count))
+                           : NpChoice(ev, static_cast<uint32_t>(l.count));
+    G::apply(s, g, ctx, l.kth(static_cast<int>(k)));
+  }
+  return G::ret0(s, g, ctx);
+}
+
+// One search, executed by the whole wave.  `path` (LDS) has path_cap
+// entries.  Same contract as mcts_search.
+template <class G, class R, int Policy, class C>
+__device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
+                                    const typename G::State& root, C& ctx,
+                                    Node<R>* nodes, uint32_t cap, WaveMt& bot,
+                                    WaveMt& ev, PathEnt<R>* path, int path_cap,
+                                    PhaseCycles& ph) {
+  const int l = lane_id();
+  const uint64_t t_begin = OS_PH_NOW();
+  SearchResult res;
+  res.status = kOk;
+  res.sims = 0;
+  res.gc_runs = 0;
+  res.max_depth = 0;
+  res.scanned = res.backed = res.expanded = res.solver_scanned = 0;
+  const int P0 = G::to_move(root);
+  if (l == 0) {
+    nodes[0].first = 0;
+    nodes[0].n = 0;
+    nodes[0].w = 0;
+    nodes[0].action = 0;
+    nodes[0].nchild = 0;
+    nodes[0].out = kUnsolved;
+  }
+  // Root statistics persist in registers across simulations.
+  uint32_t root_first = 0;
+  int32_t root_n = 0;
+  int root_nc = 0;
+  R root_w = 0;
+  int8_t root_out = kUnsolved;
+  uint32_t used = 1;
+  int nodes_count = 1;
+  int gc_limit = 5;
+  const double inf = __builtin_huge_val();
+
+  for (int sim = 0; sim < sp.max_simulations; ++sim) {
+    uint64_t t_ph = OS_PH_NOW();
+    typename G::State s = root;
+    ctx.reset();
+    uint32_t cur_idx = 0;
+    uint32_t cur_first = root_first;
+    int32_t cur_n = root_n;
+    int cur_nc = root_nc;
+    int depth = 0;
+    // ---- selection / expansion ----
+    for (;;) {
+#if OS_UNI_SEL
+      s = make_uniform(s);
+      cur_n = __builtin_amdgcn_readfirstlane(cur_n);
+      cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
+      cur_first = static_cast<uint32_t>(
+          __builtin_amdgcn_readfirstlane(static_cast<int>(cur_first)));
+      cur_idx = static_cast<uint32_t>(
+          __builtin_amdgcn_readfirstlane(static_cast<int>(cur_idx)));
+      depth = __builtin_amdgcn_readfirstlane(depth);
+#endif
+      if (G::terminal(s, g) || cur_n <= 0) break;
+      int chosen;
+      uint32_t c_action, c_first;
+      int32_t c_n;
+      int c_nc;
+      R c_w;
+      if (cur_nc == 0) {
+        const uint64_t t_ex = OS_PH_NOW();
+        const typename G::Legal lg = G::legal(s, g, ctx);
+        const int nc = lg.count;
+        LaneArr acts;
+        acts.a0 = l < nc ? static_cast<uint32_t>(lg.kth(l)) : 0u;
+        acts.a1 = l + 64 < nc ? static_cast<uint32_t>(lg.kth(l + 64)) : 0u;
+        wave_shuffle<Policy>(acts, nc, bot);
+        if (used + static_cast<uint32_t>(nc) > cap) {
+          res.status = kArenaOverflow;
+          goto done;
+        }
+        const uint32_t first = used;
+        used += nc;
+        for (int h = 0; h < 2; ++h) {
+          const int k = l + 64 * h;
+          if (k < nc) {
+            Node<R>& c = nodes[first + k];
+            c.first = 0;
+            c.n = 0;
+            c.w = 0;
+            c.action = static_cast<uint16_t>(h == 0 ? acts.a0 : acts.a1);
+            c.nchild = 0;
+            c.out = kUnsolved;
+          }
+        }
+        if (l == 0) {
+          nodes[cur_idx].first = first;
+          nodes[cur_idx].nchild = static_cast<uint8_t>(nc);
+        }
+        if (depth == 0) {
+          root_first = first;
+          root_nc = nc;
+        } else if (l == 0) {
+          path[depth].first = first;
+          path[depth].nc = nc;
+        }
+        nodes_count += nc;
+        res.expanded += nc;
+        cur_first = first;
+        cur_nc = nc;
+        chosen = 0;  // all children fresh: +inf, the first one wins
+        c_action = acts.get(0);
+        c_first = 0;
+        c_n = 0;
+        c_nc = 0;
+        c_w = 0;
+        OS_PH_ADD(ph.c[kPhExpand], t_ex);
+      } else {
+        const int cp = P0 ^ (depth & 1);
+        const double logN = sp.log_lut[cur_n];
+        res.scanned += cur_nc;
+        double bv = -inf;
+        int bk = 1 << 20;
+        Node<R> bc;
+        bc.first = 0; bc.n = 0; bc.w = 0; bc.action = 0; bc.nchild = 0; bc.out = kUnsolved;
+        for (int h = 0; h < 2; ++h) {
+          const int k = l + 64 * h;
+          if (k < cur_nc) {
+            const Node<R> c = nodes[cur_first + k];
+            double v;
+            if (c.out != kUnsolved) {
+              v = outcome_for(c.out, cp);
+            } else if (c.n == 0) {
+              v = inf;
+            } else {
+              const double dn = static_cast<double>(c.n);
+              v = static_cast<double>(c.w) / dn + sp.uct_c * __builtin_sqrt(logN / dn);
+            }
+            if (v > bv) {  // h == 1 only replaces on strict improvement
+              bv = v;
+              bk = k;
+              bc = c;
+            }
+          }
+        }
+        chosen = wave_argmax(bv, bk);
+        const int src = chosen & 63;
+        c_action = rl32(bc.action, src);
+        c_first = rl32(bc.first, src);
+        c_n = rli(bc.n, src);
+        c_nc = rli(bc.nchild, src);
+        if (sizeof(R) == 4) {
+          const int32_t wi = rli(static_cast<int32_t>(bc.w), src);
+          c_w = static_cast<R>(wi);
+        } else {
+          c_w = static_cast<R>(rld(static_cast<double>(bc.w), src));
+        }
+      }
+      G::apply(s, g, ctx, static_cast<int>(c_action));
+      if (++depth >= path_cap) {
+        res.status = kPathOverflow;
+        goto done;
+      }
+      cur_idx = cur_first + chosen;
+      cur_first = c_first;
+      cur_n = c_n;
+      cur_nc = c_nc;
+      if (l == 0) {
+        PathEnt<R>& pe = path[depth];
+        pe.idx = cur_idx;
+        pe.first = c_first;
+        pe.n = c_n;
+        pe.nc = c_nc;
+        pe.w = c_w;
+      }
+    }
+    if (depth > res.max_depth) res.max_depth = depth;
+    __builtin_amdgcn_wave_barrier();
+    OS_PH_ADD(ph.c[kPhSelect], t_ph);
+    t_ph = OS_PH_NOW();
+    {
+      // ---- evaluation ----
+      bool solved;
+      R rv0, rv1;
+      int8_t leaf_out = kUnsolved;
+      if (G::terminal(s, g)) {
+        const int r0 = G::ret0(s, g, ctx);
+        leaf_out = static_cast<int8_t>(r0);
+        if (l == 0) nodes[cur_idx].out = leaf_out;
+        solved = sp.solve != 0;
+        rv0 = static_cast<R>(r0);
+        rv1 = static_cast<R>(-r0);
+      } else {
+        solved = false;
+        if (sp.n_rollouts == 1) {
+          const int r0 = wave_rollout<G, Policy>(s, g, ctx, ev);
+          rv0 = static_cast<R>(r0);
+          rv1 = static_cast<R>(-r0);
+        } else {
+          double s0 = 0.0, s1 = 0.0;
+          for (int k = 0; k < sp.n_rollouts; ++k) {
+            const int r0 = wave_rollout<G, Policy>(s, g, ctx, ev);
+            s0 += static_cast<double>(r0);
+            s1 += static_cast<double>(-r0);
+          }
+          rv0 = static_cast<R>(s0 / sp.n_rollouts);
+          rv1 = static_cast<R>(s1 / sp.n_rollouts);
+        }
+      }
+      OS_PH_ADD(ph.c[kPhRollout], t_ph);
+      t_ph = OS_PH_NOW();
+      // ---- backup: every path node at once (lane d <-> depth d) ----
+      res.backed += depth + 1;
+      for (int d0 = 1; d0 <= depth; d0 += 64) {
+        const int d = d0 + l;
+        if (d <= depth) {
+          const PathEnt<R>& pe = path[d];
+          const int pl = P0 ^ ((d - 1) & 1);
+          Node<R>& nd = nodes[pe.idx];
+          nd.n = pe.n + 1;
+          nd.w = pe.w + (pl == 0 ? rv0 : rv1);
+        }
+      }
+      root_n += 1;
+      root_w += P0 == 0 ? rv0 : rv1;
+      if (l == 0) {
+        nodes[0].n = root_n;
+        nodes[0].w = root_w;
+      }
+      OS_PH_ADD(ph.c[kPhBackup], t_ph);
+      t_ph = OS_PH_NOW();
+      // ---- MCTS-Solver (serial up the path, children reduced across lanes)
+      if (solved) {
+        uint32_t prev_idx = cur_idx;
+        int8_t prev_out = leaf_out;
+        for (int d = depth - 1; d >= 0; --d) {
+          uint32_t nfirst, nidx;
+          int nnc;
+          if (d == 0) {
+            nfirst = root_first;
+            nnc = root_nc;
+            nidx = 0;
+          } else {
+            const PathEnt<R>& pe = path[d];
+            nfirst = pe.first;
+            nnc = pe.nc;
+            nidx = pe.idx;
+          }
+          if (nnc == 0) continue;  // unreachable: path nodes below have children
+          const int cpl = P0 ^ (d & 1);
+          res.solver_scanned += nnc;
+          bool any_unsolved = false;
+          int best_v = -128;
+          for (int h = 0; h < 2; ++h) {
+            const int k = l + 64 * h;
+            int8_t co = kUnsolved;
+            if (k < nnc) {
+              co = (nfirst + k == prev_idx) ? prev_out : nodes[nfirst + k].out;
+            }
+            const bool uns = k < nnc && co == kUnsolved;
+            if (ballot(uns)) any_unsolved = true;
+            int v = (k < nnc && co != kUnsolved) ? (cpl == 0 ? co : -co) : -128;
+            for (int off = 32; off >= 1; off >>= 1) {
+              const int ov = __shfl_xor(v, off);
+              v = ov > v ? ov : v;
+            }
+            v = rli(v, 0);
+            if (v > best_v) best_v = v;
+          }
+          if (best_v > -128 && (!any_unsolved || best_v == 1)) {
+            const int8_t no = static_cast<int8_t>(cpl == 0 ? best_v : -best_v);
+            if (l == 0) nodes[nidx].out = no;
+            if (d == 0) root_out = no;
+            prev_idx = nidx;
+            prev_out = no;
+          } else {
+            break;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    OS_PH_ADD(ph.c[kPhSolver], t_ph);
+    t_ph = OS_PH_NOW();
+    res.sims = sim + 1;
+    if (root_out != kUnsolved) break;
+    if (Policy == kPolicyCpp) {
+      if (root_nc == 1) break;
+      if (sp.max_nodes > 1 && nodes_count >= sp.max_nodes) {
+        int st = kOk;
+        if (l == 0) st = garbage_collect(nodes, used, cap, gc_limit, &nodes_count);
+        st = rli(st, 0);
+        nodes_count = rli(nodes_count, 0);
+        if (st != kOk) {
+          res.status = st;
+          goto done;
+        }
+        res.gc_runs++;
+        gc_limit = static_cast<int>(gc_limit *
+                                    (nodes_count > sp.max_nodes / 2 ? 1.25 : 0.9));
+        if (gc_limit < 5) gc_limit = 5;
+        __threadfence_block();
+        root_nc = nodes[0].nchild;
+        root_first = nodes[0].first;
+      }
+    }
+    OS_PH_ADD(ph.c[kPhTail], t_ph);
+  }
+done:
+  OS_PH_ADD(ph.c[kPhTotal], t_begin);
+  res.nodes = nodes_count;
+  res.used = used;
+  return res;
+}
+
+}  // namespace osm
+
+#endif  // OS_WAVE_H_

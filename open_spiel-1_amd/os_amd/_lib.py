@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libos_mcts.so")
+# OS_AMD_LIB selects another build of the same library (A/B kernel variants).
+LIB_PATH = os.environ.get("OS_AMD_LIB") or os.path.join(_HERE, "libos_mcts.so")
 
 OS_OK = 0
 OS_ERR_INVALID = -1
@@ -20,6 +21,9 @@ OS_ERR_CAPACITY = -4
 
 POLICY_CPP = 0
 POLICY_NUMPY = 1
+
+LAYOUT_WAVE = 0
+LAYOUT_LANE = 1
 
 if not os.path.exists(LIB_PATH):
   raise ImportError(
@@ -72,7 +76,7 @@ class GameInfo(ctypes.Structure):
 class MctsParams(ctypes.Structure):
   _fields_ = [("uct_c", _dbl), ("max_simulations", _i32), ("n_rollouts", _i32),
               ("max_memory_mb", _i64), ("solve", _i32), ("policy", _i32),
-              ("block_size", _i32), ("pad", _i32), ("arena_nodes", _i64)]
+              ("block_size", _i32), ("layout", _i32), ("arena_nodes", _i64)]
 
 
 def _sig(name, restype, argtypes):
@@ -86,6 +90,7 @@ _P = _vp  # pointers passed as raw addresses (numpy .ctypes.data)
 
 _sig("os_last_error", _cp, [])
 _sig("os_build_info", _cp, [])
+_sig("os_debug_phase_cycles", ctypes.c_int, [_P, _i32])
 _sig("os_game_load", ctypes.c_int, [_cp, ctypes.POINTER(_vp)])
 _sig("os_game_free", None, [_vp])
 _sig("os_game_get_info", ctypes.c_int, [_vp, ctypes.POINTER(GameInfo)])
@@ -118,6 +123,7 @@ _sig("os_engine_fetch", ctypes.c_int,
      [_vp, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P])
 _sig("os_engine_last_sims", _i64, [_vp])
 _sig("os_engine_stats", ctypes.c_int, [_vp, _P])
+_sig("os_engine_set_rollout_layout", ctypes.c_int, [_vp, _i32])
 _sig("os_engine_node_bytes", _i32, [_vp])
 _sig("os_engine_state_bytes", _i32, [_vp])
 _sig("os_make_roots", _i64, [_vp, _i64, _u32, _i32, _P, _P])

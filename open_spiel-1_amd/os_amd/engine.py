@@ -20,8 +20,9 @@ UNSOLVED = 2
 
 def make_params(uct_c=2.0, max_simulations=1000, n_rollouts=1,
                 max_memory_mb=1000, solve=True, policy=_lib.POLICY_CPP,
-                block_size=0, arena_nodes=0):
+                block_size=0, arena_nodes=0, layout=_lib.LAYOUT_WAVE):
   p = _lib.MctsParams()
+  p.layout = int(layout)
   p.uct_c = float(uct_c)
   p.max_simulations = int(max_simulations)
   p.n_rollouts = int(n_rollouts)
@@ -146,8 +147,9 @@ class Engine:
                              ptr(t["nchild"]), ptr(t["out0"])))
     return t
 
-  def rollouts(self, history, seeds, n_rollouts=1):
+  def rollouts(self, history, seeds, n_rollouts=1, layout=_lib.LAYOUT_WAVE):
     """RandomRolloutEvaluator(n_rollouts, seed).Evaluate(root) per seed."""
+    check(lib.os_engine_set_rollout_layout(self._h, int(layout)))
     acts = _lib.i64(history)
     s = _lib.u32(seeds)
     out = np.zeros((len(s), 2), np.float64)

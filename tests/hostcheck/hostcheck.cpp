@@ -38,10 +38,7 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
     ctx.log = logbuf.data();
     ctx.cap = 256;
-    for (uint64_t h : root.hashes) {
-      const int b = GoCtx::fbit(h);
-      ctx.base_filt[b >> 6] |= 1ull << (b & 63);
-    }
+    ctx.init_filters();
   }
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
   SearchResult res = mcts_search<G, R, Policy>(game.cfg, sp, rs, ctx, nodes.data(), cap,
@@ -232,11 +229,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
         c.n_base = static_cast<int32_t>(hs.hashes.size());
         c.log = logbuf.data();
         c.cap = 256;
-        for (uint64_t h : hs.hashes) {
-          const int b = GoCtx::fbit(h);
-          c.base_filt[b >> 6] |= 1ull << (b & 63);
-        }
-        c.reset();
+        c.init_filters();
         r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg, c, ev);
         break;
       }
