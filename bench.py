@@ -2,20 +2,29 @@
 """Headline benchmark: random-rollout MCTS simulations/s on connect_four.
 
 BASELINE.json metric: "MCTS simulations/sec (random rollout) on connect_four
-at 1/2/4/8 MI355X"; workload = configs[1]: 4096 independent roots x 1024
-simulations per GPU (weak scaling: every rank searches its own 4096 roots,
-seeded by global root id; no data-path collective).
+at 1/2/4/8 MI355X"; workload = configs[1] (`--config c2`, the default): 4096
+independent roots x 1024 simulations per GPU (weak scaling: every rank searches
+its own 4096 roots, seeded by global root id; no data-path collective).
 
-One step = one pass of the search kernel over the rank's whole batch (roots
-and seeds already resident in HBM).  Rank 0 prints ONE JSON line.
+The other BASELINE configs are reachable for measurement and parity runs:
+  c3  breakthrough(rows=8,columns=8), 65536 roots x 2048 sims per GPU
+  c4  hex(board_size=11), root-parallel: T trees per GPU on the initial
+      position, 2048 sims each, action-indexed root visits all-reduced over
+      RCCL inside every timed step
+  c5  go(board_size=9), 2^20 random playouts split across the ranks
+      (strong scaling), outcome counts all-reduced inside every timed step
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+One step = one pass of the hot path over the rank's batch (roots and seeds
+already resident in HBM).  Rank 0 prints ONE JSON line.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -24,15 +33,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "open_spiel-1_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+EVAL_OFFSET = 1 << 20
 
+# name: (mode, game string, units per GPU (or total for c5), sims, root plies)
 CONFIGS = {
-    # name: (game string, roots per GPU, sims, root plies)
-    "c2": ("connect_four", 4096, 1024, 8),
-    "c3": ("breakthrough(rows=8,columns=8)", 65536, 2048, 6),
+    "c2": ("search", "connect_four", 4096, 1024, 8),
+    "c3": ("search", "breakthrough(rows=8,columns=8)", 65536, 2048, 6),
+    "c4": ("root_parallel", "hex(board_size=11)", 8192, 2048, 0),
+    "c5": ("playouts", "go(board_size=9)", 1 << 20, 0, 0),
 }
-
-
-LAYOUTS = {}
 KERNEL = {"wave": "k_wsearch", "lane": "k_mcts"}
 
 
@@ -42,11 +51,12 @@ def parse():
   ap.add_argument("--steps", type=int, default=5)
   ap.add_argument("--warmup", type=int, default=2)
   ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-  ap.add_argument("--roots", type=int, default=0, help="override roots per GPU")
+  ap.add_argument("--roots", type=int, default=0,
+                  help="override roots / trees / playouts of the config")
   ap.add_argument("--sims", type=int, default=0, help="override simulations")
-  ap.add_argument("--block", type=int, default=0, help="lanes per workgroup")
+  ap.add_argument("--block", type=int, default=0, help="lanes per workgroup (lane layout)")
   ap.add_argument("--arena-nodes", type=int, default=0)
-  ap.add_argument("--layout", default="wave", choices=("wave", "lane"),
+  ap.add_argument("--layout", default="auto", choices=("auto", "wave", "lane"),
                   help="search kernel: one wave per search / one lane per search")
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -55,40 +65,122 @@ def parse():
   return ap.parse_args()
 
 
+class Ctx:
+  """Rank / device / collective plumbing (one process per GPU)."""
+
+  def __init__(self, args):
+    import torch
+    import torch.distributed as dist
+    self.torch, self.dist = torch, dist
+    self.world = int(os.environ.get("WORLD_SIZE", "1"))
+    self.rank = int(os.environ.get("RANK", "0"))
+    self.local = int(os.environ.get("LOCAL_RANK", "0"))
+    if self.world != args.gpus and self.world > 1:
+      raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, self.world))
+    torch.cuda.set_device(self.local)
+    if self.world > 1:
+      dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+    self.stream = torch.cuda.current_stream()
+
+  def barrier(self):
+    if self.world > 1:
+      self.dist.barrier()
+
+  def timed(self, step, steps):
+    """Barrier + sync, K steps, sync + barrier; (wall max over ranks, event ms)."""
+    torch = self.torch
+    self.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(self.stream)
+    for _ in range(steps):
+      step()
+    ev1.record(self.stream)
+    torch.cuda.synchronize()
+    self.barrier()
+    elapsed = time.perf_counter() - t0
+    if self.world > 1:
+      t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+      self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+      elapsed = float(t.item())
+    return elapsed, ev0.elapsed_time(ev1) / max(steps, 1)
+
+  def total(self, x):
+    """Sum of a per-rank count over all ranks."""
+    if self.world == 1:
+      return x
+    t = self.torch.tensor([float(x)], dtype=self.torch.float64, device="cuda")
+    self.dist.all_reduce(t)
+    return float(t.item())
+
+
 def main():
   args = parse()
-  import torch
-  import torch.distributed as dist
-  from os_amd import engine as E
+  ctx = Ctx(args)
   from os_amd import _lib
-  LAYOUTS.update(wave=_lib.LAYOUT_WAVE, lane=_lib.LAYOUT_LANE)
+  layouts = {"auto": _lib.LAYOUT_AUTO, "wave": _lib.LAYOUT_WAVE, "lane": _lib.LAYOUT_LANE}
+  mode = CONFIGS[args.config][0]
+  fn = {"search": bench_search, "root_parallel": bench_root_parallel,
+        "playouts": bench_playouts}[mode]
+  line = fn(args, ctx, layouts[args.layout])
+  if ctx.rank == 0:
+    print(json.dumps(line), flush=True)
+  if ctx.world > 1:
+    ctx.dist.destroy_process_group()
 
-  world = int(os.environ.get("WORLD_SIZE", "1"))
-  rank = int(os.environ.get("RANK", "0"))
-  local = int(os.environ.get("LOCAL_RANK", "0"))
-  if world != args.gpus and world > 1:
-    raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-  torch.cuda.set_device(local)
-  if world > 1:
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-  game, R, sims, plies = CONFIGS[args.config]
+def _resolved_layout(game, R, layout):
+  """Mirror of ResolveLayout (os_engine.hip) for reporting."""
+  from os_amd import _lib
+  if layout != _lib.LAYOUT_AUTO:
+    return "wave" if layout == _lib.LAYOUT_WAVE else "lane"
+  if game.startswith("hex") or R >= 64 * 1024:
+    return "lane"
+  return "wave"
+
+
+def _base_line(args, ctx, metric, value, unit, elapsed, config):
+  return {
+      "metric": metric, "value": value, "unit": unit, "n_gpus": ctx.world,
+      "steps": args.steps, "warmup": args.warmup,
+      "ms_per_step": elapsed / max(args.steps, 1) * 1e3, "higher_is_better": True,
+      "scaling": "weak" if args.config != "c5" else "strong",
+      "vs_baseline": None, "dtype": "int32+f64",
+      "data": "synthetic (seeded random roots; no dataset)", "config": config,
+  }
+
+
+def _roofline(kernel, game, alg_bytes, kernel_ms, units, unit_name):
+  achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+  return {
+      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(kernel, game),
+      "kernel": kernel, "kernel_ms_per_launch": kernel_ms,
+      "algorithmic_bytes_per_launch": alg_bytes,
+      "algorithmic_bytes_per_%s" % unit_name: alg_bytes / max(units, 1),
+  }
+
+
+# ---------------------------------------------------------------------------
+# c2 / c3: independent searches
+def bench_search(args, ctx, layout):
+  from os_amd import engine as E
+  _, game, R, sims, plies = CONFIGS[args.config]
   R = args.roots or R
   sims = args.sims or sims
-  params = dict(uct_c=2.0, max_simulations=sims, n_rollouts=1,
-                max_memory_mb=1000, solve=True, block_size=args.block,
-                arena_nodes=args.arena_nodes, layout=LAYOUTS[args.layout])
-  base = rank * R  # global root ids of this rank
+  params = dict(uct_c=2.0, max_simulations=sims, n_rollouts=1, max_memory_mb=1000,
+                solve=True, block_size=args.block, arena_nodes=args.arena_nodes,
+                layout=layout)
+  base = ctx.rank * R  # global root ids of this rank
   acts, offs = E.make_roots(game, R, seed_base=1000 + base, max_plies=plies)
   gid = np.arange(base, base + R, dtype=np.uint32)
-  bot_seeds = gid
-  eval_seeds = gid + np.uint32(1 << 20)
+  bot_seeds, eval_seeds = gid, gid + np.uint32(EVAL_OFFSET)
 
-  eng = E.Engine(game, device=local)
+  eng = E.Engine(game, device=ctx.local)
   eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
-  stream = torch.cuda.current_stream()
-  handle = stream.cuda_stream
-
+  handle = ctx.stream.cuda_stream
   for _ in range(args.warmup):
     eng.run_async(handle)
   out = eng.fetch()  # synchronises; validates per-root status
@@ -96,122 +188,223 @@ def main():
   alg_bytes = eng.algorithmic_bytes(R)
   stats = eng.stats()
 
-  # Parity spot check against the oracle (rank 0, a prefix of the batch).
   parity = None
-  cpu = None
-  if rank == 0:
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
-    og = oracle_lib.Game(game)
+  if ctx.rank == 0:
+    og = _oracle(game)
     pr = min(args.parity_roots, R)
-    ref = og.mcts_batch(acts[:offs[pr]], offs[:pr + 1], bot_seeds[:pr],
-                        eval_seeds[:pr], uct_c=2.0, max_simulations=sims,
-                        max_children=eng.max_children)
+    ref = og.mcts_batch(acts[:offs[pr]], offs[:pr + 1], bot_seeds[:pr], eval_seeds[:pr],
+                        uct_c=2.0, max_simulations=sims, max_children=eng.max_children)
     bad = [k for k in E.OUTPUT_KEYS if not np.array_equal(out[k][:pr], ref[k])]
     parity = {"roots_checked": pr, "bit_exact": not bad, "mismatch_fields": bad}
 
-  if world > 1:
-    dist.barrier()
-  torch.cuda.synchronize()
-  ev0 = torch.cuda.Event(enable_timing=True)
-  ev1 = torch.cuda.Event(enable_timing=True)
-  t0 = time.perf_counter()
-  ev0.record(stream)
-  for _ in range(args.steps):
-    eng.run_async(handle)
-  ev1.record(stream)
-  torch.cuda.synchronize()
-  if world > 1:
-    dist.barrier()
-  t1 = time.perf_counter()
-  elapsed = t1 - t0
-  kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+  elapsed, kernel_ms = ctx.timed(lambda: eng.run_async(handle), args.steps)
+  total_sims = ctx.total(sims_per_step * args.steps)
 
-  total_sims = sims_per_step * args.steps
-  if world > 1:
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    s = torch.tensor([total_sims], dtype=torch.float64, device="cuda")
-    dist.all_reduce(s, op=dist.ReduceOp.SUM)
-    total_sims = int(s.item())
-
-  if rank == 0 and args.gpus == 1 and not args.no_cpu_baseline:
-    cpu = cpu_baseline(game, acts, offs, bot_seeds, eval_seeds, sims,
-                       args.cpu_seconds)
-
-  if rank == 0:
-    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
-    traffic = pmc_traffic(KERNEL[args.layout], game)
-    line = {
-        "metric": "MCTS simulations/sec (random rollout) on connect_four at "
-                  "1/2/4/8 MI355X" if args.config == "c2" else
-                  "MCTS simulations/sec (random rollout) on %s" % game,
-        "value": total_sims / elapsed,
-        "unit": "sims/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int32+f64",
-        "data": "synthetic (seeded random roots; no dataset)",
-        "config": {
-            "workload": "%s, %d independent roots x %d sims per GPU" %
-                        (game, R, sims),
-            "game": game, "roots_per_gpu": R, "sims_per_root": sims,
-            "uct_c": 2.0, "n_rollouts": 1, "solve": True,
-            "max_memory_mb": 1000, "root_plies": "k~U[0,%d] from mt19937(1000+i)" % plies,
-            "parallelism": "dp%d (independent roots, no collective)" % world,
-            "layout": args.layout,
-            "block_size": args.block or (64 if args.layout == "wave" else 16),
-            "sims_per_step_per_gpu": sims_per_step,
-        },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "kernel": KERNEL[args.layout],
-            "kernel_ms_per_launch": kernel_ms,
-            "algorithmic_bytes_per_launch": alg_bytes,
-            "algorithmic_bytes_per_sim": alg_bytes / max(sims_per_step, 1),
-        },
-        "cpu_baseline": cpu,
-        "parity": parity,
-        "tree_stats": stats,
-    }
-    print(json.dumps(line), flush=True)
-  if world > 1:
-    dist.destroy_process_group()
+  cpu = None
+  if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+    cpu = cpu_baseline_search(game, acts, offs, bot_seeds, eval_seeds, sims,
+                              args.cpu_seconds)
+  if ctx.rank != 0:
+    return None
+  lay = _resolved_layout(game, R, layout)
+  metric = ("MCTS simulations/sec (random rollout) on connect_four at 1/2/4/8 MI355X"
+            if args.config == "c2" else
+            "MCTS simulations/sec (random rollout) on %s" % game)
+  line = _base_line(args, ctx, metric, total_sims / elapsed, "sims/s", elapsed, {
+      "workload": "%s, %d independent roots x %d sims per GPU" % (game, R, sims),
+      "game": game, "roots_per_gpu": R, "sims_per_root": sims, "uct_c": 2.0,
+      "n_rollouts": 1, "solve": True, "max_memory_mb": 1000,
+      "root_plies": "k~U[0,%d] from mt19937(1000+i)" % plies,
+      "parallelism": "dp%d (independent roots, no collective)" % ctx.world,
+      "layout": lay, "block_size": args.block or (64 if lay == "wave" else 16),
+      "sims_per_step_per_gpu": sims_per_step})
+  line["roofline"] = _roofline(KERNEL[lay], game, alg_bytes, kernel_ms, sims_per_step, "sim")
+  line["cpu_baseline"] = cpu
+  line["parity"] = parity
+  line["tree_stats"] = stats
+  return line
 
 
-def cpu_baseline(game, acts, offs, bot_seeds, eval_seeds, sims, seconds):
-  """Oracle (reference-faithful restatement, "port") on the host cores."""
+# ---------------------------------------------------------------------------
+# c4: root-parallel MCTS on one position + RCCL all-reduce of root visits
+def bench_root_parallel(args, ctx, layout):
+  from os_amd import dist as D
+  _, game, T, sims, _ = CONFIGS[args.config]
+  T = args.roots or T
+  sims = args.sims or sims
+  params = dict(uct_c=2.0, max_simulations=sims, n_rollouts=1, max_memory_mb=1000,
+                solve=True, block_size=args.block, arena_nodes=args.arena_nodes,
+                layout=layout)
+  be = D.HipBackend(game, ctx.local)
+  ids = np.arange(ctx.rank * T, (ctx.rank + 1) * T, dtype=np.uint32)
+  be.prepare_root_parallel([], ids, ids + np.uint32(EVAL_OFFSET), **params)
+  torch = ctx.torch
+
+  def step():
+    v, w = be.run_root_parallel()
+    if ctx.world > 1:
+      ctx.dist.all_reduce(v)
+      ctx.dist.all_reduce(w)
+    return v, w
+
+  for _ in range(args.warmup):
+    v, w = step()
+  out = be.eng.fetch()
+  sims_per_step = be.eng.last_sims()
+  alg_bytes = be.eng.algorithmic_bytes(T)
+  stats = be.eng.stats()
+  # Self-consistency of the device reduction + oracle parity on a prefix.
+  local_v = np.zeros(be.num_actions, np.int64)
+  for r in range(T):
+    for k in range(int(out["nchild"][r])):
+      local_v[out["child_action"][r, k]] += out["child_n"][r, k]
+  lv = torch.from_numpy(local_v).cuda()
+  if ctx.world > 1:
+    ctx.dist.all_reduce(lv)
+  reduce_ok = bool(torch.equal(lv, v))
+  parity = None
+  if ctx.rank == 0:
+    og = _oracle(game)
+    pr = min(args.parity_roots, 4, T)
+    acts = np.zeros(0, np.int64)
+    offs = np.zeros(pr + 1, np.int64)
+    ref = og.mcts_batch(acts, offs, ids[:pr], ids[:pr] + np.uint32(EVAL_OFFSET),
+                        uct_c=2.0, max_simulations=sims, max_children=be.eng.max_children)
+    bad = [k for k in ("child_action", "child_n", "child_w", "root_n", "best_action")
+           if not np.array_equal(out[k][:pr], ref[k])]
+    parity = {"trees_checked": pr, "bit_exact": not bad, "mismatch_fields": bad,
+              "allreduce_equals_sum_of_trees": reduce_ok}
+
+  elapsed, kernel_ms = ctx.timed(step, args.steps)
+  total_sims = ctx.total(sims_per_step * args.steps)
+  cpu = None
+  if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+    acts = np.zeros(0, np.int64)
+    offs = np.zeros(T + 1, np.int64)
+    cpu = cpu_baseline_search(game, acts, offs, ids, ids + np.uint32(EVAL_OFFSET), sims,
+                              args.cpu_seconds)
+  if ctx.rank != 0:
+    return None
+  lay = _resolved_layout(game, T, layout)
+  line = _base_line(args, ctx, "MCTS simulations/sec (random rollout) on %s, "
+                    "root-parallel" % game, total_sims / elapsed, "sims/s", elapsed, {
+                        "workload": "%s initial position, %d trees x %d sims per GPU, "
+                                    "action-indexed root visits all-reduced" % (game, T, sims),
+                        "game": game, "trees_per_gpu": T, "sims_per_tree": sims,
+                        "parallelism": "root-parallel x%d (RCCL all_reduce int64[%d] + "
+                                       "f64[%d] per step)" % (ctx.world, be.num_actions,
+                                                              be.num_actions),
+                        "layout": lay, "sims_per_step_per_gpu": sims_per_step})
+  line["roofline"] = _roofline(KERNEL[lay], game, alg_bytes, kernel_ms, sims_per_step, "sim")
+  line["cpu_baseline"] = cpu
+  line["parity"] = parity
+  line["root_visits_top5"] = sorted(
+      ((int(n), int(a)) for a, n in enumerate(v.cpu().tolist())), reverse=True)[:5]
+  line["tree_stats"] = stats
+  return line
+
+
+# ---------------------------------------------------------------------------
+# c5: sharded random playouts (no tree)
+def bench_playouts(args, ctx, layout):
+  from os_amd import dist as D
+  _, game, N, _, _ = CONFIGS[args.config]
+  N = args.roots or N
+  start, count = D.shard(N, ctx.world, ctx.rank)
+  seeds = np.arange(start, start + count, dtype=np.uint32)
+  be = D.HipBackend(game, ctx.local)
+  be.prepare_playouts([], seeds)
+
+  def step():
+    c = be.run_playouts()
+    if ctx.world > 1:
+      ctx.dist.all_reduce(c)
+    return c
+
+  for _ in range(args.warmup):
+    c = step()
+  returns = be.eng.rollouts_fetch()
+  ret0 = returns[:, 0]
+  local = np.array([(ret0 > 0).sum(), (ret0 < 0).sum(), (ret0 == 0).sum()], np.int64)
+  lc = ctx.torch.from_numpy(local).cuda()
+  if ctx.world > 1:
+    ctx.dist.all_reduce(lc)
+  parity = None
+  if ctx.rank == 0:
+    pn = min(512, count)
+    ref = _oracle(game).rollouts([], seeds[:pn])
+    parity = {"playouts_checked": pn, "bit_exact": bool(np.array_equal(ref, returns[:pn])),
+              "counts_equal_returns": bool(ctx.torch.equal(lc, c))}
+  elapsed, kernel_ms = ctx.timed(step, args.steps)
+  cpu = None
+  if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+    cpu = cpu_baseline_playouts(game, args.cpu_seconds)
+  if ctx.rank != 0:
+    return None
+  line = _base_line(args, ctx, "random playouts/sec on %s" % game, N * args.steps / elapsed,
+                    "playouts/s", elapsed, {
+                        "workload": "%s initial position, %d playouts split over %d GPUs"
+                                    % (game, N, ctx.world),
+                        "game": game, "playouts_total": N,
+                        "parallelism": "sharded x%d (RCCL all_reduce int64[3] per step)"
+                                       % ctx.world, "layout": "lane"})
+  line["roofline"] = None
+  line["kernel_ms_per_launch"] = kernel_ms
+  line["cpu_baseline"] = cpu
+  line["parity"] = parity
+  line["outcomes"] = {"p0_wins": int(c[0]), "p1_wins": int(c[1]), "draws": int(c[2])}
+  return line
+
+
+# ---------------------------------------------------------------------------
+def _oracle(game):
   sys.path.insert(0, os.path.join(ROOT, "tests"))
   import oracle_lib
-  og = oracle_lib.Game(game)
+  return oracle_lib.Game(game)
+
+
+def cpu_baseline_search(game, acts, offs, bot_seeds, eval_seeds, sims, seconds):
+  """Oracle (reference-faithful restatement, "port") on the host cores."""
+  og = _oracle(game)
   threads = max(1, min(16, len(os.sched_getaffinity(0))))
   R = len(offs) - 1
   # Calibrate on a small prefix, then size the sample to ~`seconds`.
-  probe = min(R, 8 * threads)
-  secs, n = og.time_mcts_batch(acts[:offs[probe]], offs[:probe + 1],
-                               bot_seeds[:probe], eval_seeds[:probe],
-                               max_simulations=sims, threads=threads)
-  rate = n / max(secs, 1e-9)
-  want = int(min(R, max(probe, seconds * rate / max(n / probe, 1))))
-  secs, n = og.time_mcts_batch(acts[:offs[want]], offs[:want + 1],
-                               bot_seeds[:want], eval_seeds[:want],
-                               max_simulations=sims, threads=threads)
-  return {"value": n / secs, "unit": "sims/s", "cores": threads,
-          "kind": "port",
+  probe = min(R, 2 * threads)
+  secs, n = og.time_mcts_batch(acts[:offs[probe]], offs[:probe + 1], bot_seeds[:probe],
+                               eval_seeds[:probe], max_simulations=sims, threads=threads)
+  per_root = max(secs, 1e-9) / probe * threads  # seconds per root on one thread
+  want = int(min(R, max(probe, seconds * threads / per_root)))
+  secs, n = og.time_mcts_batch(acts[:offs[want]], offs[:want + 1], bot_seeds[:want],
+                               eval_seeds[:want], max_simulations=sims, threads=threads)
+  return {"value": n / secs, "unit": "sims/s", "cores": threads, "kind": "port",
           "sample": "%d of the %d roots x %d sims (%d sims, %.1f s), oracle "
                     "restatement of mcts.cc, %d threads" %
                     (want, R, sims, n, secs, threads)}
+
+
+def cpu_baseline_playouts(game, seconds):
+  """Oracle RandomRolloutEvaluator::Evaluate on host threads (ctypes drops the GIL)."""
+  threads = max(1, min(16, len(os.sched_getaffinity(0))))
+  t0 = time.perf_counter()
+  _oracle(game).rollouts([], np.arange(64, dtype=np.uint32))
+  per = (time.perf_counter() - t0) / 64
+  n_per = max(64, int(seconds / per))
+  games = [_oracle(game) for _ in range(threads)]
+
+  def work(i):
+    games[i].rollouts([], np.arange(i * n_per, (i + 1) * n_per, dtype=np.uint32))
+
+  ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+  t0 = time.perf_counter()
+  for t in ths:
+    t.start()
+  for t in ths:
+    t.join()
+  secs = time.perf_counter() - t0
+  return {"value": threads * n_per / secs, "unit": "playouts/s", "cores": threads,
+          "kind": "port", "sample": "%d playouts (seeds 0..%d) on %d threads, %.1f s, "
+          "oracle restatement of RandomRolloutEvaluator" % (threads * n_per,
+                                                           threads * n_per - 1, threads, secs)}
 
 
 def pmc_traffic(kernel, game):

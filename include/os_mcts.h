@@ -94,6 +94,7 @@ int os_engine_destroy(os_engine* e);
  * MT19937, back up the path in parallel), or one lane per search. */
 #define OS_LAYOUT_WAVE 0
 #define OS_LAYOUT_LANE 1
+#define OS_LAYOUT_AUTO 2  /* engine picks per game and batch size */
 
 #define OS_POLICY_CPP 0    /* mcts.cc: std::mt19937 bot + evaluator streams   */
 #define OS_POLICY_NUMPY 1  /* mcts.py: numpy RandomState (shared or separate) */
@@ -106,7 +107,7 @@ typedef struct {
   int32_t solve;                /* MCTSBot solve (MCTS-Solver backup) */
   int32_t policy;               /* OS_POLICY_* */
   int32_t block_size;           /* OS_LAYOUT_LANE only: lanes per workgroup (0 = default) */
-  int32_t layout;               /* OS_LAYOUT_WAVE (default) or OS_LAYOUT_LANE */
+  int32_t layout;               /* OS_LAYOUT_WAVE (0), OS_LAYOUT_LANE, OS_LAYOUT_AUTO */
   int64_t arena_nodes;          /* 0 = exact worst case; else nodes per root */
 } os_mcts_params;
 
@@ -152,9 +153,35 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
 int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
                       int64_t n_actions, int64_t n, int32_t n_rollouts,
                       const uint32_t* seeds, double* out_returns);
-/* Kernel layout for os_rollouts_batch: OS_LAYOUT_WAVE (default: one wave per
- * evaluator, uniform game code) or OS_LAYOUT_LANE (one lane per evaluator). */
+/* Kernel layout for os_rollouts_batch: OS_LAYOUT_LANE (default: one lane per
+ * evaluator) or OS_LAYOUT_WAVE (one wave per evaluator, uniform game code). */
 int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
+
+/* Device-resident rollout pipeline (go playouts/s): prepare
+ * uploads the root and n evaluator seeds; run launches the rollout kernel on
+ * `hip_stream` without host synchronisation; fetch synchronises and copies
+ * out_returns[2*i+{0,1}] (same as os_rollouts_batch, which is prepare + run +
+ * fetch).  Preparing rollouts invalidates a prepared search batch and vice
+ * versa (they share the engine's root/seed buffers). */
+int os_rollouts_prepare(os_engine* e, const int64_t* root_actions, int64_t n_actions,
+                        int64_t n, int32_t n_rollouts, const uint32_t* seeds);
+int os_rollouts_run_async(os_engine* e, void* hip_stream);
+int os_rollouts_fetch(os_engine* e, double* out_returns);
+/* Outcome counts of the last rollout run into DEVICE memory dev_counts[3]
+ * (int64: player 0 won, player 1 won, draw — by the sign of each evaluator's
+ * mean player-0 return), on hip_stream; overwrites dev_counts.  Lets ranks
+ * all-reduce the totals without a host round trip. */
+int os_rollouts_outcomes_async(os_engine* e, int64_t* dev_counts, void* hip_stream);
+
+/* Root-parallel MCTS (the reference has no root-parallel
+ * driver — each tree is one MCTSBot::MCTSearch, mcts.cc:325-428): action-indexed
+ * sums over the prepared roots of the last run of the root children's
+ * explore_count and total_reward (mcts.h:117-118), into DEVICE buffers
+ * dev_visits[num_actions] (int64) and dev_rewards[num_actions] (f64) on
+ * hip_stream, in a fixed summation order (deterministic).  num_actions >=
+ * NumDistinctActions.  The caller all-reduces them across GPUs (RCCL). */
+int os_engine_root_sums_async(os_engine* e, int32_t num_actions, int64_t* dev_visits,
+                              double* dev_rewards, void* hip_stream);
 
 /* ---- Device-resident pipeline (inputs already in HBM; for benchmarks) ---
  * prepare: upload roots + seeds and size the arena; run: launch the search

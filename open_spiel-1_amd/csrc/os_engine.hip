@@ -401,6 +401,76 @@ __global__ void k_rollouts(RollArgs a) {
   a.out[2 * i + 1] = s1 / a.n_rollouts;
 }
 
+// Root-parallel reduction: scatter each tree's root
+// children to a dense [R][A] action-indexed image, then sum every action's
+// column in a fixed order (deterministic, independent of scheduling).
+__global__ void k_root_scatter(const int32_t* nchild, const int32_t* cact, const int32_t* cn,
+                               const double* cw, int32_t mc, int64_t A, int32_t* dn,
+                               double* dw) {
+  const int64_t r = blockIdx.x;
+  const int nc = nchild[r];
+  for (int k = threadIdx.x; k < nc && k < mc; k += blockDim.x) {
+    const int32_t act = cact[r * mc + k];
+    if (act >= 0 && act < A) {
+      dn[r * A + act] = cn[r * mc + k];
+      dw[r * A + act] = cw[r * mc + k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_root_reduce(const int32_t* dn, const double* dw,
+                                                     int64_t R, int64_t A, int64_t* visits,
+                                                     double* rewards) {
+  __shared__ int64_t sn[256];
+  __shared__ double sw[256];
+  const int64_t a = blockIdx.x;
+  const int t = threadIdx.x;
+  int64_t n = 0;
+  double w = 0.0;
+  for (int64_t r = t; r < R; r += 256) {
+    n += dn[r * A + a];
+    w += dw[r * A + a];
+  }
+  sn[t] = n;
+  sw[t] = w;
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if (t < s) {
+      sn[t] += sn[t + s];
+      sw[t] += sw[t + s];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    visits[a] = sn[0];
+    rewards[a] = sw[0];
+  }
+}
+
+// Outcome counts of a rollout batch: [0] player 0 ahead, [1] player 1 ahead,
+// [2] draws (sign of the mean player-0 return of each evaluator).
+__global__ __launch_bounds__(256) void k_outcome_counts(const double* out, int64_t n,
+                                                        unsigned long long* counts) {
+  unsigned long long c0 = 0, c1 = 0, c2 = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const double v = out[2 * i];
+    c0 += v > 0.0;
+    c1 += v < 0.0;
+    c2 += v == 0.0;
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    c0 += __shfl_xor(c0, off);
+    c1 += __shfl_xor(c1, off);
+    c2 += __shfl_xor(c2, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&counts[0], c0);
+    atomicAdd(&counts[1], c1);
+    atomicAdd(&counts[2], c2);
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -447,17 +517,22 @@ struct os_engine {
   int32_t hash_stride = 1;
   bool import_state = false;
   bool shared_stream = false;
-  int32_t rollout_layout = OS_LAYOUT_WAVE;
+  int32_t rollout_layout = OS_LAYOUT_LANE;  // 4-140x faster than WAVE (profiles/r01)
+  // prepared rollout batch
+  int64_t roll_n = 0;
+  int32_t roll_nr = 1;
+  int32_t roll_nhash = 0;
+  bool roll_ready = false;
   DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
-      d_rollout_out;
+      d_rollout_out, d_dense_n, d_dense_w;
   std::vector<SearchResult> last_results;
   int64_t last_sims = 0;
   ~os_engine() {
     DevBuf* all[] = {&d_roots, &d_bseed, &d_eseed, &d_mt,  &d_arena, &d_lut,
                      &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
-                     &d_rout,  &d_best,  &d_rollout_out};
+                     &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w};
     (void)hipSetDevice(device);
     for (DevBuf* b : all) b->release();
   }
@@ -557,13 +632,24 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
     return Fail(OS_ERR_INVALID, "unknown policy");
   if (p->block_size < 0 || p->block_size > 1024)
     return Fail(OS_ERR_INVALID, "block_size must be in [0, 1024]");
-  if (p->layout != OS_LAYOUT_WAVE && p->layout != OS_LAYOUT_LANE)
+  if (p->layout != OS_LAYOUT_WAVE && p->layout != OS_LAYOUT_LANE &&
+      p->layout != OS_LAYOUT_AUTO)
     return Fail(OS_ERR_INVALID, "unknown layout");
   if (e->game.cfg.max_children > kMaxChildren)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxChildren");
   if (e->game.cfg.max_game_length >= kMaxPath)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxPath");
   return OS_OK;
+}
+
+// OS_LAYOUT_AUTO: one wave per search unless the batch alone fills the chip
+// with lane-per-search waves, or the game's per-ply work is wide (hex: the
+// lane layout was 3.5x faster at 4096 roots; profiles/r01/layout_probe.txt).
+int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R) {
+  if (layout != OS_LAYOUT_AUTO) return layout;
+  if (cfg.kind == kHex) return OS_LAYOUT_LANE;
+  if (R >= 64 * 1024) return OS_LAYOUT_LANE;  // >= 1024 waves: one per SIMD
+  return OS_LAYOUT_WAVE;
 }
 
 // Uploads roots / seeds, sizes and allocates the arena and outputs.
@@ -575,6 +661,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   if (R < 0) return Fail(OS_ERR_INVALID, "num_roots < 0");
   HIP_TRY(hipSetDevice(e->device));
   e->params = *p;
+  e->params.layout = ResolveLayout(e->game.cfg, p->layout, R);
   e->num_roots = R;
   const GameCfg& cfg = e->game.cfg;
   e->max_children = cfg.max_children;
@@ -665,6 +752,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     return rc;
   e->import_state = false;
   e->shared_stream = false;
+  e->roll_ready = false;  // rollouts and searches share the root/seed buffers
   return OS_OK;
 }
 
@@ -785,26 +873,18 @@ int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
   return OS_OK;
 }
 
-template <class G>
-int LaunchRollouts(os_engine* e, const HostState& root, int64_t n, int32_t nr,
-                   const uint32_t* seeds, double* out) {
+// Uploads one root + n evaluator seeds for the rollout kernels.
+int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
+                const uint32_t* seeds) {
   int rc;
   const size_t sb = e->game.state_bytes;
   if ((rc = e->d_roots.ensure(sb))) return rc;
   HIP_TRY(hipMemcpy(e->d_roots.p, root.raw, sb, hipMemcpyHostToDevice));
   if ((rc = e->d_bseed.ensure(std::max<int64_t>(n, 1) * 4))) return rc;
-  HIP_TRY(hipMemcpy(e->d_bseed.p, seeds, n * 4, hipMemcpyHostToDevice));
+  if (n > 0) HIP_TRY(hipMemcpy(e->d_bseed.p, seeds, n * 4, hipMemcpyHostToDevice));
   if ((rc = e->d_mt.ensure(std::max<int64_t>(n, 1) * kMtN * 4))) return rc;
   if ((rc = e->d_rollout_out.ensure(std::max<int64_t>(n, 1) * 16))) return rc;
-  RollArgs a;
-  std::memset(&a, 0, sizeof a);
-  a.cfg = e->game.cfg;
-  a.n = n;
-  a.n_rollouts = nr;
-  a.root = e->d_roots.p;
-  a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
-  a.mt = static_cast<uint32_t*>(e->d_mt.p);
-  a.out = static_cast<double*>(e->d_rollout_out.p);
+  e->roll_nhash = 0;
   if (e->game.cfg.kind == kGo) {
     if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
     HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
@@ -812,21 +892,53 @@ int LaunchRollouts(os_engine* e, const HostState& root, int64_t n, int32_t nr,
     if ((rc = e->d_rhash.ensure(std::max<size_t>(root.hashes.size(), 1) * 8))) return rc;
     HIP_TRY(hipMemcpy(e->d_rhash.p, root.hashes.data(), root.hashes.size() * 8,
                       hipMemcpyHostToDevice));
-    a.zob = static_cast<const uint64_t*>(e->d_zob.p);
-    a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
-    a.n_root_hashes = static_cast<int32_t>(root.hashes.size());
+    e->roll_nhash = static_cast<int32_t>(root.hashes.size());
   }
+  e->roll_n = n;
+  e->roll_nr = nr;
+  e->roll_ready = true;
+  e->num_roots = 0;  // the search buffers now hold no prepared batch
+  return OS_OK;
+}
+
+template <class G>
+int RollLaunch(os_engine* e, hipStream_t stream) {
+  RollArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.n = e->roll_n;
+  a.n_rollouts = e->roll_nr;
+  a.root = e->d_roots.p;
+  a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.out = static_cast<double*>(e->d_rollout_out.p);
+  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+  a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
+  a.n_root_hashes = e->roll_nhash;
+  const int64_t n = e->roll_n;
   if (e->rollout_layout == OS_LAYOUT_WAVE) {
-    hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, 0, a);
+    hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream, a);
   } else {
     const int bs = 64;
     hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                       dim3(bs), 0, 0, a);
+                       dim3(bs), 0, stream, a);
   }
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, e->d_rollout_out.p, n * 16, hipMemcpyDeviceToHost));
   return OS_OK;
+}
+
+int RollRun(os_engine* e, hipStream_t stream) {
+  if (!e->roll_ready) return Fail(OS_ERR_INVALID, "os_rollouts_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  if (e->roll_n == 0) return OS_OK;
+  switch (e->game.cfg.kind) {
+    case kTicTacToe: return RollLaunch<TicTacToe>(e, stream);
+    case kConnectFour: return RollLaunch<ConnectFour>(e, stream);
+    case kBreakthrough: return RollLaunch<Breakthrough>(e, stream);
+    case kHex: return RollLaunch<Hex>(e, stream);
+    case kGo: return RollLaunch<Go>(e, stream);
+  }
+  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
 }
 
 }  // namespace
@@ -1117,25 +1229,91 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
   return OS_OK;
 }
 
-int os_rollouts_batch(os_engine* e, const int64_t* root_actions, int64_t n_actions,
-                      int64_t n, int32_t n_rollouts, const uint32_t* seeds,
-                      double* out_returns) {
-  if (!e || !seeds || !out_returns) return Fail(OS_ERR_INVALID, "null argument");
+int os_rollouts_prepare(os_engine* e, const int64_t* root_actions, int64_t n_actions,
+                        int64_t n, int32_t n_rollouts, const uint32_t* seeds) {
+  if (!e || (n > 0 && !seeds)) return Fail(OS_ERR_INVALID, "null argument");
+  if (n < 0) return Fail(OS_ERR_INVALID, "n < 0");
+  if (n > 0x7FFFFFFFll * 64) return Fail(OS_ERR_CAPACITY, "too many evaluators");
   if (n_rollouts < 1) return Fail(OS_ERR_INVALID, "n_rollouts must be >= 1");
   HIP_TRY(hipSetDevice(e->device));
   HostState root;
   std::string err;
   if (!ReplayRoot(e->game, root_actions, n_actions, &root, &err))
     return Fail(OS_ERR_INVALID, err);
-  if (n == 0) return OS_OK;
-  switch (e->game.cfg.kind) {
-    case kTicTacToe: return LaunchRollouts<TicTacToe>(e, root, n, n_rollouts, seeds, out_returns);
-    case kConnectFour: return LaunchRollouts<ConnectFour>(e, root, n, n_rollouts, seeds, out_returns);
-    case kBreakthrough: return LaunchRollouts<Breakthrough>(e, root, n, n_rollouts, seeds, out_returns);
-    case kHex: return LaunchRollouts<Hex>(e, root, n, n_rollouts, seeds, out_returns);
-    case kGo: return LaunchRollouts<Go>(e, root, n, n_rollouts, seeds, out_returns);
+  return RollPrepare(e, root, n, n_rollouts, seeds);
+}
+
+int os_rollouts_run_async(os_engine* e, void* hip_stream) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return RollRun(e, static_cast<hipStream_t>(hip_stream));
+}
+
+int os_rollouts_fetch(os_engine* e, double* out_returns) {
+  if (!e || !out_returns) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->roll_ready) return Fail(OS_ERR_INVALID, "os_rollouts_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (e->roll_n > 0)
+    HIP_TRY(hipMemcpy(out_returns, e->d_rollout_out.p, e->roll_n * 16, hipMemcpyDeviceToHost));
+  return OS_OK;
+}
+
+int os_rollouts_outcomes_async(os_engine* e, int64_t* dev_counts, void* hip_stream) {
+  if (!e || !dev_counts) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->roll_ready) return Fail(OS_ERR_INVALID, "os_rollouts_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  HIP_TRY(hipMemsetAsync(dev_counts, 0, 3 * sizeof(int64_t), st));
+  if (e->roll_n == 0) return OS_OK;
+  const int64_t blocks = std::min<int64_t>((e->roll_n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_outcome_counts, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+                     static_cast<const double*>(e->d_rollout_out.p), e->roll_n,
+                     reinterpret_cast<unsigned long long*>(dev_counts));
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
+}
+
+int os_rollouts_batch(os_engine* e, const int64_t* root_actions, int64_t n_actions,
+                      int64_t n, int32_t n_rollouts, const uint32_t* seeds,
+                      double* out_returns) {
+  if (!e || (n > 0 && (!seeds || !out_returns))) return Fail(OS_ERR_INVALID, "null argument");
+  int rc = os_rollouts_prepare(e, root_actions, n_actions, n, n_rollouts, seeds);
+  if (rc) return rc;
+  if ((rc = RollRun(e, nullptr))) return rc;
+  return os_rollouts_fetch(e, out_returns);
+}
+
+int os_engine_root_sums_async(os_engine* e, int32_t num_actions, int64_t* dev_visits,
+                              double* dev_rewards, void* hip_stream) {
+  if (!e || !dev_visits || !dev_rewards) return Fail(OS_ERR_INVALID, "null argument");
+  if (num_actions < e->game.cfg.num_actions)
+    return Fail(OS_ERR_INVALID, "num_actions smaller than NumDistinctActions");
+  HIP_TRY(hipSetDevice(e->device));
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  const int64_t R = e->num_roots;
+  const int64_t A = num_actions;
+  int rc;
+  if ((rc = e->d_dense_n.ensure(static_cast<size_t>(std::max<int64_t>(R, 1)) * A * 4)) ||
+      (rc = e->d_dense_w.ensure(static_cast<size_t>(std::max<int64_t>(R, 1)) * A * 8)))
+    return rc;
+  if (R > 0) {
+    HIP_TRY(hipMemsetAsync(e->d_dense_n.p, 0, R * A * 4, st));
+    HIP_TRY(hipMemsetAsync(e->d_dense_w.p, 0, R * A * 8, st));
+    hipLaunchKernelGGL(k_root_scatter, dim3(static_cast<unsigned>(R)), dim3(128), 0, st,
+                       static_cast<const int32_t*>(e->d_nch.p),
+                       static_cast<const int32_t*>(e->d_cact.p),
+                       static_cast<const int32_t*>(e->d_cn.p),
+                       static_cast<const double*>(e->d_cw.p), e->max_children, A,
+                       static_cast<int32_t*>(e->d_dense_n.p),
+                       static_cast<double*>(e->d_dense_w.p));
+    HIP_TRY(hipGetLastError());
   }
-  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  hipLaunchKernelGGL(k_root_reduce, dim3(static_cast<unsigned>(A)), dim3(256), 0, st,
+                     static_cast<const int32_t*>(e->d_dense_n.p),
+                     static_cast<const double*>(e->d_dense_w.p), R, A, dev_visits,
+                     dev_rewards);
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
 }
 
 int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base,

@@ -24,6 +24,7 @@ POLICY_NUMPY = 1
 
 LAYOUT_WAVE = 0
 LAYOUT_LANE = 1
+LAYOUT_AUTO = 2
 
 if not os.path.exists(LIB_PATH):
   raise ImportError(
@@ -124,6 +125,11 @@ _sig("os_engine_fetch", ctypes.c_int,
 _sig("os_engine_last_sims", _i64, [_vp])
 _sig("os_engine_stats", ctypes.c_int, [_vp, _P])
 _sig("os_engine_set_rollout_layout", ctypes.c_int, [_vp, _i32])
+_sig("os_rollouts_prepare", ctypes.c_int, [_vp, _P, _i64, _i64, _i32, _P])
+_sig("os_rollouts_run_async", ctypes.c_int, [_vp, _vp])
+_sig("os_rollouts_fetch", ctypes.c_int, [_vp, _P])
+_sig("os_rollouts_outcomes_async", ctypes.c_int, [_vp, _vp, _vp])
+_sig("os_engine_root_sums_async", ctypes.c_int, [_vp, _i32, _vp, _vp, _vp])
 _sig("os_engine_node_bytes", _i32, [_vp])
 _sig("os_engine_state_bytes", _i32, [_vp])
 _sig("os_make_roots", _i64, [_vp, _i64, _u32, _i32, _P, _P])

@@ -20,7 +20,7 @@ UNSOLVED = 2
 
 def make_params(uct_c=2.0, max_simulations=1000, n_rollouts=1,
                 max_memory_mb=1000, solve=True, policy=_lib.POLICY_CPP,
-                block_size=0, arena_nodes=0, layout=_lib.LAYOUT_WAVE):
+                block_size=0, arena_nodes=0, layout=_lib.LAYOUT_AUTO):
   p = _lib.MctsParams()
   p.layout = int(layout)
   p.uct_c = float(uct_c)
@@ -147,7 +147,7 @@ class Engine:
                              ptr(t["nchild"]), ptr(t["out0"])))
     return t
 
-  def rollouts(self, history, seeds, n_rollouts=1, layout=_lib.LAYOUT_WAVE):
+  def rollouts(self, history, seeds, n_rollouts=1, layout=_lib.LAYOUT_LANE):
     """RandomRolloutEvaluator(n_rollouts, seed).Evaluate(root) per seed."""
     check(lib.os_engine_set_rollout_layout(self._h, int(layout)))
     acts = _lib.i64(history)
@@ -156,6 +156,32 @@ class Engine:
     check(lib.os_rollouts_batch(self._h, ptr(acts), len(acts), len(s),
                                 int(n_rollouts), ptr(s), ptr(out)))
     return out
+
+  def rollouts_prepare(self, history, seeds, n_rollouts=1, layout=_lib.LAYOUT_LANE):
+    """Device-resident rollout batch (see os_rollouts_prepare)."""
+    check(lib.os_engine_set_rollout_layout(self._h, int(layout)))
+    self._roll = (_lib.i64(history), _lib.u32(seeds))
+    acts, s = self._roll
+    check(lib.os_rollouts_prepare(self._h, ptr(acts), len(acts), len(s),
+                                  int(n_rollouts), ptr(s)))
+
+  def rollouts_run_async(self, stream=None):
+    check(lib.os_rollouts_run_async(self._h, stream))
+
+  def rollouts_fetch(self):
+    out = np.zeros((len(self._roll[1]), 2), np.float64)
+    check(lib.os_rollouts_fetch(self._h, ptr(out)))
+    return out
+
+  def rollouts_outcomes_async(self, dev_counts_ptr, stream=None):
+    """Writes int64[3] (p0 wins, p1 wins, draws) to a device address."""
+    check(lib.os_rollouts_outcomes_async(self._h, dev_counts_ptr, stream))
+
+  def root_sums_async(self, num_actions, dev_visits_ptr, dev_rewards_ptr, stream=None):
+    """Action-indexed root visit / reward sums of the last run into device
+    buffers int64[num_actions] / f64[num_actions] (root-parallel MCTS)."""
+    check(lib.os_engine_root_sums_async(self._h, int(num_actions), dev_visits_ptr,
+                                        dev_rewards_ptr, stream))
 
   # ---- device-resident pipeline (bench) ----
   def prepare(self, root_actions, root_offsets, bot_seeds, eval_seeds=None,
