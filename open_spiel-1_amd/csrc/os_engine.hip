@@ -1,12 +1,14 @@
 // libos_mcts.so — gfx950 search / rollout kernels and the C-ABI declared in
 // include/os_mcts.h.
 //
-// Execution model: one lane = one independent search
-// (MCTSBot::MCTSearch, mcts.cc:325-428).  A lane keeps its working game state
-// in registers, its two MT19937 streams (bot + evaluator, 2 x 624 words) and
-// its flat node arena in HBM, and its path / expansion buffers in private
-// scratch.  Searches never share memory, so there are no atomics and results
-// are bit-exact regardless of scheduling.
+// Execution model: every root is one independent search
+// (MCTSBot::MCTSearch, mcts.cc:325-428) with its own flat node arena in HBM.
+//   k_wsearch (OS_LAYOUT_WAVE): one 64-lane wavefront per search; game state
+//     wave-uniform in SGPRs, MT19937 streams + visit path in LDS (os_wave.h).
+//   k_mcts (OS_LAYOUT_LANE): one lane per search; game state in VGPRs, MT
+//     streams in HBM, path / expansion buffers in LDS slices (os_mcts.h).
+// Searches never share memory, so there are no atomics in the search and
+// results are bit-exact regardless of scheduling.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

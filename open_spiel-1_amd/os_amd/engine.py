@@ -3,8 +3,9 @@
 `Engine(game_string, device)` replaces a population of the reference's
 `algorithms::MCTSBot` + `RandomRolloutEvaluator` pairs
 (open_spiel/algorithms/mcts.h:92-159): `mcts_batch` runs one independent
-`MCTSBot::MCTSearch` (mcts.cc:325-428) per root on the GPU, one lane per
-search, bit-exact with the reference for the same seeds.
+`MCTSBot::MCTSearch` (mcts.cc:325-428) per root on the GPU (one wavefront
+or one lane per search), bit-exact with the reference for the
+same seeds.
 """
 import ctypes
 
