@@ -273,18 +273,74 @@ __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
   }
 }
 
-// Wave argmax: max v, lowest index among equal maxima (== first maximum of a
-// strict '>' scan in index order).  Returns the index (uniform).
-__device__ __forceinline__ int wave_argmax(double v, int idx) {
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ov = __shfl_xor(v, off);
-    const int oi = __shfl_xor(idx, off);
-    if (ov > v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
+// v from the lane selected by DPP control `Ctrl`; lanes without a source (or
+// rows outside RowMask) keep `v` itself.
+template <int Ctrl, int RowMask = 0xf>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int nlo = __builtin_amdgcn_update_dpp(lo, lo, Ctrl, RowMask, 0xf, false);
+  const int nhi = __builtin_amdgcn_update_dpp(hi, hi, Ctrl, RowMask, 0xf, false);
+  return __hiloint2double(nhi, nlo);
+}
+
+// Wave-uniform maximum of v over all 64 lanes (all lanes active) by DPP:
+// butterflies within each 16-lane row (quad_perm 1032 / 2301, half-mirror,
+// mirror), then the row_bcast15 / row_bcast31 scan across rows; lane 63 ends
+// with the maximum.  `Lanes` (<= 64) bounds the lanes that can hold a
+// candidate (the others hold -inf), so narrow games skip the cross-row steps.
+template <int Lanes>
+__device__ __forceinline__ double wave_max_f64(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));  // quad_perm [1,0,3,2]
+  if (Lanes > 2) v = fmax(v, dpp_f64<0x4E>(v));   // quad_perm [2,3,0,1]
+  if (Lanes > 4) v = fmax(v, dpp_f64<0x141>(v));  // row_half_mirror
+  if (Lanes > 8) v = fmax(v, dpp_f64<0x140>(v));  // row_mirror
+  if (Lanes > 16) {
+    v = fmax(v, dpp_f64<0x142, 0xa>(v));  // row_bcast15 -> rows 1, 3
+    v = fmax(v, dpp_f64<0x143, 0xc>(v));  // row_bcast31 -> rows 2, 3
+    return rld(v, 63);
   }
-  return rli(idx, 0);
+  return rld(v, 0);
+}
+
+// Wave argmax over a lane-distributed candidate array: element k = l + 64 h
+// has value v0 (h = 0) or v1 (h = 1) in lane l; absent elements hold -inf.
+// Returns the LOWEST index among the maxima (== the first maximum of
+// mcts.cc's strict '>' scan in index order), wave-uniform.  No NaNs occur
+// (UCT values are finite, +inf or solver outcomes); -0 == +0 as in '>'.
+template <int Lanes, bool TwoSlots>
+__device__ __forceinline__ int wave_argmax2(double v0, double v1) {
+  const double m = wave_max_f64<Lanes>(TwoSlots ? fmax(v0, v1) : v0);
+  const uint64_t b0 = ballot(v0 == m);
+  if (b0) return ctz64(b0);
+  return 64 + ctz64(ballot(v1 == m));
+}
+
+// Lanes that can hold a child of a node (compile-time, per game): the UCT
+// argmax only reduces over those; TwoSlots when a node can have > 64 children.
+template <class G>
+struct WaveWidth {
+  static constexpr int kLanes = 64;
+  static constexpr bool kTwoSlots = true;
+};
+template <>
+struct WaveWidth<TicTacToe> {  // <= 9 children
+  static constexpr int kLanes = 16;
+  static constexpr bool kTwoSlots = false;
+};
+template <>
+struct WaveWidth<ConnectFour> {  // <= 7 children
+  static constexpr int kLanes = 8;
+  static constexpr bool kTwoSlots = false;
+};
+
+// SearchNode::UCTValue (mcts.cc:89-100) for the player to move at the parent.
+template <class R>
+__device__ __forceinline__ double uct_value(const Node<R>& c, int cp, double logN,
+                                            double uct_c) {
+  if (c.out != kUnsolved) return outcome_for(c.out, cp);
+  if (c.n == 0) return __builtin_huge_val();
+  const double dn = static_cast<double>(c.n);
+  return static_cast<double>(c.w) / dn + uct_c * __builtin_sqrt(logN / dn);
 }
 
 template <class G, int Policy, class Rng, class C>
@@ -338,6 +394,11 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   int nodes_count = 1;
   int gc_limit = 5;
   const double inf = __builtin_huge_val();
+  using WW = WaveWidth<G>;
+  Node<R> zero_node;
+  zero_node.first = 0; zero_node.n = 0; zero_node.w = 0; zero_node.action = 0;
+  zero_node.nchild = 0; zero_node.out = kUnsolved;
+  double root_logN = sp.log_lut[0];
 
   for (int sim = 0; sim < sp.max_simulations; ++sim) {
     uint64_t t_ph = OS_PH_NOW();
@@ -347,6 +408,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     uint32_t cur_first = root_first;
     int32_t cur_n = root_n;
     int cur_nc = root_nc;
+    double cur_logN = root_logN;  // log(N) of the node being scanned (mcts.cc:99)
     int depth = 0;
     // ---- selection / expansion ----
     for (;;) {
@@ -415,35 +477,27 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         c_w = 0;
         OS_PH_ADD(ph.c[kPhExpand], t_ex);
       } else {
+        // Lane k scores child k (and k + 64); each lane also fetches
+        // log(n) of its own child, which is log(N_parent) one level down if
+        // that child is chosen, so the next level needs no dependent load.
         const int cp = P0 ^ (depth & 1);
-        const double logN = sp.log_lut[cur_n];
         res.scanned += cur_nc;
-        double bv = -inf;
-        int bk = 1 << 20;
-        Node<R> bc;
-        bc.first = 0; bc.n = 0; bc.w = 0; bc.action = 0; bc.nchild = 0; bc.out = kUnsolved;
-        for (int h = 0; h < 2; ++h) {
-          const int k = l + 64 * h;
-          if (k < cur_nc) {
-            const Node<R> c = nodes[cur_first + k];
-            double v;
-            if (c.out != kUnsolved) {
-              v = outcome_for(c.out, cp);
-            } else if (c.n == 0) {
-              v = inf;
-            } else {
-              const double dn = static_cast<double>(c.n);
-              v = static_cast<double>(c.w) / dn + sp.uct_c * __builtin_sqrt(logN / dn);
-            }
-            if (v > bv) {  // h == 1 only replaces on strict improvement
-              bv = v;
-              bk = k;
-              bc = c;
-            }
-          }
+        Node<R> c0 = zero_node, c1 = zero_node;
+        double v0 = -inf, v1 = -inf, lg0 = 0.0, lg1 = 0.0;
+        if (l < cur_nc) {
+          c0 = nodes[cur_first + l];
+          lg0 = sp.log_lut[c0.n];
+          v0 = uct_value(c0, cp, cur_logN, sp.uct_c);
         }
-        chosen = wave_argmax(bv, bk);
+        if (WW::kTwoSlots && l + 64 < cur_nc) {
+          c1 = nodes[cur_first + l + 64];
+          lg1 = sp.log_lut[c1.n];
+          v1 = uct_value(c1, cp, cur_logN, sp.uct_c);
+        }
+        chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
         const int src = chosen & 63;
+        const bool hi = WW::kTwoSlots && chosen >= 64;  // wave-uniform
+        const Node<R> bc = hi ? c1 : c0;
         c_action = rl32(bc.action, src);
         c_first = rl32(bc.first, src);
         c_n = rli(bc.n, src);
@@ -454,6 +508,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         } else {
           c_w = static_cast<R>(rld(static_cast<double>(bc.w), src));
         }
+        cur_logN = rld(hi ? lg1 : lg0, src);
       }
       G::apply(s, g, ctx, static_cast<int>(c_action));
       if (++depth >= path_cap) {
@@ -521,6 +576,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         }
       }
       root_n += 1;
+      root_logN = sp.log_lut[root_n];  // next simulation's root scan
       root_w += P0 == 0 ? rv0 : rv1;
       if (l == 0) {
         nodes[0].n = root_n;
