@@ -108,12 +108,14 @@ struct TicTacToe {
 // connect_four: 6 rows x 7 cols, column-major bitboard, 7 bits per column
 // (6 cells + an always-empty sentinel), bit = col * 7 + row, row 0 = bottom.
 struct ConnectFour {
+  // Dword fields (no byte packing on the scalar unit); `legal` is the
+  // playable-column mask kept incrementally by apply().
   struct State {
     uint64_t bb[2];
-    uint8_t to_play;
-    int8_t outcome;  // -1 unknown, 0/1 winner, 2 draw
-    uint8_t moves;
-    uint8_t pad[5];
+    int32_t to_play;
+    int32_t outcome;  // -1 unknown, 0/1 winner, 2 draw
+    int32_t moves;
+    uint32_t legal;   // bit c = column c not full (LegalActions, ascending)
     static constexpr bool kNeedsLog = false;
   };
   using Ctx = NoCtx;
@@ -123,7 +125,12 @@ struct ConnectFour {
   struct Legal {
     uint32_t mask;  // bit c = column c playable
     int count;
-    OS_HD int kth(int k) const { return select64(mask, k); }
+    // k-th set bit of a <= 7-bit mask: drop the k lowest bits.
+    OS_HD int kth(int k) const {
+      uint32_t m = mask;
+      for (int i = 0; i < k; ++i) m &= m - 1;
+      return ctz64(m);
+    }
   };
   OS_HD static bool has_four(uint64_t b) {
     uint64_t m = b & (b >> 1);
@@ -137,18 +144,14 @@ struct ConnectFour {
     return false;
   }
   OS_HD static void init(State& s, const GameCfg&) {
-    s.bb[0] = s.bb[1] = 0; s.to_play = 0; s.outcome = -1; s.moves = 0;
-    for (int i = 0; i < 5; ++i) s.pad[i] = 0;
+    s.bb[0] = s.bb[1] = 0; s.to_play = 0; s.outcome = -1; s.moves = 0; s.legal = 0x7f;
   }
   OS_HD static bool terminal(const State& s, const GameCfg&) { return s.outcome >= 0; }
   OS_HD static int to_move(const State& s) { return s.to_play; }
   OS_HD static Legal legal(const State& s, const GameCfg&, Ctx&) {
-    const uint64_t top = (s.bb[0] | s.bb[1]) & kTopRow;
-    uint32_t m = 0;
-    for (int c = 0; c < 7; ++c) m |= static_cast<uint32_t>(((top >> (7 * c + 5)) & 1) ^ 1) << c;
     Legal l;
-    l.mask = m;
-    l.count = popc64(m);
+    l.mask = s.legal;
+    l.count = popc64(s.legal);
     return l;
   }
   OS_HD static void apply(State& s, const GameCfg&, Ctx&, int col) {
@@ -159,9 +162,10 @@ struct ConnectFour {
     const uint64_t mine = pick(s.bb, p) | mv;
     put(s.bb, p, mine);
     s.moves++;
-    if (has_four(mine)) s.outcome = static_cast<int8_t>(p);
+    if (mv & kTopRow) s.legal &= ~(1u << col);  // column now full
+    if (has_four(mine)) s.outcome = p;
     else if (s.moves == 42) s.outcome = 2;
-    s.to_play = static_cast<uint8_t>(1 - p);
+    s.to_play = 1 - p;
   }
   OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) {
     return s.outcome == 0 ? 1 : (s.outcome == 1 ? -1 : 0);

@@ -90,12 +90,18 @@ template <class G>
 OS_HD uint32_t AbslUniform(G& g, uint32_t n) {
   uint64_t hi = g.next();
   uint64_t lo = g.next();
+  if ((n & (n - 1u)) == 0) return static_cast<uint32_t>(lo) & (n - 1u);  // 2^k: low bits
+  // bits * n with bits = hi:lo and n < 2^32, in 32x32->64 pieces:
+  //   P = (hi*n << 32) + lo*n;  P >> 64 = (hi*n + (lo*n >> 32)) >> 32 (no overflow);
+  //   P mod 2^64 = low32(mid):low32(lo*n) with mid = hi*n + (lo*n >> 32).
+  const uint64_t b = lo * n;
+  const uint64_t mid = hi * n + (b >> 32);
+  if (static_cast<uint32_t>(mid) != 0 || static_cast<uint32_t>(b) >= n)
+    return static_cast<uint32_t>(mid >> 32);  // P mod 2^64 >= n: no rejection test
   uint64_t bits = (hi << 32) | lo;
-  const uint64_t R = static_cast<uint64_t>(n) - 1;
-  if ((R & static_cast<uint64_t>(n)) == 0) return static_cast<uint32_t>(bits & R);
   uint64_t plo = bits * n;
   uint64_t phi = umulhi64(bits, n);
-  if (plo < n) {
+  {
     const uint64_t thr = (0ull - static_cast<uint64_t>(n)) % n;
     while (plo < thr) {
       hi = g.next();

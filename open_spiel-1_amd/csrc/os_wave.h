@@ -22,14 +22,19 @@
 
 #include "os_mcts.h"
 
-// Re-assert wave-uniformity of the playout state each rollout ply / of the
-// walk state each selection step (A/B switches; measured on MI355X, C4 4096x1024:
-// ROLL=0,SEL=1 25.6 ms; 0,0 25.8; 1,1 27.8; 1,0 28.5 — profiles/r01/ab_uniform.txt).
+// Where wave-uniformity of the playout / walk state is re-asserted with
+// readfirstlane (A/B switches): 0 never, 1 every ply / step, 2 once on entry
+// to the loop (so the loop-carried state can stay in SGPRs).  Measured on
+// MI355X, C4 4096 x 1024 (profiles/r01/ab_uniform.txt): ROLL/SEL 0/1 25.6 ms,
+// 1/1 27.8, 1/0 28.5; with the DPP argmax 0/1 23.75, 2/1 23.3, 2/2 22.8.
 #ifndef OS_UNI_ROLL
-#define OS_UNI_ROLL 0
+#define OS_UNI_ROLL 2
 #endif
 #ifndef OS_UNI_SEL
-#define OS_UNI_SEL 1
+#define OS_UNI_SEL 2
+#endif
+#ifndef OS_UNI_MT
+#define OS_UNI_MT 0
 #endif
 // Diagnostic build (-DOS_PHASE_TIMING=1): per-phase shader-clock cycles of the
 // wave search, summed over waves into PhaseCycles (os_debug_phase_cycles).
@@ -170,7 +175,20 @@ struct WaveMt {
     cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
     pos = 0;
   }
+  __device__ void uniformize() {
+    pos = __builtin_amdgcn_readfirstlane(pos);
+    valid = __builtin_amdgcn_readfirstlane(valid);
+    base = __builtin_amdgcn_readfirstlane(base);
+    words = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(words)));
+  }
   __device__ uint32_t next() {
+#if OS_UNI_MT
+    // The counters are wave-uniform; say so, or a divergent loop exit upstream
+    // (temporal divergence) leaves them in VGPRs with exec-masked branches.
+    pos = __builtin_amdgcn_readfirstlane(pos);
+    valid = __builtin_amdgcn_readfirstlane(valid);
+    base = __builtin_amdgcn_readfirstlane(base);
+#endif
     if (pos >= valid) refill();
     const uint32_t w = rl32(cur, pos);
     ++pos;
@@ -345,8 +363,12 @@ __device__ __forceinline__ double uct_value(const Node<R>& c, int cp, double log
 
 template <class G, int Policy, class Rng, class C>
 __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
+#if OS_UNI_ROLL == 2
+  s = make_uniform(s);  // uniform on entry => the loop-carried state can stay in SGPRs
+  ev.uniformize();
+#endif
   for (;;) {
-#if OS_UNI_ROLL
+#if OS_UNI_ROLL == 1
     s = make_uniform(s);  // keep the playout on the scalar unit
 #endif
     if (G::terminal(s, g)) break;
@@ -410,9 +432,18 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     int cur_nc = root_nc;
     double cur_logN = root_logN;  // log(N) of the node being scanned (mcts.cc:99)
     int depth = 0;
+#if OS_UNI_SEL == 2
+    s = make_uniform(s);
+    cur_n = __builtin_amdgcn_readfirstlane(cur_n);
+    cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
+    cur_first = static_cast<uint32_t>(
+        __builtin_amdgcn_readfirstlane(static_cast<int>(cur_first)));
+    cur_logN = make_uniform(cur_logN);
+    bot.uniformize();
+#endif
     // ---- selection / expansion ----
     for (;;) {
-#if OS_UNI_SEL
+#if OS_UNI_SEL == 1
       s = make_uniform(s);
       cur_n = __builtin_amdgcn_readfirstlane(cur_n);
       cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
