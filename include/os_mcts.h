@@ -157,6 +157,34 @@ int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
  * evaluator) or OS_LAYOUT_WAVE (one wave per evaluator, uniform game code). */
 int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
 
+/* ---- Self-play -----------------------------------
+ * num_games independent games, each played on the device the way
+ * examples/mcts_example.cc:77-136 PlayGame drives two MCTSBots sharing ONE
+ * RandomRolloutEvaluator (mcts_example.cc:151-157; evaluate_bots.cc:21-60):
+ * every move is bots[CurrentPlayer]->Step(state) = MCTSearch + BestChild
+ * (mcts.cc:219-226), the bots' rng_ (seeds bot_seeds[2g], bot_seeds[2g+1])
+ * and the evaluator's rng (eval_seeds[g]) persisting across moves;
+ * MCTSBot::InformAction / Restart are no-ops (mcts.h:162-163).  Game g starts
+ * from history start_actions[start_offsets[g] .. start_offsets[g+1]).
+ * Outputs: actions[g][max_len] (-1 padded), length[g], returns[g][2], and, if
+ * visits != NULL (record_visits != 0 at prepare), visits[g][move][A] = the
+ * root children's explore_count indexed by action (A = NumDistinctActions),
+ * i.e. the MCTS policy targets of the trajectory.  C++ policy only
+ * (OS_POLICY_NUMPY -> OS_ERR_UNSUPPORTED).  A game longer than max_len fails
+ * with OS_ERR_CAPACITY. */
+int os_selfplay(os_engine* e, const os_mcts_params* p, int64_t num_games,
+                const int64_t* start_actions, const int64_t* start_offsets,
+                const uint32_t* bot_seeds, const uint32_t* eval_seeds, int32_t max_len,
+                int64_t* actions, int32_t* length, double* returns, int32_t* visits);
+/* The same as prepare / run (async, on hip_stream) / fetch (synchronising). */
+int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games,
+                        const int64_t* start_actions, const int64_t* start_offsets,
+                        const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                        int32_t max_len, int32_t record_visits);
+int os_selfplay_run_async(os_engine* e, void* hip_stream);
+int os_selfplay_fetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
+                      int32_t* visits);
+
 /* Device-resident rollout pipeline (go playouts/s): prepare
  * uploads the root and n evaluator seeds; run launches the rollout kernel on
  * `hip_stream` without host synchronisation; fetch synchronises and copies

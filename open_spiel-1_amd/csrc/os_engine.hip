@@ -305,6 +305,173 @@ __global__ __launch_bounds__(64) void k_wsearch(DevArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Self-play: one wave plays a whole game the way
+// examples/mcts_example.cc:77-136 PlayGame does with two MCTSBots sharing one
+// RandomRolloutEvaluator: every move is bots[CurrentPlayer]->Step(state) =
+// MCTSearch + BestChild (mcts.cc:219-226, 325-428), both bots' rng_ and the
+// shared evaluator's rng persist across moves.
+struct SpArgs {
+  GameCfg cfg;
+  SearchParams sp;
+  int64_t num_games;      // games in this launch
+  int64_t game_base;      // global index of the first game of this launch
+  const void* starts;     // [total] G::State
+  const uint32_t* bot_seeds;   // [total][2]
+  const uint32_t* eval_seeds;  // [total]
+  void* arena;            // [num_games][cap] Node<R>
+  uint32_t cap;
+  int32_t path_cap;
+  int32_t max_len;        // trajectory slots per game
+  int32_t num_actions;
+  // go: per-game position history (grows by one per move)
+  const uint64_t* zob;
+  uint64_t* hist;         // [total][hash_stride]
+  int32_t* hist_n;        // [total]
+  int32_t hash_stride;
+  // outputs
+  int32_t* actions;       // [total][max_len], -1 padded
+  int32_t* length;        // [total]
+  double* returns;        // [total][2]
+  int32_t* visits;        // [total][max_len][num_actions] or null
+  SearchResult* results;  // [total], summed over the game's searches
+};
+
+template <class G>
+struct SpCtx {  // games without a history context
+  __device__ static NoCtx make(const SpArgs&, int64_t, uint64_t*) { return NoCtx(); }
+  __device__ static void commit(NoCtx&, const SpArgs&, int64_t) {}
+};
+template <>
+struct SpCtx<Go> {
+  __device__ static GoWaveCtx make(const SpArgs& a, int64_t gg, uint64_t* log) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.hist + gg * a.hash_stride;
+    c.n_base = a.hist_n[gg];
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+  // The move just applied logged its position (go.cc:199-208): append it to
+  // the game history that the next searches treat as "before the root".
+  __device__ static void commit(GoWaveCtx& c, const SpArgs& a, int64_t gg) {
+    uint64_t* h = a.hist + gg * a.hash_stride;
+    if (lane_id() == 0)
+      for (int i = 0; i < c.n_log && c.n_base + i < a.hash_stride; ++i) h[c.n_base + i] = c.log[i];
+    __threadfence_block();
+    c.n_base = c.n_base + c.n_log < a.hash_stride ? c.n_base + c.n_log : a.hash_stride;
+    c.init_filters();
+  }
+};
+
+template <class G, class R>
+__host__ __device__ constexpr size_t SelfPlayLdsBytes(int path_cap) {
+  return static_cast<size_t>(3 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
+}
+
+template <class G, class R>
+__global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
+  const int64_t lg = blockIdx.x;
+  if (lg >= a.num_games) return;
+  const int64_t gg = a.game_base + lg;
+  const int l = lane_id();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 3 * kMtN * 4);
+  uint64_t* glog = reinterpret_cast<uint64_t*>(
+      smem + ((3 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  WaveMt b0, b1, ev;
+  b0.s = mt;
+  b1.s = mt + kMtN;
+  ev.s = mt + 2 * kMtN;
+  if (l == 0) {
+    mt_seed(b0.s, a.bot_seeds[2 * gg]);
+    mt_seed(b1.s, a.bot_seeds[2 * gg + 1]);
+    mt_seed(ev.s, a.eval_seeds[gg]);
+  }
+  __syncthreads();
+  b0.init_seeded();
+  b1.init_seeded();
+  ev.init_seeded();
+  typename G::State s = make_uniform(static_cast<const typename G::State*>(a.starts)[gg]);
+  typename WaveCtxOf<G>::type ctx = SpCtx<G>::make(a, gg, glog);
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lg * static_cast<int64_t>(a.cap);
+  PhaseCycles ph = {};
+  SearchResult tot;
+  tot.status = kOk;
+  tot.sims = tot.nodes = tot.gc_runs = tot.max_depth = 0;
+  tot.used = tot.scanned = tot.backed = tot.expanded = tot.solver_scanned = 0;
+  tot.rng_words = tot.pad = 0;
+  int m = 0;
+  while (!G::terminal(s, a.cfg)) {
+    if (m >= a.max_len) {
+      tot.status = kGameOverflow;
+      break;
+    }
+    const int p = G::to_move(s);
+    WaveMt bot = p == 0 ? b0 : b1;
+    const SearchResult r =
+        wave_search<G, R, kPolicyCpp>(a.cfg, a.sp, s, ctx, nodes, a.cap, bot, ev, path,
+                                      a.path_cap, ph);
+    if (p == 0) b0 = bot;
+    else b1 = bot;
+    tot.sims += r.sims;
+    tot.nodes += r.nodes;
+    tot.used = r.used > tot.used ? r.used : tot.used;
+    tot.gc_runs += r.gc_runs;
+    tot.max_depth = r.max_depth > tot.max_depth ? r.max_depth : tot.max_depth;
+    tot.scanned += r.scanned;
+    tot.backed += r.backed;
+    tot.expanded += r.expanded;
+    tot.solver_scanned += r.solver_scanned;
+    if (r.status != kOk) {
+      tot.status = r.status;
+      break;
+    }
+    __threadfence_block();
+    // MCTSBot::Step: BestChild of the root (mcts.cc:222-225).
+    int bi = 0;
+    if (l == 0) bi = best_child(nodes, p);
+    bi = rli(bi, 0);
+    const uint32_t rfirst = static_cast<uint32_t>(rli(static_cast<int>(nodes[0].first), 0));
+    const int rnc = rli(nodes[0].nchild, 0);
+    const int act = rli(nodes[rfirst + bi].action, 0);
+    if (a.visits) {
+      int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+      for (int i = l; i < a.num_actions; i += 64) v[i] = 0;
+      __threadfence_block();
+      for (int k = l; k < rnc; k += 64) {
+        const Node<R> c = nodes[rfirst + k];
+        v[c.action] = c.n;
+      }
+    }
+    if (l == 0) a.actions[gg * a.max_len + m] = act;
+    ctx.reset();
+    G::apply(s, a.cfg, ctx, act);
+    SpCtx<G>::commit(ctx, a, gg);
+    s = make_uniform(s);
+    ++m;
+  }
+  tot.rng_words = b0.words + b1.words + ev.words;
+  for (int k = m + l; k < a.max_len; k += 64) a.actions[gg * a.max_len + k] = -1;
+  if (a.visits) {  // rows after the last move are all-zero policy targets
+    int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.num_actions;
+    for (int64_t i = l; i < nz; i += 64) v[i] = 0;
+  }
+  if (l == 0) {
+    const int r0 = G::terminal(s, a.cfg) ? G::ret0(s, a.cfg, ctx) : 0;
+    a.length[gg] = m;
+    a.returns[2 * gg] = static_cast<double>(r0);
+    a.returns[2 * gg + 1] = static_cast<double>(-r0);
+    a.results[gg] = tot;
+  }
+}
+
 struct RollArgs {
   GameCfg cfg;
   int64_t n;
@@ -525,16 +692,22 @@ struct os_engine {
   int32_t roll_nr = 1;
   int32_t roll_nhash = 0;
   bool roll_ready = false;
+  // prepared self-play batch
+  int64_t sp_games = 0;
+  int32_t sp_max_len = 0;
+  bool sp_visits = false;
+  bool sp_ready = false;
   DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
-      d_rollout_out, d_dense_n, d_dense_w;
+      d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis;
   std::vector<SearchResult> last_results;
   int64_t last_sims = 0;
   ~os_engine() {
     DevBuf* all[] = {&d_roots, &d_bseed, &d_eseed, &d_mt,  &d_arena, &d_lut,
                      &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
-                     &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w};
+                     &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
+                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis};
     (void)hipSetDevice(device);
     for (DevBuf* b : all) b->release();
   }
@@ -754,7 +927,8 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     return rc;
   e->import_state = false;
   e->shared_stream = false;
-  e->roll_ready = false;  // rollouts and searches share the root/seed buffers
+  e->roll_ready = false;  // rollouts, searches and self-play share buffers
+  e->sp_ready = false;
   return OS_OK;
 }
 
@@ -875,6 +1049,205 @@ int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
   return OS_OK;
 }
 
+// Node capacity per tree: the exact worst case 1 + sims * max_children (one
+// expansion per simulation at most), plus the GC stack reserve when GC can
+// fire (mcts.cc:402-424), unless the caller caps it.
+int ArenaCap(const os_engine* e, const os_mcts_params* p, uint32_t* cap_out) {
+  const GameCfg& cfg = e->game.cfg;
+  int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * cfg.max_children;
+  const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+  if (max_nodes > 1 && worst >= max_nodes) worst += GcStackReserve(cfg.max_children);
+  int64_t cap = p->arena_nodes > 0 ? std::min<int64_t>(p->arena_nodes, worst) : worst;
+  if (cap < 1) cap = 1;
+  if (cap > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "arena too large per tree");
+  *cap_out = static_cast<uint32_t>(cap);
+  return OS_OK;
+}
+
+// Self-play batch: replays the start positions, uploads them with the seeds
+// and sizes one tree arena per game (reused by every move's search).
+int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* start_actions,
+              const int64_t* start_offsets, const uint32_t* bot_seeds,
+              const uint32_t* eval_seeds, int32_t max_len, bool with_visits) {
+  int rc = CheckParams(e, p);
+  if (rc) return rc;
+  if (p->policy != OS_POLICY_CPP)
+    return Fail(OS_ERR_UNSUPPORTED, "self-play implements the C++ MCTSBot policy only");
+  if (G < 0 || max_len < 0) return Fail(OS_ERR_INVALID, "negative size");
+  if (G > 0 && (!bot_seeds || !eval_seeds || !start_offsets))
+    return Fail(OS_ERR_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->device));
+  e->params = *p;
+  e->params.layout = OS_LAYOUT_WAVE;
+  e->node_bytes = p->n_rollouts == 1 ? static_cast<int>(sizeof(Node<int32_t>))
+                                      : static_cast<int>(sizeof(Node<double>));
+  if ((rc = ArenaCap(e, p, &e->cap))) return rc;
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const size_t per_game = static_cast<size_t>(e->cap) * e->node_bytes;
+  const int64_t chunk = static_cast<int64_t>(free_b * 0.6 / std::max<size_t>(per_game, 1));
+  if (chunk < 1) return Fail(OS_ERR_CAPACITY, "not enough device memory for one game");
+  e->chunk_roots = std::max<int64_t>(1, std::min<int64_t>(chunk, std::max<int64_t>(G, 1)));
+  const GameCfg& cfg = e->game.cfg;
+  const int sb = e->game.state_bytes;
+  const bool go = cfg.kind == kGo;
+  e->hash_stride = go ? cfg.max_game_length + 2 : 1;
+  const size_t Gz = static_cast<size_t>(std::max<int64_t>(G, 1));
+  std::vector<unsigned char> starts(Gz * sb);
+  std::vector<uint64_t> hist(go ? Gz * e->hash_stride : 1, 0);
+  std::vector<int32_t> histn(Gz, 0);
+  for (int64_t r = 0; r < G; ++r) {
+    HostState hs;
+    std::string err;
+    if (!ReplayRoot(e->game, start_actions + start_offsets[r],
+                    start_offsets[r + 1] - start_offsets[r], &hs, &err))
+      return Fail(OS_ERR_INVALID, "game " + std::to_string(r) + ": " + err);
+    std::memcpy(starts.data() + r * sb, hs.raw, sb);
+    if (go) {
+      const int64_t nh = static_cast<int64_t>(hs.hashes.size());
+      if (nh > e->hash_stride) return Fail(OS_ERR_CAPACITY, "go hash history too long");
+      std::memcpy(hist.data() + r * e->hash_stride, hs.hashes.data(), nh * 8);
+      histn[r] = static_cast<int32_t>(nh);
+    }
+  }
+  if ((rc = e->d_roots.ensure(Gz * sb)) || (rc = e->d_bseed.ensure(Gz * 8)) ||
+      (rc = e->d_eseed.ensure(Gz * 4)) || (rc = e->d_rhash.ensure(hist.size() * 8)) ||
+      (rc = e->d_rnh.ensure(Gz * 4)))
+    return rc;
+  HIP_TRY(hipMemcpy(e->d_roots.p, starts.data(), Gz * sb, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_rhash.p, hist.data(), hist.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_rnh.p, histn.data(), Gz * 4, hipMemcpyHostToDevice));
+  if (G > 0) {
+    HIP_TRY(hipMemcpy(e->d_bseed.p, bot_seeds, G * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_eseed.p, eval_seeds, G * 4, hipMemcpyHostToDevice));
+  }
+  if (go) {
+    if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
+    HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
+                      hipMemcpyHostToDevice));
+  }
+  std::vector<double> lut(static_cast<size_t>(p->max_simulations) + 2);
+  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  if ((rc = e->d_lut.ensure(lut.size() * 8))) return rc;
+  HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice));
+  const size_t L = static_cast<size_t>(std::max(max_len, 1));
+  const size_t A = static_cast<size_t>(cfg.num_actions);
+  if ((rc = e->d_arena.ensure(static_cast<size_t>(e->chunk_roots) * per_game)) ||
+      (rc = e->d_res.ensure(Gz * sizeof(SearchResult))) ||
+      (rc = e->d_sp_act.ensure(Gz * L * 4)) || (rc = e->d_sp_len.ensure(Gz * 4)) ||
+      (rc = e->d_sp_ret.ensure(Gz * 16)) ||
+      (with_visits && (rc = e->d_sp_vis.ensure(Gz * L * A * 4))))
+    return rc;
+  e->sp_games = G;
+  e->sp_max_len = max_len;
+  e->sp_visits = with_visits;
+  e->sp_ready = true;
+  e->num_roots = 0;       // the search buffers now hold no prepared batch
+  e->roll_ready = false;
+  return OS_OK;
+}
+
+template <class G, class R>
+int SpLaunch(os_engine* e, hipStream_t stream) {
+  SpArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.sp.uct_c = e->params.uct_c;
+  a.sp.max_simulations = e->params.max_simulations;
+  a.sp.n_rollouts = e->params.n_rollouts;
+  a.sp.solve = e->params.solve;
+  a.sp.max_nodes = static_cast<int32_t>((e->params.max_memory_mb << 20) / 80 + 1);
+  a.sp.policy = kPolicyCpp;
+  a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
+  a.starts = e->d_roots.p;
+  a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.eval_seeds = static_cast<const uint32_t*>(e->d_eseed.p);
+  a.arena = e->d_arena.p;
+  a.cap = e->cap;
+  a.path_cap = e->game.cfg.max_game_length + 2;
+  a.max_len = e->sp_max_len;
+  a.num_actions = e->game.cfg.num_actions;
+  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+  a.hist = static_cast<uint64_t*>(e->d_rhash.p);
+  a.hist_n = static_cast<int32_t*>(e->d_rnh.p);
+  a.hash_stride = e->hash_stride;
+  a.actions = static_cast<int32_t*>(e->d_sp_act.p);
+  a.length = static_cast<int32_t*>(e->d_sp_len.p);
+  a.returns = static_cast<double*>(e->d_sp_ret.p);
+  a.visits = e->sp_visits ? static_cast<int32_t*>(e->d_sp_vis.p) : nullptr;
+  a.results = static_cast<SearchResult*>(e->d_res.p);
+  const size_t lds = SelfPlayLdsBytes<G, R>(a.path_cap);
+  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "self-play LDS slice exceeds the CU's LDS");
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay<G, R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)));
+  for (int64_t base = 0; base < e->sp_games; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->sp_games - base);
+    a.game_base = base;
+    a.num_games = n;
+    hipLaunchKernelGGL((k_wselfplay<G, R>), dim3(static_cast<unsigned>(n)), dim3(64), lds,
+                       stream, a);
+    HIP_TRY(hipGetLastError());
+  }
+  return OS_OK;
+}
+
+int SpRun(os_engine* e, hipStream_t stream) {
+  if (!e->sp_ready) return Fail(OS_ERR_INVALID, "os_selfplay_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  if (e->sp_games == 0) return OS_OK;
+  const bool dbl = e->params.n_rollouts != 1;
+  switch (e->game.cfg.kind) {
+#define OS_SP_CASE(K, G) \
+  case K: return dbl ? SpLaunch<G, double>(e, stream) : SpLaunch<G, int32_t>(e, stream);
+    OS_SP_CASE(kTicTacToe, TicTacToe)
+    OS_SP_CASE(kConnectFour, ConnectFour)
+    OS_SP_CASE(kBreakthrough, Breakthrough)
+    OS_SP_CASE(kHex, Hex)
+    OS_SP_CASE(kGo, Go)
+#undef OS_SP_CASE
+  }
+  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+}
+
+int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
+            int32_t* visits) {
+  if (!e->sp_ready) return Fail(OS_ERR_INVALID, "os_selfplay_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const int64_t G = e->sp_games;
+  if (G == 0) return OS_OK;
+  e->last_results.resize(G);
+  HIP_TRY(hipMemcpy(e->last_results.data(), e->d_res.p, G * sizeof(SearchResult),
+                    hipMemcpyDeviceToHost));
+  e->last_sims = 0;
+  for (int64_t r = 0; r < G; ++r) {
+    const SearchResult& s = e->last_results[r];
+    if (s.status != kOk) {
+      const char* why = s.status == kGameOverflow ? "game longer than max_len"
+                        : s.status == kArenaOverflow ? "node arena overflow (raise arena_nodes)"
+                        : s.status == kPathOverflow ? "tree path overflow"
+                                                    : "GC stack overflow";
+      return Fail(OS_ERR_CAPACITY, "game " + std::to_string(r) + ": " + why);
+    }
+    e->last_sims += s.sims;
+  }
+  const size_t L = static_cast<size_t>(e->sp_max_len);
+  if (actions) {
+    std::vector<int32_t> a32(G * L);
+    if (L) HIP_TRY(hipMemcpy(a32.data(), e->d_sp_act.p, a32.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < a32.size(); ++i) actions[i] = a32[i];
+  }
+  if (length) HIP_TRY(hipMemcpy(length, e->d_sp_len.p, G * 4, hipMemcpyDeviceToHost));
+  if (returns) HIP_TRY(hipMemcpy(returns, e->d_sp_ret.p, G * 16, hipMemcpyDeviceToHost));
+  if (visits) {
+    if (!e->sp_visits) return Fail(OS_ERR_INVALID, "prepared without visit recording");
+    HIP_TRY(hipMemcpy(visits, e->d_sp_vis.p, G * L * e->game.cfg.num_actions * 4,
+                      hipMemcpyDeviceToHost));
+  }
+  return OS_OK;
+}
+
 // Uploads one root + n evaluator seeds for the rollout kernels.
 int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
                 const uint32_t* seeds) {
@@ -900,6 +1273,7 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
   e->roll_nr = nr;
   e->roll_ready = true;
   e->num_roots = 0;  // the search buffers now hold no prepared batch
+  e->sp_ready = false;
   return OS_OK;
 }
 
@@ -1229,6 +1603,37 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
     }
   }
   return OS_OK;
+}
+
+int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games,
+                        const int64_t* start_actions, const int64_t* start_offsets,
+                        const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                        int32_t max_len, int32_t record_visits) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return SpPrepare(e, p, num_games, start_actions, start_offsets, bot_seeds, eval_seeds,
+                   max_len, record_visits != 0);
+}
+
+int os_selfplay_run_async(os_engine* e, void* hip_stream) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return SpRun(e, static_cast<hipStream_t>(hip_stream));
+}
+
+int os_selfplay_fetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
+                      int32_t* visits) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return SpFetch(e, actions, length, returns, visits);
+}
+
+int os_selfplay(os_engine* e, const os_mcts_params* p, int64_t num_games,
+                const int64_t* start_actions, const int64_t* start_offsets,
+                const uint32_t* bot_seeds, const uint32_t* eval_seeds, int32_t max_len,
+                int64_t* actions, int32_t* length, double* returns, int32_t* visits) {
+  int rc = os_selfplay_prepare(e, p, num_games, start_actions, start_offsets, bot_seeds,
+                               eval_seeds, max_len, visits != nullptr);
+  if (rc) return rc;
+  if ((rc = SpRun(e, nullptr))) return rc;
+  return SpFetch(e, actions, length, returns, visits);
 }
 
 int os_rollouts_prepare(os_engine* e, const int64_t* root_actions, int64_t n_actions,

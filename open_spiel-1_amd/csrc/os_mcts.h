@@ -34,6 +34,7 @@ enum SearchStatus : int32_t {
   kArenaOverflow = 1,   // node arena capacity exceeded
   kPathOverflow = 2,    // tree depth exceeded kMaxPath
   kGcStackOverflow = 3, // no arena space left for the GC traversal stack
+  kGameOverflow = 4,    // self-play game longer than the trajectory buffer
 };
 
 template <class R>

@@ -184,6 +184,45 @@ class Engine:
     check(lib.os_engine_root_sums_async(self._h, int(num_actions), dev_visits_ptr,
                                         dev_rewards_ptr, stream))
 
+  # ---- self-play (two MCTSBots + one shared RandomRolloutEvaluator) ----
+  def selfplay_prepare(self, start_actions, start_offsets, bot_seeds, eval_seeds,
+                       max_len=None, record_visits=True, **params):
+    """Device self-play batch (os_selfplay_prepare).  bot_seeds: [G][2]."""
+    self._sp_params = make_params(**params)
+    offs = _lib.i64(start_offsets)
+    G = len(offs) - 1
+    bs = _lib.u32(np.asarray(bot_seeds, np.uint32).reshape(-1))
+    es = _lib.u32(eval_seeds)
+    assert len(bs) == 2 * G and len(es) == G
+    self._sp = (_lib.i64(start_actions), offs, bs, es)
+    self._sp_G = G
+    self._sp_len = int(max_len if max_len is not None else self.max_game_length)
+    self._sp_vis = bool(record_visits)
+    acts = self._sp[0]
+    check(lib.os_selfplay_prepare(self._h, ctypes.byref(self._sp_params), G, ptr(acts),
+                                  ptr(offs), ptr(bs), ptr(es), self._sp_len,
+                                  1 if record_visits else 0))
+
+  def selfplay_run_async(self, stream=None):
+    check(lib.os_selfplay_run_async(self._h, stream))
+
+  def selfplay_fetch(self):
+    G, L, A = self._sp_G, self._sp_len, self.num_distinct_actions
+    o = dict(actions=np.zeros((G, L), np.int64), length=np.zeros(G, np.int32),
+             returns=np.zeros((G, 2), np.float64),
+             visits=np.zeros((G, L, A), np.int32) if self._sp_vis else None)
+    check(lib.os_selfplay_fetch(self._h, ptr(o["actions"]), ptr(o["length"]),
+                                ptr(o["returns"]), ptr(o["visits"])))
+    return o
+
+  def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len=None,
+               record_visits=True, **params):
+    """Plays G games on the device; see include/os_mcts.h os_selfplay."""
+    self.selfplay_prepare(start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
+                          record_visits, **params)
+    self.selfplay_run_async()
+    return self.selfplay_fetch()
+
   # ---- device-resident pipeline (bench) ----
   def prepare(self, root_actions, root_offsets, bot_seeds, eval_seeds=None,
               **params):

@@ -291,4 +291,66 @@ double oref_time_mcts_batch(void* g, int64_t num_roots,
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// Self-play as examples/mcts_example.cc:77-136 PlayGame drives it (and
+// evaluate_bots.cc:21-60): two MCTSBots (seeds bot_seeds[2g], [2g+1]) sharing
+// ONE RandomRolloutEvaluator (eval_seeds[g]; mcts_example.cc:151-157), each
+// move = bots[CurrentPlayer]->Step = MCTSearch + BestChild (mcts.cc:219-226),
+// until terminal; MCTSBot's InformAction/Restart are no-ops (mcts.h:162-163).
+// Per game: actions[g*max_len ...], len[g], returns[2g..2g+1]; visits (may be
+// NULL) [g][max_len][num_actions] = action-indexed root child explore counts.
+int oref_selfplay(void* g, int64_t num_games, const int64_t* start_actions,
+                  const int64_t* start_offsets, double uct_c, int32_t max_simulations,
+                  int32_t n_rollouts, int64_t max_memory_mb, int32_t solve,
+                  const uint32_t* bot_seeds, const uint32_t* eval_seeds,
+                  int32_t max_len, int64_t* actions, int32_t* len, double* returns,
+                  int32_t* visits, int32_t threads) {
+  auto* og = static_cast<OGame*>(g);
+  const int A = og->game->NumDistinctActions();
+  if (threads < 1) threads = 1;
+  std::atomic<int> err{0};
+  auto work = [&](int t) {
+    for (int64_t r = t; r < num_games; r += threads) {
+      auto state = Replay(*og->game, start_actions + start_offsets[r],
+                          start_offsets[r + 1] - start_offsets[r]);
+      RandomRolloutEvaluator ev(n_rollouts, eval_seeds[r]);
+      MCTSBot b0(*og->game, &ev, uct_c, max_simulations, max_memory_mb, solve != 0,
+                 bot_seeds[2 * r]);
+      MCTSBot b1(*og->game, &ev, uct_c, max_simulations, max_memory_mb, solve != 0,
+                 bot_seeds[2 * r + 1]);
+      MCTSBot* bots[2] = {&b0, &b1};
+      int m = 0;
+      while (!state->IsTerminal()) {
+        if (m >= max_len) {
+          err = 1;
+          break;
+        }
+        SearchStats st;
+        auto root = bots[state->CurrentPlayer()]->MCTSearch(*state, &st);
+        const Action a = root->BestChild().action;
+        actions[r * max_len + m] = a;
+        if (visits) {
+          int32_t* v = visits + (r * max_len + m) * static_cast<int64_t>(A);
+          for (int i = 0; i < A; ++i) v[i] = 0;
+          for (const SearchNode& c : root->children) v[c.action] = c.explore_count;
+        }
+        state->ApplyAction(a);
+        ++m;
+      }
+      for (int k = m; k < max_len; ++k) actions[r * max_len + k] = -1;
+      len[r] = m;
+      std::vector<double> ret = state->Returns();
+      returns[2 * r] = ret[0];
+      returns[2 * r + 1] = ret[1];
+    }
+  };
+  if (threads == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) ts.emplace_back(work, t);
+    for (auto& t : ts) t.join();
+  }
+  return err.load() ? -1 : 0;
+}
+
 }  // extern "C"

@@ -64,6 +64,10 @@ def lib():
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
         _u32p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
+    L.oref_selfplay.argtypes = [
+        ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
+        ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
+        _u32p, ctypes.c_int32, _i64p, _i32p, _f64p, ctypes.c_void_p, ctypes.c_int32]
     _lib = L
   return _lib
 
@@ -159,6 +163,31 @@ class Game:
         np.ascontiguousarray(eval_seeds, dtype=np.uint32), threads,
         ctypes.byref(sims))
     return secs, sims.value
+
+  def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
+               uct_c=2.0, max_simulations=100, n_rollouts=1, max_memory_mb=1000,
+               solve=True, with_visits=True, threads=1):
+    """Games of two MCTSBots sharing one evaluator (mcts_example.cc PlayGame).
+
+    bot_seeds: [G][2]; eval_seeds: [G].  Returns dict(actions [G][max_len]
+    (-1 padded), length [G], returns [G][2], visits [G][max_len][A] or None).
+    """
+    G = len(start_offsets) - 1
+    A = self.num_distinct_actions
+    out = dict(actions=np.zeros((G, max_len), np.int64),
+               length=np.zeros(G, np.int32), returns=np.zeros((G, 2), np.float64),
+               visits=np.zeros((G, max_len, A), np.int32) if with_visits else None)
+    rc = lib().oref_selfplay(
+        self._h, G, np.ascontiguousarray(start_actions, dtype=np.int64),
+        np.ascontiguousarray(start_offsets, dtype=np.int64), uct_c, max_simulations,
+        n_rollouts, max_memory_mb, int(solve),
+        np.ascontiguousarray(bot_seeds, dtype=np.uint32).reshape(-1),
+        np.ascontiguousarray(eval_seeds, dtype=np.uint32), max_len, out["actions"],
+        out["length"], out["returns"],
+        out["visits"].ctypes.data if with_visits else None, threads)
+    if rc:
+      raise RuntimeError("oref_selfplay: game longer than max_len")
+    return out
 
 
 def mt19937(seed, n):

@@ -1,0 +1,114 @@
+"""Self-play driver: two MCTSBots sharing one
+RandomRolloutEvaluator play whole games (examples/mcts_example.cc PlayGame).
+
+CPU tests pin the oracle's self-play against the oracle's own single-search
+path (every move of a game == one MCTSearch from that position with the bot
+and evaluator streams advanced by all earlier moves) and against the game
+rules; GPU tests check the device driver bit-exact against the oracle:
+actions, lengths, returns and per-move action-indexed root visit counts.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+from os_amd import engine as E
+
+STARTS = {  # game -> list of start histories
+    "tic_tac_toe": [[], [4], [0, 4], []],
+    "connect_four": [[], [3, 3], [], [0, 1, 2]],
+    "breakthrough(rows=6,columns=6)": [[], []],
+    "hex(board_size=5)": [[], [12], []],
+    "go(board_size=5,komi=0.5)": [[], [12]],
+}
+SIMS = {"tic_tac_toe": 60, "connect_four": 48, "breakthrough(rows=6,columns=6)": 24,
+        "hex(board_size=5)": 32, "go(board_size=5,komi=0.5)": 24}
+
+
+def _batch(game):
+  hs = STARTS[game]
+  acts, offs = E.roots_from_histories(hs)
+  G = len(hs)
+  bot = np.arange(2 * G, dtype=np.uint32).reshape(G, 2) * 7 + 3
+  ev = np.arange(G, dtype=np.uint32) + 1000
+  return acts, offs, bot, ev
+
+
+@pytest.mark.parametrize("game", sorted(STARTS))
+def test_oracle_selfplay_games_are_legal_and_scored(game):
+  og = oracle_lib.Game(game)
+  acts, offs, bot, ev = _batch(game)
+  o = og.selfplay(acts, offs, bot, ev, og.max_game_length, max_simulations=SIMS[game])
+  for g in range(len(offs) - 1):
+    hist = list(acts[offs[g]:offs[g + 1]])
+    n = int(o["length"][g])
+    for m in range(n):
+      info = og.state_info(hist)
+      a = int(o["actions"][g, m])
+      assert a in info["legal_actions"]
+      v = o["visits"][g, m]
+      assert v[a] > 0 and (v >= 0).all()
+      assert set(np.nonzero(v)[0]) <= set(info["legal_actions"])
+      hist.append(a)
+    assert (o["actions"][g, n:] == -1).all()
+    info = og.state_info(hist)
+    assert info["is_terminal"]
+    assert list(o["returns"][g]) == list(info["returns"])
+
+
+def test_oracle_selfplay_first_move_is_one_search():
+  # Move 0 of a game == MCTSBot(seed b0) + evaluator(seed e) searching the start.
+  og = oracle_lib.Game("connect_four")
+  acts, offs, bot, ev = _batch("connect_four")
+  o = og.selfplay(acts, offs, bot, ev, 42, max_simulations=48)
+  ref = og.mcts_batch(acts, offs, bot[:, 0].copy(), ev, max_simulations=48,
+                      max_children=7)
+  for g in range(len(offs) - 1):
+    # player to move at the start picks bot 0 or 1
+    p = len(acts[offs[g]:offs[g + 1]]) % 2
+    if p == 0:
+      assert o["actions"][g, 0] == ref["best_action"][g]
+      v = np.zeros(7, np.int32)
+      for k in range(ref["nchild"][g]):
+        v[ref["child_action"][g, k]] = ref["child_n"][g, k]
+      np.testing.assert_array_equal(o["visits"][g, 0], v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("game", sorted(STARTS))
+def test_gpu_selfplay_matches_oracle(require_gpu, game):
+  og = oracle_lib.Game(game)
+  acts, offs, bot, ev = _batch(game)
+  L = og.max_game_length
+  ref = og.selfplay(acts, offs, bot, ev, L, max_simulations=SIMS[game])
+  eng = E.Engine(game)
+  out = eng.selfplay(acts, offs, bot, ev, max_len=L, max_simulations=SIMS[game])
+  for k in ("actions", "length", "returns", "visits"):
+    np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_selfplay_many_games_no_visits(require_gpu):
+  game = "connect_four"
+  G = 96
+  acts, offs = E.make_roots(game, G, seed_base=77, max_plies=4)
+  bot = np.arange(2 * G, dtype=np.uint32).reshape(G, 2)
+  ev = np.arange(G, dtype=np.uint32) + 5
+  eng = E.Engine(game)
+  out = eng.selfplay(acts, offs, bot, ev, max_len=42, record_visits=False,
+                     max_simulations=32)
+  ref = oracle_lib.Game(game).selfplay(acts, offs, bot, ev, 42, max_simulations=32,
+                                       with_visits=False, threads=8)
+  for k in ("actions", "length", "returns"):
+    np.testing.assert_array_equal(out[k], ref[k], err_msg=k)
+  assert out["visits"] is None
+
+
+@pytest.mark.gpu
+def test_gpu_selfplay_errors(require_gpu):
+  from os_amd import _lib
+  eng = E.Engine("tic_tac_toe")
+  acts, offs = E.roots_from_histories([[]])
+  with pytest.raises(ValueError):
+    eng.selfplay(acts, offs, [[1, 2]], [3], policy=_lib.POLICY_NUMPY, max_simulations=10)
+  with pytest.raises(_lib.SpielError):
+    eng.selfplay(acts, offs, [[1, 2]], [3], max_len=2, max_simulations=10)
