@@ -41,6 +41,9 @@ CONFIGS = {
     "c3": ("search", "breakthrough(rows=8,columns=8)", 65536, 2048, 6),
     "c4": ("root_parallel", "hex(board_size=11)", 8192, 2048, 0),
     "c5": ("playouts", "go(board_size=9)", 1 << 20, 0, 0),
+    # SURVEY §8f rank 1 (not a BASELINE config): full self-play games, two
+    # MCTSBots + one shared evaluator per game, one wave per game.
+    "sp": ("selfplay", "connect_four", 4096, 256, 4),
 }
 KERNEL = {"wave": "k_wsearch", "lane": "k_mcts"}
 
@@ -123,7 +126,7 @@ def main():
   layouts = {"auto": _lib.LAYOUT_AUTO, "wave": _lib.LAYOUT_WAVE, "lane": _lib.LAYOUT_LANE}
   mode = CONFIGS[args.config][0]
   fn = {"search": bench_search, "root_parallel": bench_root_parallel,
-        "playouts": bench_playouts}[mode]
+        "playouts": bench_playouts, "selfplay": bench_selfplay}[mode]
   line = fn(args, ctx, layouts[args.layout])
   if ctx.rank == 0:
     print(json.dumps(line), flush=True)
@@ -353,6 +356,60 @@ def bench_playouts(args, ctx, layout):
   line["cpu_baseline"] = cpu
   line["parity"] = parity
   line["outcomes"] = {"p0_wins": int(c[0]), "p1_wins": int(c[1]), "draws": int(c[2])}
+  return line
+
+
+# ---------------------------------------------------------------------------
+# sp: self-play games
+def bench_selfplay(args, ctx, layout):
+  from os_amd import engine as E
+  _, game, G, sims, plies = CONFIGS[args.config]
+  G = args.roots or G
+  sims = args.sims or sims
+  base = ctx.rank * G
+  acts, offs = E.make_roots(game, G, seed_base=1000 + base, max_plies=plies)
+  gid = np.arange(base, base + G, dtype=np.uint32)
+  bot = np.stack([2 * gid, 2 * gid + 1], axis=1).astype(np.uint32)
+  ev = gid + np.uint32(EVAL_OFFSET)
+  eng = E.Engine(game, device=ctx.local)
+  L = eng.max_game_length
+  eng.selfplay_prepare(acts, offs, bot, ev, max_len=L, record_visits=True,
+                       max_simulations=sims, uct_c=2.0)
+  handle = ctx.stream.cuda_stream
+  for _ in range(args.warmup):
+    eng.selfplay_run_async(handle)
+  out = eng.selfplay_fetch()
+  moves = int(out["length"].sum())
+  sims_step = eng.last_sims()
+  parity = None
+  if ctx.rank == 0:
+    pg = min(args.parity_roots, 8, G)
+    ref = _oracle(game).selfplay(acts[:offs[pg]], offs[:pg + 1], bot[:pg], ev[:pg], L,
+                                 max_simulations=sims)
+    bad = [k for k in ("actions", "length", "returns", "visits")
+           if not np.array_equal(out[k][:pg], ref[k])]
+    parity = {"games_checked": pg, "bit_exact": not bad, "mismatch_fields": bad}
+  elapsed, kernel_ms = ctx.timed(lambda: eng.selfplay_run_async(handle), args.steps)
+  total_moves = ctx.total(moves * args.steps)
+  total_sims = ctx.total(sims_step * args.steps)
+  if ctx.rank != 0:
+    return None
+  line = _base_line(args, ctx, "self-play MCTS moves/sec on %s (%d sims per move)"
+                    % (game, sims), total_moves / elapsed, "moves/s", elapsed, {
+                        "workload": "%s, %d games per GPU, two MCTSBots + shared "
+                                    "RandomRolloutEvaluator per game, %d sims/move"
+                                    % (game, G, sims),
+                        "game": game, "games_per_gpu": G, "sims_per_move": sims,
+                        "parallelism": "dp%d (independent games)" % ctx.world,
+                        "layout": "wave", "moves_per_step_per_gpu": moves})
+  line["sims_per_s"] = total_sims / elapsed
+  line["kernel_ms_per_launch"] = kernel_ms
+  line["roofline"] = None
+  line["cpu_baseline"] = None
+  line["parity"] = parity
+  line["outcomes"] = {"p0_wins": int((out["returns"][:, 0] > 0).sum()),
+                      "p1_wins": int((out["returns"][:, 0] < 0).sum()),
+                      "draws": int((out["returns"][:, 0] == 0).sum())}
   return line
 
 
