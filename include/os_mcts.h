@@ -82,6 +82,16 @@ int32_t os_state_history(const os_state* s, int64_t* out, int32_t cap);
 int64_t os_state_to_string(const os_state* s, char* buf, int64_t cap);
 int64_t os_state_action_to_string(const os_state* s, int32_t player,
                                   int64_t action, char* buf, int64_t cap);
+/* ObservationTensorShape (spiel.h Game::ObservationTensorShape; per game:
+ * tic_tac_toe [3,3,3], connect_four [3,6,7], breakthrough [3,R,C], hex
+ * [9,n,n], go [4,n,n]; all CHW): writes shape3 (may be NULL), returns C*H*W. */
+int64_t os_game_observation_shape(const os_game* game, int32_t* shape3);
+/* State::ObservationTensor(player) (connect_four.cc:211-221,
+ * tic_tac_toe.cc:165-175, breakthrough.cc:326-340, hex.cc:266-277,
+ * go.cc:102-122) as float32 [C][H][W].  Returns the size; writes only when
+ * cap >= size. */
+int64_t os_state_observation_tensor(const os_state* s, int32_t player, float* out,
+                                    int64_t cap);
 
 /* ---- Engine: replaces algorithms::MCTSBot / RandomRolloutEvaluator --------
  * mcts.h:152-159 MCTSBot(game, evaluator, uct_c, max_simulations,
@@ -166,24 +176,32 @@ int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
  * and the evaluator's rng (eval_seeds[g]) persisting across moves;
  * MCTSBot::InformAction / Restart are no-ops (mcts.h:162-163).  Game g starts
  * from history start_actions[start_offsets[g] .. start_offsets[g+1]).
- * Outputs: actions[g][max_len] (-1 padded), length[g], returns[g][2], and, if
- * visits != NULL (record_visits != 0 at prepare), visits[g][move][A] = the
- * root children's explore_count indexed by action (A = NumDistinctActions),
- * i.e. the MCTS policy targets of the trajectory.  C++ policy only
- * (OS_POLICY_NUMPY -> OS_ERR_UNSUPPORTED).  A game longer than max_len fails
- * with OS_ERR_CAPACITY. */
+ * Outputs: actions[g][max_len] (-1 padded), length[g], returns[g][2]; if
+ * visits != NULL, visits[g][move][A] = the root children's explore_count
+ * indexed by action (A = NumDistinctActions), i.e. the MCTS policy targets;
+ * if observations != NULL, observations[g][move][C*H*W] = ObservationTensor
+ * of the position searched, for the player to move (os_state_observation_
+ * tensor layout) -- a trajectory buffer for training without a host replay
+ * (alpha_zero.cc:50-62).  Rows past the game end are
+ * zero.  C++ policy only (OS_POLICY_NUMPY -> OS_ERR_UNSUPPORTED).  A game
+ * longer than max_len fails with OS_ERR_CAPACITY. */
 int os_selfplay(os_engine* e, const os_mcts_params* p, int64_t num_games,
                 const int64_t* start_actions, const int64_t* start_offsets,
                 const uint32_t* bot_seeds, const uint32_t* eval_seeds, int32_t max_len,
-                int64_t* actions, int32_t* length, double* returns, int32_t* visits);
-/* The same as prepare / run (async, on hip_stream) / fetch (synchronising). */
+                int64_t* actions, int32_t* length, double* returns, int32_t* visits,
+                float* observations);
+/* The same as prepare / run (async, on hip_stream) / fetch (synchronising);
+ * `record` is a mask of OS_RECORD_* selecting the optional buffers, which
+ * fetch then requires (NULL skips the copy). */
+#define OS_RECORD_VISITS 1
+#define OS_RECORD_OBSERVATIONS 2
 int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games,
                         const int64_t* start_actions, const int64_t* start_offsets,
                         const uint32_t* bot_seeds, const uint32_t* eval_seeds,
-                        int32_t max_len, int32_t record_visits);
+                        int32_t max_len, int32_t record);
 int os_selfplay_run_async(os_engine* e, void* hip_stream);
 int os_selfplay_fetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
-                      int32_t* visits);
+                      int32_t* visits, float* observations);
 
 /* Device-resident rollout pipeline (go playouts/s): prepare
  * uploads the root and n evaluator seeds; run launches the rollout kernel on

@@ -334,6 +334,8 @@ struct SpArgs {
   int32_t* length;        // [total]
   double* returns;        // [total][2]
   int32_t* visits;        // [total][max_len][num_actions] or null
+  float* obs;             // [total][max_len][obs_size] or null
+  int32_t obs_size;       // C * H * W
   SearchResult* results;  // [total], summed over the game's searches
 };
 
@@ -449,6 +451,11 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
         v[c.action] = c.n;
       }
     }
+    if (a.obs) {  // ObservationTensor(player to move) of the position searched
+      float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
+      const int cells = a.cfg.rows * a.cfg.cols;
+      for (int i = l; i < a.obs_size; i += 64) o[i] = G::obs(s, a.cfg, p, i / cells, i % cells);
+    }
     if (l == 0) a.actions[gg * a.max_len + m] = act;
     ctx.reset();
     G::apply(s, a.cfg, ctx, act);
@@ -462,6 +469,11 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
     int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
     const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.num_actions;
     for (int64_t i = l; i < nz; i += 64) v[i] = 0;
+  }
+  if (a.obs) {
+    float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
+    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.obs_size;
+    for (int64_t i = l; i < nz; i += 64) o[i] = 0.0f;
   }
   if (l == 0) {
     const int r0 = G::terminal(s, a.cfg) ? G::ret0(s, a.cfg, ctx) : 0;
@@ -696,10 +708,12 @@ struct os_engine {
   int64_t sp_games = 0;
   int32_t sp_max_len = 0;
   bool sp_visits = false;
+  bool sp_obs = false;
   bool sp_ready = false;
   DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
-      d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis;
+      d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
+      d_sp_obs;
   std::vector<SearchResult> last_results;
   int64_t last_sims = 0;
   ~os_engine() {
@@ -707,7 +721,7 @@ struct os_engine {
                      &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
-                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis};
+                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs};
     (void)hipSetDevice(device);
     for (DevBuf* b : all) b->release();
   }
@@ -1068,7 +1082,9 @@ int ArenaCap(const os_engine* e, const os_mcts_params* p, uint32_t* cap_out) {
 // and sizes one tree arena per game (reused by every move's search).
 int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* start_actions,
               const int64_t* start_offsets, const uint32_t* bot_seeds,
-              const uint32_t* eval_seeds, int32_t max_len, bool with_visits) {
+              const uint32_t* eval_seeds, int32_t max_len, int32_t record) {
+  const bool with_visits = (record & OS_RECORD_VISITS) != 0;
+  const bool with_obs = (record & OS_RECORD_OBSERVATIONS) != 0;
   int rc = CheckParams(e, p);
   if (rc) return rc;
   if (p->policy != OS_POLICY_CPP)
@@ -1136,11 +1152,13 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
       (rc = e->d_res.ensure(Gz * sizeof(SearchResult))) ||
       (rc = e->d_sp_act.ensure(Gz * L * 4)) || (rc = e->d_sp_len.ensure(Gz * 4)) ||
       (rc = e->d_sp_ret.ensure(Gz * 16)) ||
-      (with_visits && (rc = e->d_sp_vis.ensure(Gz * L * A * 4))))
+      (with_visits && (rc = e->d_sp_vis.ensure(Gz * L * A * 4))) ||
+      (with_obs && (rc = e->d_sp_obs.ensure(Gz * L * ObservationShape(e->game, nullptr) * 4))))
     return rc;
   e->sp_games = G;
   e->sp_max_len = max_len;
   e->sp_visits = with_visits;
+  e->sp_obs = with_obs;
   e->sp_ready = true;
   e->num_roots = 0;       // the search buffers now hold no prepared batch
   e->roll_ready = false;
@@ -1175,6 +1193,8 @@ int SpLaunch(os_engine* e, hipStream_t stream) {
   a.length = static_cast<int32_t*>(e->d_sp_len.p);
   a.returns = static_cast<double*>(e->d_sp_ret.p);
   a.visits = e->sp_visits ? static_cast<int32_t*>(e->d_sp_vis.p) : nullptr;
+  a.obs = e->sp_obs ? static_cast<float*>(e->d_sp_obs.p) : nullptr;
+  a.obs_size = ObservationShape(e->game, nullptr);
   a.results = static_cast<SearchResult*>(e->d_res.p);
   const size_t lds = SelfPlayLdsBytes<G, R>(a.path_cap);
   if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "self-play LDS slice exceeds the CU's LDS");
@@ -1211,7 +1231,7 @@ int SpRun(os_engine* e, hipStream_t stream) {
 }
 
 int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
-            int32_t* visits) {
+            int32_t* visits, float* observations) {
   if (!e->sp_ready) return Fail(OS_ERR_INVALID, "os_selfplay_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipDeviceSynchronize());
@@ -1244,6 +1264,11 @@ int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
     if (!e->sp_visits) return Fail(OS_ERR_INVALID, "prepared without visit recording");
     HIP_TRY(hipMemcpy(visits, e->d_sp_vis.p, G * L * e->game.cfg.num_actions * 4,
                       hipMemcpyDeviceToHost));
+  }
+  if (observations) {
+    if (!e->sp_obs) return Fail(OS_ERR_INVALID, "prepared without observation recording");
+    HIP_TRY(hipMemcpy(observations, e->d_sp_obs.p,
+                      G * L * ObservationShape(e->game, nullptr) * 4, hipMemcpyDeviceToHost));
   }
   return OS_OK;
 }
@@ -1421,6 +1446,18 @@ int32_t os_state_is_terminal(const os_state* s) { return StateTerminal(s->s) ? 1
 int os_state_returns(const os_state* s, double* out2) {
   StateReturns(s->s, out2);
   return OS_OK;
+}
+int64_t os_game_observation_shape(const os_game* game, int32_t* shape3) {
+  if (!game) return Fail(OS_ERR_INVALID, "null game");
+  return ObservationShape(game->g, shape3);
+}
+int64_t os_state_observation_tensor(const os_state* s, int32_t player, float* out,
+                                    int64_t cap) {
+  if (!s) return Fail(OS_ERR_INVALID, "null state");
+  if (player < 0 || player > 1) return Fail(OS_ERR_INVALID, "player must be 0 or 1");
+  const int64_t n = ObservationShape(*s->s.game, nullptr);
+  if (out && cap >= n) StateObservation(s->s, player, out);
+  return n;
 }
 int32_t os_state_legal_actions(const os_state* s, int64_t* out, int32_t cap) {
   std::vector<int64_t> v;
@@ -1608,10 +1645,10 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
 int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games,
                         const int64_t* start_actions, const int64_t* start_offsets,
                         const uint32_t* bot_seeds, const uint32_t* eval_seeds,
-                        int32_t max_len, int32_t record_visits) {
+                        int32_t max_len, int32_t record) {
   if (!e) return Fail(OS_ERR_INVALID, "null engine");
   return SpPrepare(e, p, num_games, start_actions, start_offsets, bot_seeds, eval_seeds,
-                   max_len, record_visits != 0);
+                   max_len, record);
 }
 
 int os_selfplay_run_async(os_engine* e, void* hip_stream) {
@@ -1620,20 +1657,23 @@ int os_selfplay_run_async(os_engine* e, void* hip_stream) {
 }
 
 int os_selfplay_fetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
-                      int32_t* visits) {
+                      int32_t* visits, float* observations) {
   if (!e) return Fail(OS_ERR_INVALID, "null engine");
-  return SpFetch(e, actions, length, returns, visits);
+  return SpFetch(e, actions, length, returns, visits, observations);
 }
 
 int os_selfplay(os_engine* e, const os_mcts_params* p, int64_t num_games,
                 const int64_t* start_actions, const int64_t* start_offsets,
                 const uint32_t* bot_seeds, const uint32_t* eval_seeds, int32_t max_len,
-                int64_t* actions, int32_t* length, double* returns, int32_t* visits) {
+                int64_t* actions, int32_t* length, double* returns, int32_t* visits,
+                float* observations) {
+  const int32_t record = (visits ? OS_RECORD_VISITS : 0) |
+                         (observations ? OS_RECORD_OBSERVATIONS : 0);
   int rc = os_selfplay_prepare(e, p, num_games, start_actions, start_offsets, bot_seeds,
-                               eval_seeds, max_len, visits != nullptr);
+                               eval_seeds, max_len, record);
   if (rc) return rc;
   if ((rc = SpRun(e, nullptr))) return rc;
-  return SpFetch(e, actions, length, returns, visits);
+  return SpFetch(e, actions, length, returns, visits, observations);
 }
 
 int os_rollouts_prepare(os_engine* e, const int64_t* root_actions, int64_t n_actions,

@@ -102,6 +102,13 @@ struct TicTacToe {
   OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) {
     return s.winner == 0 ? 1 : (s.winner == 1 ? -1 : 0);
   }
+  // ObservationTensor (tic_tac_toe.cc:165-175): [3][3][3], plane = CellState
+  // {empty, nought (player 1), cross (player 0)}; not player-relative.
+  static constexpr int kObsPlanes = 3;
+  OS_HD static float obs(const State& s, const GameCfg&, int, int plane, int cell) {
+    const int want = (s.b[0] >> cell) & 1 ? 2 : ((s.b[1] >> cell) & 1 ? 1 : 0);
+    return plane == want ? 1.0f : 0.0f;
+  }
 };
 
 // ----------------------------------------------------------------------------
@@ -169,6 +176,17 @@ struct ConnectFour {
   }
   OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) {
     return s.outcome == 0 ? 1 : (s.outcome == 1 ? -1 : 0);
+  }
+  // ObservationTensor(player) (connect_four.cc:211-221): [3][6][7], tensor
+  // cell = row * 7 + col with row 0 at the bottom; PlayerRelative (:198-209)
+  // puts the OPPONENT's stones in plane 0, the player's own in plane 1, empty
+  // cells in plane 2.
+  static constexpr int kObsPlanes = 3;
+  OS_HD static float obs(const State& s, const GameCfg&, int player, int plane, int cell) {
+    const int bit = (cell % 7) * 7 + cell / 7;
+    const int q = (s.bb[0] >> bit) & 1 ? 0 : ((s.bb[1] >> bit) & 1 ? 1 : -1);
+    const int want = q < 0 ? 2 : (q == player ? 1 : 0);
+    return plane == want ? 1.0f : 0.0f;
   }
 };
 
@@ -280,6 +298,13 @@ struct Breakthrough {
     if (s.winner == 1 || s.pc[0] == 0) return -1;
     return 0;
   }
+  // ObservationTensor (breakthrough.cc:326-340, planes :284-300):
+  // [3][rows][cols], {black, white, empty}; not player-relative.
+  static constexpr int kObsPlanes = 3;
+  OS_HD static float obs(const State& s, const GameCfg&, int, int plane, int cell) {
+    const int want = (s.pc[0] >> cell) & 1 ? 0 : ((s.pc[1] >> cell) & 1 ? 1 : 2);
+    return plane == want ? 1.0f : 0.0f;
+  }
 };
 
 // ----------------------------------------------------------------------------
@@ -368,6 +393,22 @@ struct Hex {
     s.moves++;
   }
   OS_HD static int ret0(const State& s, const GameCfg&, Ctx&) { return s.result; }
+  // ObservationTensor (hex.cc:266-277): [9][n][n], plane = CellState + 4
+  // (hex.h:40-61): white win 0, west 1, east 2, plain 3, empty 4, black
+  // plain 5, south 6, north 7, win 8.  Edge A = north / west, B = south /
+  // east; the winning stone keeps its win label (no flood, hex.cc:149-156).
+  static constexpr int kObsPlanes = 9;
+  OS_HD static float obs(const State& s, const GameCfg&, int, int plane, int cell) {
+    int want = 4;
+    for (int p = 0; p < 2; ++p) {
+      if (!test(pick(s.st, p), cell)) continue;
+      const int sgn = p == 0 ? 1 : -1;
+      const int label = cell == s.win_cell ? 4 : (test(pick(s.ea, p), cell) ? 3
+                                                  : (test(pick(s.eb, p), cell) ? 2 : 1));
+      want = 4 + sgn * label;
+    }
+    return plane == want ? 1.0f : 0.0f;
+  }
 };
 
 // ----------------------------------------------------------------------------
@@ -629,6 +670,15 @@ struct Go {
     if (s.flags & kSuperko) return 0;
     const float sc = score(s, g);
     return sc > 0 ? 1 : (sc < 0 ? -1 : 0);
+  }
+  // ObservationTensor (go.cc:102-122): [4][n][n], planes black, white, empty
+  // (GoColor order) in BoardPoints order (== action order), then a constant
+  // plane = 1 when white is to play (komi bias); not player-relative.
+  static constexpr int kObsPlanes = 4;
+  OS_HD static float obs(const State& s, const GameCfg&, int, int plane, int cell) {
+    if (plane == 3) return s.to_play == 1 ? 1.0f : 0.0f;
+    const int want = test(s.bw[0], cell) ? 0 : (test(s.bw[1], cell) ? 1 : 2);
+    return plane == want ? 1.0f : 0.0f;
   }
 };
 

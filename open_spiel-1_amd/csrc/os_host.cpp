@@ -379,6 +379,45 @@ void StateReturns(const HostState& s, double* r) {
 }
 
 namespace {
+template <class G>
+int ObsPlanes() { return G::kObsPlanes; }
+template <class G>
+void ObsFill(const HostState& s, int player, float* out) {
+  const GameCfg& g = s.game->cfg;
+  const int cells = g.rows * g.cols;
+  for (int c = 0; c < G::kObsPlanes; ++c)
+    for (int i = 0; i < cells; ++i) out[c * cells + i] = G::obs(St<G>(s), g, player, c, i);
+}
+}  // namespace
+
+int ObservationShape(const HostGame& g, int32_t* shape3) {
+  int c = 0;
+  switch (g.cfg.kind) {
+    case kTicTacToe: c = ObsPlanes<TicTacToe>(); break;
+    case kConnectFour: c = ObsPlanes<ConnectFour>(); break;
+    case kBreakthrough: c = ObsPlanes<Breakthrough>(); break;
+    case kHex: c = ObsPlanes<Hex>(); break;
+    case kGo: c = ObsPlanes<Go>(); break;
+  }
+  if (shape3) {
+    shape3[0] = c;
+    shape3[1] = g.cfg.rows;
+    shape3[2] = g.cfg.cols;
+  }
+  return c * g.cfg.rows * g.cfg.cols;
+}
+
+void StateObservation(const HostState& s, int player, float* out) {
+  switch (s.game->cfg.kind) {
+    case kTicTacToe: ObsFill<TicTacToe>(s, player, out); break;
+    case kConnectFour: ObsFill<ConnectFour>(s, player, out); break;
+    case kBreakthrough: ObsFill<Breakthrough>(s, player, out); break;
+    case kHex: ObsFill<Hex>(s, player, out); break;
+    case kGo: ObsFill<Go>(s, player, out); break;
+  }
+}
+
+namespace {
 
 std::string TttString(const TicTacToe::State& s) {
   std::string out;

@@ -41,6 +41,10 @@ void StateLegal(const HostState& s, std::vector<int64_t>* out);
 // Returns false if the action is illegal.
 bool StateApply(HostState* s, int64_t a);
 void StateReturns(const HostState& s, double* r);
+// ObservationTensorShape: {C, H, W}; returns C * H * W.
+int ObservationShape(const HostGame& g, int32_t* shape3);
+// ObservationTensor(player) as float [C][H][W] (size ObservationShape).
+void StateObservation(const HostState& s, int player, float* out);
 std::string StateToString(const HostState& s);
 std::string StateActionToString(const HostState& s, int player, int64_t a);
 

@@ -107,6 +107,8 @@ _sig("os_state_legal_actions", _i32, [_vp, _P, _i32])
 _sig("os_state_history", _i32, [_vp, _P, _i32])
 _sig("os_state_to_string", _i64, [_vp, _cp, _i64])
 _sig("os_state_action_to_string", _i64, [_vp, _i32, _i64, _cp, _i64])
+_sig("os_game_observation_shape", _i64, [_vp, _P])
+_sig("os_state_observation_tensor", _i64, [_vp, _i32, _P, _i64])
 _sig("os_engine_create", ctypes.c_int, [_cp, _i32, ctypes.POINTER(_vp)])
 _sig("os_engine_destroy", ctypes.c_int, [_vp])
 _sig("os_mcts_batch", ctypes.c_int,
@@ -131,11 +133,13 @@ _sig("os_rollouts_fetch", ctypes.c_int, [_vp, _P])
 _sig("os_rollouts_outcomes_async", ctypes.c_int, [_vp, _vp, _vp])
 _sig("os_engine_root_sums_async", ctypes.c_int, [_vp, _i32, _vp, _vp, _vp])
 _sig("os_selfplay", ctypes.c_int,
-     [_vp, ctypes.POINTER(MctsParams), _i64, _P, _P, _P, _P, _i32, _P, _P, _P, _P])
+     [_vp, ctypes.POINTER(MctsParams), _i64, _P, _P, _P, _P, _i32, _P, _P, _P, _P, _P])
 _sig("os_selfplay_prepare", ctypes.c_int,
      [_vp, ctypes.POINTER(MctsParams), _i64, _P, _P, _P, _P, _i32, _i32])
 _sig("os_selfplay_run_async", ctypes.c_int, [_vp, _vp])
-_sig("os_selfplay_fetch", ctypes.c_int, [_vp, _P, _P, _P, _P])
+_sig("os_selfplay_fetch", ctypes.c_int, [_vp, _P, _P, _P, _P, _P])
+RECORD_VISITS = 1
+RECORD_OBSERVATIONS = 2
 _sig("os_engine_node_bytes", _i32, [_vp])
 _sig("os_engine_state_bytes", _i32, [_vp])
 _sig("os_make_roots", _i64, [_vp, _i64, _u32, _i32, _P, _P])

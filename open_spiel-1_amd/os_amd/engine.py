@@ -81,6 +81,12 @@ class Engine:
     self.num_distinct_actions = info.num_distinct_actions
     self.max_children = info.max_children
     self.max_game_length = info.max_game_length
+    shape = np.zeros(3, np.int32)
+    g2 = ctypes.c_void_p()
+    check(lib.os_game_load(game_string.encode(), ctypes.byref(g2)))
+    lib.os_game_observation_shape(g2, ptr(shape))
+    lib.os_game_free(g2)
+    self.observation_shape = [int(x) for x in shape]
 
   def close(self):
     if getattr(self, "_h", None) and self._h.value:
@@ -186,7 +192,8 @@ class Engine:
 
   # ---- self-play (two MCTSBots + one shared RandomRolloutEvaluator) ----
   def selfplay_prepare(self, start_actions, start_offsets, bot_seeds, eval_seeds,
-                       max_len=None, record_visits=True, **params):
+                       max_len=None, record_visits=True, record_observations=False,
+                       **params):
     """Device self-play batch (os_selfplay_prepare).  bot_seeds: [G][2]."""
     self._sp_params = make_params(**params)
     offs = _lib.i64(start_offsets)
@@ -198,10 +205,12 @@ class Engine:
     self._sp_G = G
     self._sp_len = int(max_len if max_len is not None else self.max_game_length)
     self._sp_vis = bool(record_visits)
+    self._sp_obs = bool(record_observations)
     acts = self._sp[0]
+    record = ((_lib.RECORD_VISITS if record_visits else 0) |
+              (_lib.RECORD_OBSERVATIONS if record_observations else 0))
     check(lib.os_selfplay_prepare(self._h, ctypes.byref(self._sp_params), G, ptr(acts),
-                                  ptr(offs), ptr(bs), ptr(es), self._sp_len,
-                                  1 if record_visits else 0))
+                                  ptr(offs), ptr(bs), ptr(es), self._sp_len, record))
 
   def selfplay_run_async(self, stream=None):
     check(lib.os_selfplay_run_async(self._h, stream))
@@ -210,16 +219,19 @@ class Engine:
     G, L, A = self._sp_G, self._sp_len, self.num_distinct_actions
     o = dict(actions=np.zeros((G, L), np.int64), length=np.zeros(G, np.int32),
              returns=np.zeros((G, 2), np.float64),
-             visits=np.zeros((G, L, A), np.int32) if self._sp_vis else None)
+             visits=np.zeros((G, L, A), np.int32) if self._sp_vis else None,
+             observations=(np.zeros((G, L) + tuple(self.observation_shape), np.float32)
+                           if self._sp_obs else None))
     check(lib.os_selfplay_fetch(self._h, ptr(o["actions"]), ptr(o["length"]),
-                                ptr(o["returns"]), ptr(o["visits"])))
+                                ptr(o["returns"]), ptr(o["visits"]),
+                                ptr(o["observations"])))
     return o
 
   def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len=None,
-               record_visits=True, **params):
+               record_visits=True, record_observations=False, **params):
     """Plays G games on the device; see include/os_mcts.h os_selfplay."""
     self.selfplay_prepare(start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
-                          record_visits, **params)
+                          record_visits, record_observations, **params)
     self.selfplay_run_async()
     return self.selfplay_fetch()
 

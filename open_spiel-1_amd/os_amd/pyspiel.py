@@ -142,6 +142,17 @@ class Game:
   def max_game_length(self):
     return self._info.max_game_length
 
+  def observation_tensor_shape(self):
+    shape = np.zeros(3, np.int32)
+    lib.os_game_observation_shape(self._h, shape.ctypes.data)
+    return [int(x) for x in shape]
+
+  def observation_tensor_size(self):
+    return int(lib.os_game_observation_shape(self._h, None))
+
+  def observation_tensor_layout(self):
+    return TensorLayout.CHW
+
   def get_type(self):
     return _TYPES[self._info.kind]
 
@@ -294,6 +305,19 @@ class State:
 
   def observation_string(self, player=None):
     return str(self)
+
+  def observation_tensor(self, player=None):
+    """State.observation_tensor([player]) (pyspiel.cc:292-360): flat list of
+    floats in ObservationTensorShape (CHW) order."""
+    p = self.current_player() if player is None else int(player)
+    if p < 0:
+      p = 0  # terminal: the reference's default player argument is 0 there
+    n = self._game.observation_tensor_size()
+    out = np.zeros(n, np.float32)
+    rc = lib.os_state_observation_tensor(self._h, p, out.ctypes.data, n)
+    if rc < 0:
+      check(int(rc))
+    return [float(x) for x in out]
 
   def chance_outcomes(self):
     return []

@@ -104,6 +104,31 @@ def test_gpu_selfplay_many_games_no_visits(require_gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("game", ["connect_four", "hex(board_size=5)",
+                                  "go(board_size=5,komi=0.5)"])
+def test_gpu_selfplay_observations_match_host_state(require_gpu, game):
+  from os_amd import pyspiel
+  acts, offs, bot, ev = _batch(game)
+  eng = E.Engine(game)
+  out = eng.selfplay(acts, offs, bot, ev, record_observations=True,
+                     max_simulations=SIMS[game])
+  g = pyspiel.load_game(game)
+  obs = out["observations"]
+  assert obs.shape[2:] == tuple(g.observation_tensor_shape())
+  for gi in range(len(offs) - 1):
+    st = g.new_initial_state()
+    for a in acts[offs[gi]:offs[gi + 1]]:
+      st.apply_action(int(a))
+    n = int(out["length"][gi])
+    for m in range(n):
+      want = np.array(st.observation_tensor(st.current_player()), np.float32)
+      np.testing.assert_array_equal(obs[gi, m].reshape(-1), want)
+      st.apply_action(int(out["actions"][gi, m]))
+    assert st.is_terminal()
+    assert not obs[gi, n:].any()
+
+
+@pytest.mark.gpu
 def test_gpu_selfplay_errors(require_gpu):
   from os_amd import _lib
   eng = E.Engine("tic_tac_toe")

@@ -53,16 +53,39 @@ def _str_list(s):
   return json.loads(s.strip())
 
 
+_GLYPH = {"◯": 0, "◉": 1}  # ◯ = 0.0, ◉ = 1.0 (binary tensors only)
+
+
+def _tensor_rows(lines, i):
+  """Glyph rows of an ObservationTensor(p): block starting at lines[i]:
+  each row holds the C planes of one tensor row, separated by two spaces.
+  Returns ([C][H][W] nested lists, next index)."""
+  rows = []
+  while i < len(lines) and lines[i] and lines[i][0] in _GLYPH:
+    rows.append([[_GLYPH[ch] for ch in plane] for plane in lines[i].split("  ")])
+    i += 1
+  C = len(rows[0])
+  return [[row[c] for row in rows] for c in range(C)], i
+
+
 def parse(path):
   states = []
   cur = None
   header = {}
   with open(path) as f:
     lines = f.read().split("\n")
-  for line in lines:
+  i = 0
+  while i < len(lines):
+    line = lines[i]
+    i += 1
     if line.startswith("# State "):
       cur = {}
       states.append(cur)
+      continue
+    mt = re.match(r"^ObservationTensor\(([01])\):$", line)
+    if cur is not None and mt:
+      t, i = _tensor_rows(lines, i)
+      cur.setdefault("observation_tensor", [None, None])[int(mt.group(1))] = t
       continue
     m = re.match(r"^([A-Za-z]+)\(\) = (.*)$", line)
     if cur is None:
@@ -92,6 +115,7 @@ def parse(path):
       "max_utility": float(header["MaxUtility"]),
       "min_utility": float(header["MinUtility"]),
       "game_to_string": _unquote(header["ToString"]),
+      "observation_tensor_shape": _int_list(header["ObservationTensorShape"]),
   }
   return meta, states
 
