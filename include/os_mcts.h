@@ -167,6 +167,36 @@ int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
  * evaluator) or OS_LAYOUT_WAVE (one wave per evaluator, uniform game code). */
 int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
 
+/* ---- External evaluator / PUCT --------------------
+ * MCTSBot::MCTSearch (mcts.cc:325-428) whose Evaluator is outside the GPU
+ * kernel -- the AlphaZero actor boundary (VPNetEvaluator, vpevaluator.cc:70-98:
+ * Evaluate = {v, -v}, Prior = policy over LegalActions, both from (legal
+ * actions, ObservationTensor)).  Child selection is UCT (puct = 0,
+ * mcts.cc:89-100) or PUCT (puct = 1, mcts.cc:102-111).  Each of num_roots
+ * searches (bot rng seed bot_seeds[r]) advances, one os_az_step_async at a
+ * time, to its next evaluator request, written into CALLER-OWNED DEVICE
+ * buffers so the caller's network reads them in place:
+ *   dev_kind[r]          0 none (finished), 1 Prior, 2 Evaluate
+ *   dev_obs[r][C*H*W]    ObservationTensor(current player), f32
+ *   dev_legal[r][A]      legal-action mask (u8)
+ * and answered before the next step in
+ *   dev_prior[r][A]      f64 action-indexed priors (read for legal actions)
+ *   dev_value[r]         f64 player-0 value
+ * *dev_pending = number of requests written by the last step (0 = all done).
+ * os_az_fetch then returns the root statistics (os_mcts_batch layout).
+ * Supported: tic_tac_toe, connect_four, breakthrough, hex (go needs its
+ * superko history context: OS_ERR_UNSUPPORTED); C++ policy; no Dirichlet
+ * noise (mcts.cc:177-192, alpha = 0). */
+int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
+                  const int64_t* root_actions, const int64_t* root_offsets,
+                  const uint32_t* bot_seeds, int32_t* dev_kind, float* dev_obs,
+                  uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
+                  int32_t* dev_pending);
+int os_az_step_async(os_engine* e, void* hip_stream);
+int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32_t* child_n,
+                double* child_w, int8_t* child_out, int32_t* nchild, int32_t* root_n,
+                double* root_w, int8_t* root_out, int64_t* best_action, int32_t* nodes);
+
 /* ---- Self-play -----------------------------------
  * num_games independent games, each played on the device the way
  * examples/mcts_example.cc:77-136 PlayGame drives two MCTSBots sharing ONE

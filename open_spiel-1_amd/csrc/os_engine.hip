@@ -25,6 +25,7 @@
 #include "os_host.h"
 #include "os_mcts.h"
 #include "os_wave.h"
+#include "os_az.h"
 
 using namespace osm;
 
@@ -484,6 +485,100 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// External-evaluator MCTS (os_az.h): one lane per search, one step per launch.
+struct AzArgs {
+  GameCfg cfg;
+  SearchParams sp;
+  int32_t puct;
+  int64_t num_roots;
+  const void* roots;        // [R] G::State
+  void* slots;              // [R] AzSlot<G>
+  Node<double>* arena;      // [R][cap]
+  double* priors;           // [R][cap]
+  uint32_t cap;
+  uint32_t* mt;             // [R][624] bot rng
+  const uint32_t* bot_seeds;
+  int32_t obs_size;
+  int32_t num_actions;
+  int32_t* kind;            // [R]
+  float* obs;               // [R][obs_size]
+  uint8_t* legal;           // [R][A]
+  const double* prior_in;   // [R][A]
+  const double* value_in;   // [R]
+  int32_t* pending;         // requests written by this step
+  // outputs (same layout as the search kernels)
+  SearchResult* results;
+  int32_t max_children;
+  int32_t* child_action;
+  int32_t* child_n;
+  double* child_w;
+  int8_t* child_out;
+  int32_t* nchild;
+  int32_t* root_n;
+  double* root_w;
+  int8_t* root_out;
+  int64_t* best_action;
+};
+
+template <class G>
+__global__ void k_az_step(AzArgs a) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= a.num_roots) return;
+  AzSlot<G>& sl = static_cast<AzSlot<G>*>(a.slots)[r];
+  const int stage0 = sl.stage;
+  if (stage0 == kAzDone) {
+    a.kind[r] = kAzNone;
+    return;
+  }
+  uint32_t* mt = a.mt + r * kMtN;
+  if (stage0 == kAzStart) {
+    mt_seed(mt, a.bot_seeds[r]);
+    sl.mt_idx = kMtN;
+    sl.mt_pre = 0;
+    sl.depth = 0;
+    sl.s = static_cast<const typename G::State*>(a.roots)[r];
+  }
+  MtStream bot{mt, sl.mt_idx, sl.mt_pre, 0};
+  const typename G::State root = static_cast<const typename G::State*>(a.roots)[r];
+  Node<double>* nodes = a.arena + r * static_cast<int64_t>(a.cap);
+  AzIo io;
+  io.kind = a.kind + r;
+  io.obs = a.obs + r * a.obs_size;
+  io.legal = a.legal + r * a.num_actions;
+  io.prior = a.prior_in + r * a.num_actions;
+  io.value = a.value_in + r;
+  az_step<G>(a.cfg, a.sp, a.puct, root, sl, nodes, a.priors + r * static_cast<int64_t>(a.cap),
+             a.cap, bot, io, a.obs_size, a.num_actions);
+  sl.mt_idx = bot.idx;
+  sl.mt_pre = bot.pre;
+  if (*io.kind != kAzNone) {
+    atomicAdd(a.pending, 1);
+    return;
+  }
+  // Finished in this step: publish the root's children like the search kernels.
+  const int P0 = G::to_move(root);
+  const Node<double> rn = nodes[0];
+  const int nc = rn.nchild;
+  const int64_t ob = r * a.max_children;
+  for (int k = 0; k < nc && k < a.max_children; ++k) {
+    const Node<double> c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = c.w;
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  a.results[r] = sl.res;
+  a.nchild[r] = nc;
+  a.root_n[r] = rn.n;
+  a.root_w[r] = rn.w;
+  a.root_out[r] = rn.out == kUnsolved ? kUnsolved
+                                      : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+  const int b = best_child(nodes, P0);
+  a.best_action[r] = b < 0 ? -1 : nodes[rn.first + b].action;
+}
+
 struct RollArgs {
   GameCfg cfg;
   int64_t n;
@@ -710,6 +805,16 @@ struct os_engine {
   bool sp_visits = false;
   bool sp_obs = false;
   bool sp_ready = false;
+  // prepared external-evaluator batch (os_az_*): caller-owned device buffers
+  bool az_ready = false;
+  int32_t az_puct = 0;
+  int32_t* az_kind = nullptr;
+  float* az_obs = nullptr;
+  uint8_t* az_legal = nullptr;
+  const double* az_prior = nullptr;
+  const double* az_value = nullptr;
+  int32_t* az_pending = nullptr;
+  DevBuf d_az_slots, d_az_prior;
   DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -721,7 +826,8 @@ struct os_engine {
                      &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
-                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs};
+                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
+                     &d_az_slots, &d_az_prior};
     (void)hipSetDevice(device);
     for (DevBuf* b : all) b->release();
   }
@@ -943,6 +1049,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   e->shared_stream = false;
   e->roll_ready = false;  // rollouts, searches and self-play share buffers
   e->sp_ready = false;
+  e->az_ready = false;
   return OS_OK;
 }
 
@@ -1162,6 +1269,7 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
   e->sp_ready = true;
   e->num_roots = 0;       // the search buffers now hold no prepared batch
   e->roll_ready = false;
+  e->az_ready = false;
   return OS_OK;
 }
 
@@ -1273,6 +1381,110 @@ int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
   return OS_OK;
 }
 
+// ---- external-evaluator search (os_az_*) ----
+template <class G>
+size_t AzSlotBytes() { return sizeof(AzSlot<G>); }
+
+int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
+              const int64_t* root_actions, const int64_t* root_offsets,
+              const uint32_t* bot_seeds, int32_t* kind, float* obs, uint8_t* legal,
+              const double* prior, const double* value, int32_t* pending) {
+  if (!p) return Fail(OS_ERR_INVALID, "null params");
+  if (e->game.cfg.kind == kGo)
+    return Fail(OS_ERR_UNSUPPORTED,
+                "external-evaluator search does not support go (superko history context)");
+  if (p->policy != OS_POLICY_CPP)
+    return Fail(OS_ERR_UNSUPPORTED, "external-evaluator search implements the C++ MCTSBot");
+  if (R > 0 && (!kind || !obs || !legal || !prior || !value || !pending || !bot_seeds))
+    return Fail(OS_ERR_INVALID, "null request / response buffer");
+  os_mcts_params q = *p;
+  q.n_rollouts = 2;  // f64 node rewards (Node<double>): values are not integral
+  q.layout = OS_LAYOUT_LANE;
+  int rc = Prepare(e, &q, R, root_actions, root_offsets, bot_seeds, bot_seeds);
+  if (rc) return rc;
+  if (e->chunk_roots < R)
+    return Fail(OS_ERR_CAPACITY, "external-evaluator searches must all fit in HBM at once");
+  size_t slot_bytes = 0;
+  switch (e->game.cfg.kind) {
+    case kTicTacToe: slot_bytes = AzSlotBytes<TicTacToe>(); break;
+    case kConnectFour: slot_bytes = AzSlotBytes<ConnectFour>(); break;
+    case kBreakthrough: slot_bytes = AzSlotBytes<Breakthrough>(); break;
+    case kHex: slot_bytes = AzSlotBytes<Hex>(); break;
+    default: return Fail(OS_ERR_UNSUPPORTED, "game");
+  }
+  const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
+  if ((rc = e->d_az_slots.ensure(Rz * slot_bytes)) ||
+      (rc = e->d_az_prior.ensure(Rz * static_cast<size_t>(e->cap) * 8)))
+    return rc;
+  HIP_TRY(hipMemset(e->d_az_slots.p, 0, Rz * slot_bytes));  // stage kAzStart
+  e->az_puct = puct ? 1 : 0;
+  e->az_kind = kind;
+  e->az_obs = obs;
+  e->az_legal = legal;
+  e->az_prior = prior;
+  e->az_value = value;
+  e->az_pending = pending;
+  e->az_ready = true;
+  return OS_OK;
+}
+
+template <class G>
+int AzLaunch(os_engine* e, hipStream_t stream) {
+  AzArgs a;
+  std::memset(&a, 0, sizeof a);
+  const DevArgs d = MakeArgs(e);
+  a.cfg = d.cfg;
+  a.sp = d.sp;
+  a.puct = e->az_puct;
+  a.num_roots = e->num_roots;
+  a.roots = d.roots;
+  a.slots = e->d_az_slots.p;
+  a.arena = static_cast<Node<double>*>(e->d_arena.p);
+  a.priors = static_cast<double*>(e->d_az_prior.p);
+  a.cap = e->cap;
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.bot_seeds = d.bot_seeds;
+  a.obs_size = ObservationShape(e->game, nullptr);
+  a.num_actions = e->game.cfg.num_actions;
+  a.kind = e->az_kind;
+  a.obs = e->az_obs;
+  a.legal = e->az_legal;
+  a.prior_in = e->az_prior;
+  a.value_in = e->az_value;
+  a.pending = e->az_pending;
+  a.results = d.results;
+  a.max_children = d.max_children;
+  a.child_action = d.child_action;
+  a.child_n = d.child_n;
+  a.child_w = d.child_w;
+  a.child_out = d.child_out;
+  a.nchild = d.nchild;
+  a.root_n = d.root_n;
+  a.root_w = d.root_w;
+  a.root_out = d.root_out;
+  a.best_action = d.best_action;
+  HIP_TRY(hipMemsetAsync(e->az_pending, 0, sizeof(int32_t), stream));
+  if (e->num_roots == 0) return OS_OK;
+  const int bs = 64;
+  hipLaunchKernelGGL(k_az_step<G>, dim3(static_cast<unsigned>((e->num_roots + bs - 1) / bs)),
+                     dim3(bs), 0, stream, a);
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
+}
+
+int AzStep(os_engine* e, hipStream_t stream) {
+  if (!e->az_ready) return Fail(OS_ERR_INVALID, "os_az_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  switch (e->game.cfg.kind) {
+    case kTicTacToe: return AzLaunch<TicTacToe>(e, stream);
+    case kConnectFour: return AzLaunch<ConnectFour>(e, stream);
+    case kBreakthrough: return AzLaunch<Breakthrough>(e, stream);
+    case kHex: return AzLaunch<Hex>(e, stream);
+    default: break;
+  }
+  return Fail(OS_ERR_UNSUPPORTED, "game");
+}
+
 // Uploads one root + n evaluator seeds for the rollout kernels.
 int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
                 const uint32_t* seeds) {
@@ -1299,6 +1511,7 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
   e->roll_ready = true;
   e->num_roots = 0;  // the search buffers now hold no prepared batch
   e->sp_ready = false;
+  e->az_ready = false;
   return OS_OK;
 }
 
@@ -1640,6 +1853,37 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
     }
   }
   return OS_OK;
+}
+
+int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
+                  const int64_t* root_actions, const int64_t* root_offsets,
+                  const uint32_t* bot_seeds, int32_t* dev_kind, float* dev_obs,
+                  uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
+                  int32_t* dev_pending) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, bot_seeds, dev_kind,
+                   dev_obs, dev_legal, dev_prior, dev_value, dev_pending);
+}
+
+int os_az_step_async(os_engine* e, void* hip_stream) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  return AzStep(e, static_cast<hipStream_t>(hip_stream));
+}
+
+int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32_t* child_n,
+                double* child_w, int8_t* child_out, int32_t* nchild, int32_t* root_n,
+                double* root_w, int8_t* root_out, int64_t* best_action, int32_t* nodes) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (!e->az_ready) return Fail(OS_ERR_INVALID, "os_az_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  int32_t pending = 0;
+  HIP_TRY(hipMemcpy(&pending, e->az_pending, 4, hipMemcpyDeviceToHost));
+  if (pending != 0)
+    return Fail(OS_ERR_INVALID, std::to_string(pending) +
+                                    " searches still wait for the evaluator: step again");
+  return Fetch(e, max_children, child_action, child_n, child_w, child_out, nchild, root_n,
+               root_w, root_out, best_action, nodes);
 }
 
 int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games,

@@ -291,6 +291,62 @@ double oref_time_mcts_batch(void* g, int64_t num_roots,
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// An external evaluator (the VPNetEvaluator role, vpevaluator.cc:70-80):
+// Prior / Evaluate delegate to a C callback that sees the state's history.
+// kind 1 = Prior: prior_out[a] for every legal a (action-indexed);
+// kind 2 = Evaluate: *value_out = player-0 value (returns {v, -v}).
+typedef int (*oref_eval_cb)(const int64_t* history, int64_t n, int32_t kind,
+                            double* prior_out, double* value_out);
+
+class CallbackEvaluator : public oref::Evaluator {
+ public:
+  CallbackEvaluator(oref_eval_cb cb, int num_actions) : cb_(cb), buf_(num_actions) {}
+  std::vector<double> Evaluate(const RState& state) override {
+    double v = 0;
+    const auto& h = state.History();
+    cb_(h.data(), static_cast<int64_t>(h.size()), 2, buf_.data(), &v);
+    return {v, -v};
+  }
+  std::vector<std::pair<Action, double>> Prior(const RState& state) override {
+    const auto& h = state.History();
+    double v = 0;
+    cb_(h.data(), static_cast<int64_t>(h.size()), 1, buf_.data(), &v);
+    std::vector<std::pair<Action, double>> out;
+    for (Action a : state.LegalActions()) out.emplace_back(a, buf_[a]);
+    return out;  // LegalActions order, as VPNetModel::Inference returns it
+  }
+
+ private:
+  oref_eval_cb cb_;
+  std::vector<double> buf_;
+};
+
+// MCTSBot::MCTSearch with an external evaluator and UCT (puct = 0) or PUCT
+// (puct = 1) child selection (mcts.cc:297-304), one bot seed per root; same
+// output layout as oref_mcts_batch.
+int oref_mcts_external(void* g, int64_t num_roots, const int64_t* root_actions,
+                       const int64_t* root_offsets, double uct_c, int32_t max_simulations,
+                       int64_t max_memory_mb, int32_t solve, int32_t puct,
+                       const uint32_t* bot_seeds, oref_eval_cb cb, int32_t max_children,
+                       int32_t* child_action, int32_t* child_n, double* child_w,
+                       int8_t* child_out, int32_t* nchild, int32_t* root_n, double* root_w,
+                       int8_t* root_out, int64_t* best_action, int32_t* nodes) {
+  auto* og = static_cast<OGame*>(g);
+  RootOut o{child_action, child_n, child_w, child_out, nchild,
+            root_n,       root_w,  root_out, best_action, nodes};
+  CallbackEvaluator ev(cb, og->game->NumDistinctActions());
+  for (int64_t r = 0; r < num_roots; ++r) {
+    auto state = Replay(*og->game, root_actions + root_offsets[r],
+                        root_offsets[r + 1] - root_offsets[r]);
+    MCTSBot bot(*og->game, &ev, uct_c, max_simulations, max_memory_mb, solve != 0,
+                bot_seeds[r], puct != 0);
+    SearchStats st;
+    auto root = bot.MCTSearch(*state, &st);
+    FillOut(*root, max_children, r, st, o);
+  }
+  return 0;
+}
+
 // Self-play as examples/mcts_example.cc:77-136 PlayGame drives it (and
 // evaluate_bots.cc:21-60): two MCTSBots (seeds bot_seeds[2g], [2g+1]) sharing
 // ONE RandomRolloutEvaluator (eval_seeds[g]; mcts_example.cc:151-157), each

@@ -21,12 +21,20 @@
 
 namespace oref {
 
+// mcts.h:78-87 Evaluator interface.
+class Evaluator {
+ public:
+  virtual ~Evaluator() {}
+  virtual std::vector<double> Evaluate(const RState& state) = 0;
+  virtual std::vector<std::pair<Action, double>> Prior(const RState& state) = 0;
+};
+
 // mcts.h:92-106 / mcts.cc:42-71
-class RandomRolloutEvaluator {
+class RandomRolloutEvaluator : public Evaluator {
  public:
   RandomRolloutEvaluator(int n_rollouts, uint32_t seed)
       : n_rollouts_(n_rollouts), rng_(seed) {}
-  std::vector<double> Evaluate(const RState& state) {
+  std::vector<double> Evaluate(const RState& state) override {
     std::vector<double> result;
     for (int i = 0; i < n_rollouts_; ++i) {
       std::unique_ptr<RState> ws = state.Clone();
@@ -45,7 +53,7 @@ class RandomRolloutEvaluator {
     return result;
   }
   // mcts.cc:73-86 (deterministic games only: no chance branch needed).
-  std::vector<std::pair<Action, double>> Prior(const RState& state) {
+  std::vector<std::pair<Action, double>> Prior(const RState& state) override {
     std::vector<Action> legal = state.LegalActions();
     std::vector<std::pair<Action, double>> prior;
     prior.reserve(legal.size());
@@ -80,6 +88,12 @@ struct SearchNode {
     return total_reward / explore_count +
            uct_c * std::sqrt(std::log(parent_explore_count) / explore_count);
   }
+  // mcts.cc:102-111
+  double PUCTValue(int parent_explore_count, double uct_c) const {
+    if (!outcome.empty()) return outcome[player];
+    return ((explore_count != 0 ? total_reward / explore_count : 0) +
+            uct_c * prior * std::sqrt(parent_explore_count) / (explore_count + 1));
+  }
   // mcts.cc:113-123
   bool CompareFinal(const SearchNode& b) const {
     double out = outcome.empty() ? 0 : outcome[player];
@@ -105,9 +119,11 @@ struct SearchStats {
 // mcts.cc:194-443, UCT policy, no Dirichlet noise (alpha = 0).
 class MCTSBot {
  public:
-  MCTSBot(const RGame& game, RandomRolloutEvaluator* evaluator, double uct_c,
-          int max_simulations, int64_t max_memory_mb, bool solve, uint32_t seed)
-      : uct_c_(uct_c),
+  MCTSBot(const RGame& game, Evaluator* evaluator, double uct_c,
+          int max_simulations, int64_t max_memory_mb, bool solve, uint32_t seed,
+          bool puct = false)
+      : puct_(puct),
+        uct_c_(uct_c),
         max_simulations_(max_simulations),
         max_nodes_(static_cast<int>((max_memory_mb << 20) / kNodeBytes + 1)),
         solve_(solve),
@@ -202,7 +218,8 @@ class MCTSBot {
       SearchNode* chosen = nullptr;
       double max_value = -std::numeric_limits<double>::infinity();
       for (SearchNode& child : cur->children) {
-        double val = child.UCTValue(cur->explore_count, uct_c_);
+        double val = puct_ ? child.PUCTValue(cur->explore_count, uct_c_)
+                           : child.UCTValue(cur->explore_count, uct_c_);
         if (val > max_value) {
           max_value = val;
           chosen = &child;
@@ -226,6 +243,7 @@ class MCTSBot {
     }
   }
 
+  bool puct_;
   double uct_c_;
   int max_simulations_;
   int max_nodes_;
@@ -234,7 +252,7 @@ class MCTSBot {
   bool solve_;
   double max_utility_;
   std::mt19937 rng_;
-  RandomRolloutEvaluator* evaluator_;
+  Evaluator* evaluator_;
 };
 
 // python/algorithms/mcts.py:199-443 with ONE numpy RandomState (MT19937,

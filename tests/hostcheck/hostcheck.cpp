@@ -2,12 +2,15 @@
 // game state machines compiled for the host CPU with g++, so the CPU test
 // suite can check the exact engine logic the gfx950 kernel runs against the
 // oracle without a GPU.  Never shipped, never used by bench.py or the C-ABI.
+#include <algorithm>
 #include <cmath>
+#include <memory>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "os_host.h"
+#include "os_az.h"
 #include "os_mcts.h"
 
 using namespace osm;
@@ -148,6 +151,120 @@ int hc_mcts_batch(const char* game_string, int64_t num_roots,
       HC_CASE(kGo, Go)
 #undef HC_CASE
     }
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// External-evaluator search (csrc/os_az.h) stepped on the host: every request
+// goes to `cb(obs, obs_size, legal, A, kind, prior_out, value_out)`.  Same
+// output layout as hc_mcts_batch.
+typedef int (*hc_az_cb)(const float* obs, int32_t obs_size, const uint8_t* legal,
+                        int32_t num_actions, int32_t kind, double* prior, double* value);
+}  // extern "C"
+
+namespace {
+template <class G>
+int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp, int puct,
+             uint32_t seed, uint32_t cap, hc_az_cb cb, int32_t mc, int32_t* ca, int32_t* cn,
+             double* cw, int8_t* co, int32_t* nch, int32_t* rn, double* rw, int8_t* ro,
+             int64_t* ba, int32_t* nd) {
+  const int A = game.cfg.num_actions;
+  const int obs_size = ObservationShape(game, nullptr);
+  std::vector<Node<double>> nodes(cap);
+  std::vector<double> prior(cap);
+  std::vector<uint32_t> mt(kMtN);
+  mt_seed(mt.data(), seed);
+  MtStream bot{mt.data(), kMtN, 0, 0};
+  std::vector<float> obs(obs_size);
+  std::vector<uint8_t> legal(A);
+  std::vector<double> pri(A);
+  double value = 0;
+  int32_t kind = 0;
+  AzIo io{&kind, obs.data(), legal.data(), pri.data(), &value};
+  auto sl = std::make_unique<AzSlot<G>>();
+  std::memset(sl.get(), 0, sizeof(AzSlot<G>));
+  const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
+  sl->s = rs;
+  for (;;) {
+    az_step<G>(game.cfg, sp, puct, rs, *sl, nodes.data(), prior.data(), cap, bot, io, obs_size,
+               A);
+    if (kind == kAzNone) break;
+    std::fill(pri.begin(), pri.end(), 0.0);
+    cb(obs.data(), obs_size, legal.data(), A, kind, pri.data(), &value);
+  }
+  if (sl->res.status != kOk) {
+    g_err = "search status " + std::to_string(sl->res.status);
+    return -4;
+  }
+  const int P0 = G::to_move(rs);
+  const Node<double>& r0 = nodes[0];
+  *nch = r0.nchild;
+  for (int k = 0; k < r0.nchild && k < mc; ++k) {
+    const Node<double>& c = nodes[r0.first + k];
+    ca[k] = c.action;
+    cn[k] = c.n;
+    cw[k] = c.w;
+    co[k] = c.out == kUnsolved ? kUnsolved : (P0 == 0 ? c.out : -c.out);
+  }
+  *rn = r0.n;
+  *rw = r0.w;
+  *ro = r0.out == kUnsolved ? kUnsolved : (P0 == 0 ? r0.out : -r0.out);
+  const int b = best_child(nodes.data(), P0);
+  *ba = b < 0 ? -1 : nodes[r0.first + b].action;
+  *nd = sl->res.nodes;
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int hc_az_batch(const char* game_string, int64_t num_roots, const int64_t* root_actions,
+                const int64_t* root_offsets, double uct_c, int32_t max_simulations,
+                int64_t max_memory_mb, int32_t solve, int32_t puct,
+                const uint32_t* bot_seeds, hc_az_cb cb, int32_t max_children,
+                int32_t* child_action, int32_t* child_n, double* child_w, int8_t* child_out,
+                int32_t* nchild, int32_t* root_n, double* root_w, int8_t* root_out,
+                int64_t* best_action, int32_t* nodes) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty()) {
+    g_err = err;
+    return -1;
+  }
+  std::vector<double> lut(max_simulations + 2);
+  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  SearchParams sp;
+  std::memset(&sp, 0, sizeof sp);
+  sp.uct_c = uct_c;
+  sp.max_simulations = max_simulations;
+  sp.n_rollouts = 1;
+  sp.solve = solve;
+  sp.max_nodes = static_cast<int32_t>((max_memory_mb << 20) / 80 + 1);
+  sp.policy = kPolicyCpp;
+  sp.log_lut = lut.data();
+  const uint32_t cap = 1 + static_cast<uint32_t>(max_simulations) * game.cfg.max_children +
+                       static_cast<uint32_t>(GcStackReserve(game.cfg.max_children));
+  for (int64_t r = 0; r < num_roots; ++r) {
+    HostState hs;
+    hs.game = &game;
+    StateInit(&hs);
+    for (int64_t i = root_offsets[r]; i < root_offsets[r + 1]; ++i) StateApply(&hs, root_actions[i]);
+    const int64_t o = r * max_children;
+    int rc = 0;
+#define HC_AZ(G)                                                                          \
+  rc = AzRunOne<G>(game, hs, sp, puct, bot_seeds[r], cap, cb, max_children,               \
+                   child_action + o, child_n + o, child_w + o, child_out + o, nchild + r, \
+                   root_n + r, root_w + r, root_out + r, best_action + r, nodes + r)
+    switch (game.cfg.kind) {
+      case kTicTacToe: HC_AZ(TicTacToe); break;
+      case kConnectFour: HC_AZ(ConnectFour); break;
+      case kBreakthrough: HC_AZ(Breakthrough); break;
+      case kHex: HC_AZ(Hex); break;
+      default: g_err = "unsupported"; return -2;
+    }
+#undef HC_AZ
     if (rc) return rc;
   }
   return 0;

@@ -110,3 +110,50 @@ def mt_roundtrip(key, pos, k):
   out = np.zeros(k, np.uint32)
   lib().hc_mt_roundtrip(key.ctypes.data, p.ctypes.data, k, out.ctypes.data)
   return out, key, int(p[0])
+
+
+# int cb(const float* obs, int32 obs_size, const uint8* legal, int32 A, int32 kind,
+#        double* prior, double* value)
+AZ_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int32,
+                         ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32, ctypes.c_int32,
+                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double))
+
+
+def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=True,
+             uct_c=2.0, max_simulations=100, max_memory_mb=1000, solve=True):
+  """csrc/os_az.h stepped on the host; eval_fn(obs float32[obs_size], legal
+  bool[A], kind) -> (prior [A], value)."""
+  L = lib()
+  vp = ctypes.c_void_p
+  L.hc_az_batch.argtypes = [ctypes.c_char_p, ctypes.c_int64, vp, vp, ctypes.c_double,
+                            ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                            vp, AZ_CB, ctypes.c_int32] + [vp] * 10
+  R = len(offs) - 1
+  mc = max_children
+  o = dict(child_action=np.zeros((R, mc), np.int32), child_n=np.zeros((R, mc), np.int32),
+           child_w=np.zeros((R, mc), np.float64), child_out=np.zeros((R, mc), np.int8),
+           nchild=np.zeros(R, np.int32), root_n=np.zeros(R, np.int32),
+           root_w=np.zeros(R, np.float64), root_out=np.zeros(R, np.int8),
+           best_action=np.zeros(R, np.int64), nodes=np.zeros(R, np.int32))
+  o["child_action"][:] = -1
+  o["child_out"][:] = 2
+
+  def cb(obs, obs_size, legal, A, kind, prior_out, value_out):
+    ob = np.ctypeslib.as_array(obs, shape=(obs_size,)).copy()
+    lg = np.ctypeslib.as_array(legal, shape=(A,)).astype(bool)
+    pr, v = eval_fn(ob, lg, int(kind))
+    for a in range(A):
+      prior_out[a] = float(pr[a])
+    value_out[0] = float(v)
+    return 0
+
+  fn = AZ_CB(cb)
+  acts = np.ascontiguousarray(acts, np.int64)
+  offs = np.ascontiguousarray(offs, np.int64)
+  bs = np.ascontiguousarray(bot_seeds, np.uint32)
+  rc = L.hc_az_batch(game_string.encode(), R, acts.ctypes.data, offs.ctypes.data, uct_c,
+                     max_simulations, max_memory_mb, int(solve), int(puct), bs.ctypes.data,
+                     fn, mc, *[o[k].ctypes.data for k in KEYS])
+  if rc:
+    raise RuntimeError(L.hc_last_error().decode())
+  return o

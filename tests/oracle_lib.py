@@ -21,6 +21,10 @@ _u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
 _u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
 _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
 _i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
+# int cb(const int64_t* history, int64_t n, int32_t kind, double* prior, double* value)
+EVAL_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64,
+                           ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
+                           ctypes.POINTER(ctypes.c_double))
 
 
 def build():
@@ -64,6 +68,10 @@ def lib():
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
         _u32p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
+    L.oref_mcts_external.argtypes = [
+        ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double, ctypes.c_int32,
+        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _u32p, EVAL_CB, ctypes.c_int32,
+        _i32p, _i32p, _f64p, _i8p, _i32p, _i32p, _f64p, _i8p, _i64p, _i32p]
     L.oref_selfplay.argtypes = [
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
@@ -163,6 +171,41 @@ class Game:
         np.ascontiguousarray(eval_seeds, dtype=np.uint32), threads,
         ctypes.byref(sims))
     return secs, sims.value
+
+  def mcts_external(self, root_actions, root_offsets, bot_seeds, eval_fn, puct=True,
+                    uct_c=2.0, max_simulations=100, max_memory_mb=1000, solve=True,
+                    max_children=None):
+    """MCTSBot with an external evaluator: eval_fn(history, kind) -> (prior
+    [A] action-indexed, value for player 0); kind 1 = Prior, 2 = Evaluate."""
+    R = len(root_offsets) - 1
+    mc = max_children or self.num_distinct_actions
+    A = self.num_distinct_actions
+    out = dict(
+        child_action=np.zeros((R, mc), np.int32), child_n=np.zeros((R, mc), np.int32),
+        child_w=np.zeros((R, mc), np.float64), child_out=np.zeros((R, mc), np.int8),
+        nchild=np.zeros(R, np.int32), root_n=np.zeros(R, np.int32),
+        root_w=np.zeros(R, np.float64), root_out=np.zeros(R, np.int8),
+        best_action=np.zeros(R, np.int64), nodes=np.zeros(R, np.int32))
+    out["child_action"][:] = -1
+    out["child_out"][:] = 2
+
+    def cb(hist, n, kind, prior_out, value_out):
+      h = [int(hist[i]) for i in range(n)]
+      pr, v = eval_fn(h, int(kind))
+      for a in range(A):
+        prior_out[a] = float(pr[a])
+      value_out[0] = float(v)
+      return 0
+
+    fn = EVAL_CB(cb)
+    lib().oref_mcts_external(
+        self._h, R, np.ascontiguousarray(root_actions, dtype=np.int64),
+        np.ascontiguousarray(root_offsets, dtype=np.int64), uct_c, max_simulations,
+        max_memory_mb, int(solve), int(puct),
+        np.ascontiguousarray(bot_seeds, dtype=np.uint32), fn, mc, out["child_action"],
+        out["child_n"], out["child_w"], out["child_out"], out["nchild"], out["root_n"],
+        out["root_w"], out["root_out"], out["best_action"], out["nodes"])
+    return out
 
   def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
                uct_c=2.0, max_simulations=100, n_rollouts=1, max_memory_mb=1000,
