@@ -139,6 +139,9 @@ struct ConnectFour {
       return ctz64(m);
     }
   };
+  // Four in a row in any direction (column, row, both diagonals).  Early-exit
+  // form: measured 3-7% faster in the wave kernel than a branch-free OR of
+  // the four tests (profiles/r01/ab_uniform.txt).
   OS_HD static bool has_four(uint64_t b) {
     uint64_t m = b & (b >> 1);
     if (m & (m >> 2)) return true;

@@ -421,6 +421,14 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   zero_node.first = 0; zero_node.n = 0; zero_node.w = 0; zero_node.action = 0;
   zero_node.nchild = 0; zero_node.out = kUnsolved;
   double root_logN = sp.log_lut[0];
+  // The root's children, register-resident across simulations (lane k holds
+  // child k, and k + 64 in the second slot), with log(n) of each; every write
+  // to a root child (expansion, leaf outcome, backup, solver, GC) is mirrored
+  // here, so the root scan issues no loads.  root_k = this simulation's
+  // root child (the depth-1 node of the path).
+  Node<R> rc0 = zero_node, rc1 = zero_node;
+  double rlg0 = 0.0, rlg1 = 0.0;
+  int root_k = 0;
 
   for (int sim = 0; sim < sp.max_simulations; ++sim) {
     uint64_t t_ph = OS_PH_NOW();
@@ -492,9 +500,29 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         if (depth == 0) {
           root_first = first;
           root_nc = nc;
-        } else if (l == 0) {
-          path[depth].first = first;
-          path[depth].nc = nc;
+          // Root children live in registers from now on (lane k <-> child k).
+          rc0 = zero_node;
+          rc1 = zero_node;
+          if (l < nc) rc0.action = static_cast<uint16_t>(acts.a0);
+          if (WW::kTwoSlots && l + 64 < nc) rc1.action = static_cast<uint16_t>(acts.a1);
+          rlg0 = rlg1 = sp.log_lut[0];
+          root_k = 0;
+        } else {
+          if (l == 0) {
+            path[depth].first = first;
+            path[depth].nc = nc;
+          }
+          if (depth == 1) {  // the expanded node is root child root_k
+            if (l == (root_k & 63)) {
+              if (root_k < 64) {
+                rc0.first = first;
+                rc0.nchild = static_cast<uint8_t>(nc);
+              } else {
+                rc1.first = first;
+                rc1.nchild = static_cast<uint8_t>(nc);
+              }
+            }
+          }
         }
         nodes_count += nc;
         res.expanded += nc;
@@ -515,17 +543,31 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         res.scanned += cur_nc;
         Node<R> c0 = zero_node, c1 = zero_node;
         double v0 = -inf, v1 = -inf, lg0 = 0.0, lg1 = 0.0;
-        if (l < cur_nc) {
-          c0 = nodes[cur_first + l];
-          lg0 = sp.log_lut[c0.n];
-          v0 = uct_value(c0, cp, cur_logN, sp.uct_c);
-        }
-        if (WW::kTwoSlots && l + 64 < cur_nc) {
-          c1 = nodes[cur_first + l + 64];
-          lg1 = sp.log_lut[c1.n];
-          v1 = uct_value(c1, cp, cur_logN, sp.uct_c);
+        if (depth == 0) {  // root children: register-resident, no loads
+          if (l < cur_nc) {
+            c0 = rc0;
+            lg0 = rlg0;
+            v0 = uct_value(c0, cp, cur_logN, sp.uct_c);
+          }
+          if (WW::kTwoSlots && l + 64 < cur_nc) {
+            c1 = rc1;
+            lg1 = rlg1;
+            v1 = uct_value(c1, cp, cur_logN, sp.uct_c);
+          }
+        } else {
+          if (l < cur_nc) {
+            c0 = nodes[cur_first + l];
+            lg0 = sp.log_lut[c0.n];
+            v0 = uct_value(c0, cp, cur_logN, sp.uct_c);
+          }
+          if (WW::kTwoSlots && l + 64 < cur_nc) {
+            c1 = nodes[cur_first + l + 64];
+            lg1 = sp.log_lut[c1.n];
+            v1 = uct_value(c1, cp, cur_logN, sp.uct_c);
+          }
         }
         chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
+        if (depth == 0) root_k = chosen;
         const int src = chosen & 63;
         const bool hi = WW::kTwoSlots && chosen >= 64;  // wave-uniform
         const Node<R> bc = hi ? c1 : c0;
@@ -572,6 +614,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         const int r0 = G::ret0(s, g, ctx);
         leaf_out = static_cast<int8_t>(r0);
         if (l == 0) nodes[cur_idx].out = leaf_out;
+        if (depth == 1 && l == (root_k & 63)) {
+          if (root_k < 64) rc0.out = leaf_out;
+          else rc1.out = leaf_out;
+        }
         solved = sp.solve != 0;
         rv0 = static_cast<R>(r0);
         rv1 = static_cast<R>(-r0);
@@ -609,6 +655,17 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       root_n += 1;
       root_logN = sp.log_lut[root_n];  // next simulation's root scan
       root_w += P0 == 0 ? rv0 : rv1;
+      if (depth >= 1 && l == (root_k & 63)) {  // mirror of path[1]'s update
+        if (root_k < 64) {
+          rc0.n += 1;
+          rc0.w += P0 == 0 ? rv0 : rv1;
+          rlg0 = sp.log_lut[rc0.n];
+        } else {
+          rc1.n += 1;
+          rc1.w += P0 == 0 ? rv0 : rv1;
+          rlg1 = sp.log_lut[rc1.n];
+        }
+      }
       if (l == 0) {
         nodes[0].n = root_n;
         nodes[0].w = root_w;
@@ -641,7 +698,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             const int k = l + 64 * h;
             int8_t co = kUnsolved;
             if (k < nnc) {
-              co = (nfirst + k == prev_idx) ? prev_out : nodes[nfirst + k].out;
+              co = (nfirst + k == prev_idx)
+                       ? prev_out
+                       : (d == 0 ? (h == 0 ? rc0.out : rc1.out) : nodes[nfirst + k].out);
             }
             const bool uns = k < nnc && co == kUnsolved;
             if (ballot(uns)) any_unsolved = true;
@@ -657,6 +716,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             const int8_t no = static_cast<int8_t>(cpl == 0 ? best_v : -best_v);
             if (l == 0) nodes[nidx].out = no;
             if (d == 0) root_out = no;
+            if (d == 1 && l == (root_k & 63)) {
+              if (root_k < 64) rc0.out = no;
+              else rc1.out = no;
+            }
             prev_idx = nidx;
             prev_out = no;
           } else {
@@ -688,6 +751,11 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         __threadfence_block();
         root_nc = nodes[0].nchild;
         root_first = nodes[0].first;
+        // GC may have detached root children's subtrees: reload the mirror.
+        rc0 = l < root_nc ? nodes[root_first + l] : zero_node;
+        rc1 = WW::kTwoSlots && l + 64 < root_nc ? nodes[root_first + l + 64] : zero_node;
+        rlg0 = sp.log_lut[rc0.n];
+        rlg1 = sp.log_lut[rc1.n];
       }
     }
     OS_PH_ADD(ph.c[kPhTail], t_ph);
