@@ -239,6 +239,8 @@ __global__ __launch_bounds__(64) void k_wsearch(DevArgs a) {
   WaveMt bot, ev;
   bot.s = mt;
   ev.s = mt + kMtN;
+  bot.use7 = 0;
+  ev.use7 = SmallAbsl<G>::value && Policy == kPolicyCpp && !shared ? 1 : 0;
   if (a.import_state) {
     const uint32_t* g0 = a.mt + lr * 2 * kMtN;
     for (int i = l; i < 2 * kMtN; i += 64) mt[i] = g0[i];
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(64) void k_wsearch(DevArgs a) {
                                   a.path_cap, ph)
       : wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
                                   a.path_cap, ph);
-  res.rng_words = bot.words + (shared ? 0u : ev.words);
+  res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
   ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);
   if (l == 0)
@@ -391,6 +393,8 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
   b0.s = mt;
   b1.s = mt + kMtN;
   ev.s = mt + 2 * kMtN;
+  b0.use7 = b1.use7 = 0;
+  ev.use7 = SmallAbsl<G>::value ? 1 : 0;
   if (l == 0) {
     mt_seed(b0.s, a.bot_seeds[2 * gg]);
     mt_seed(b1.s, a.bot_seeds[2 * gg + 1]);
@@ -464,7 +468,7 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
     s = make_uniform(s);
     ++m;
   }
-  tot.rng_words = b0.words + b1.words + ev.words;
+  tot.rng_words = b0.words.get() + b1.words.get() + ev.words.get();
   for (int k = m + l; k < a.max_len; k += 64) a.actions[gg * a.max_len + k] = -1;
   if (a.visits) {  // rows after the last move are all-zero policy targets
     int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
@@ -639,6 +643,7 @@ __global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
   __shared__ uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
   WaveMt ev;
   ev.s = mt;
+  ev.use7 = SmallAbsl<G>::value ? 1 : 0;
   if (lane_id() == 0) mt_seed(mt, a.seeds[i]);
   __syncthreads();
   ev.init_seeded();

@@ -79,6 +79,20 @@ __device__ __forceinline__ uint32_t wl32(uint32_t v, int lane, uint32_t old) {
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// An instrumentation counter kept in lane 0 of a VGPR rather than in an
+// SGPR: the wave kernels are SGPR-bound (the state, the tree walk and both
+// MT streams are scalar), and a spilled SGPR costs far more than one VALU op.
+struct LaneCount {
+  uint32_t v;
+  __device__ void reset() { v = 0; }
+  __device__ void add(uint32_t x) { v += lane_id() == 0 ? x : 0u; }
+  __device__ void max(uint32_t x) {
+    const uint32_t y = lane_id() == 0 ? x : 0u;
+    v = y > v ? y : v;
+  }
+  __device__ uint32_t get() const { return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0)); }
+};
+
 // Marks a trivially-copyable value as wave-uniform (v_readfirstlane per
 // dword) so the compiler keeps it, and everything computed from it, in SGPRs
 // and runs the game logic on the scalar unit.
@@ -103,7 +117,7 @@ struct WaveMt {
   int base;        // first word index held in cur; kMtN => block exhausted
   int valid;       // words held in cur
   int pos;         // next word (offset in cur)
-  uint32_t words;  // draws (instrumentation)
+  LaneCount words;  // draws (instrumentation; lane 0 of a VGPR)
 #if OS_PHASE_TIMING
   uint64_t twist_cycles;
 #endif
@@ -112,14 +126,14 @@ struct WaveMt {
     base = kMtN;
     valid = 0;
     pos = 0;
-    words = 0;
+    words.reset();
 #if OS_PHASE_TIMING
     twist_cycles = 0;
 #endif
   }
   // numpy legacy (key, p): key is a fully twisted block, p words consumed.
   __device__ void init_import(int p) {
-    words = 0;
+    words.reset();
 #if OS_PHASE_TIMING
     twist_cycles = 0;
 #endif
@@ -134,6 +148,7 @@ struct WaveMt {
     const int i = base + lane_id();
     cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
     pos = p - base;
+    if (use7) compute_small();
   }
   __device__ int export_pos() const { return base >= kMtN ? kMtN : base + pos; }
 
@@ -174,12 +189,54 @@ struct WaveMt {
     const int i = base + lane_id();
     cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
     pos = 0;
+    if (use7) compute_small();
+  }
+
+  // Small-range absl draws precomputed on the vector unit (connect_four
+  // rollouts, n = |LegalActions| <= 7): lane l packs, for the word pair
+  // (w_l, w_{l+1}) of the window, absl::Uniform(0, n) for n = 1..7 in bits
+  // 3(n-1)..3(n-1)+2 (os_rng.h AbslUniform: power-of-two n -> low bits of the
+  // second word; else the high half of the 64x32 Lemire product); bit 31 marks
+  // a pair without a next word in the window or one that could need absl's
+  // rejection step -- uniform_small() then takes the exact scalar path.
+  uint32_t pre7;
+  int use7;
+  __device__ void compute_small() {
+    const int l = lane_id();
+    const uint32_t hi = cur;
+    const uint32_t lo = static_cast<uint32_t>(__shfl_down(static_cast<int>(cur), 1));
+    uint32_t pk = (l + 1 >= valid) ? 0x80000000u : 0u;
+    for (uint32_t n = 2; n <= 7; ++n) {
+      uint32_t r;
+      if ((n & (n - 1)) == 0) {
+        r = lo & (n - 1);
+      } else {
+        const uint64_t b = static_cast<uint64_t>(lo) * n;
+        const uint64_t mid = static_cast<uint64_t>(hi) * n + (b >> 32);
+        if (static_cast<uint32_t>(mid) == 0 && static_cast<uint32_t>(b) < n) pk |= 0x80000000u;
+        r = static_cast<uint32_t>(mid >> 32);
+      }
+      pk |= r << (3 * (n - 1));
+    }
+    pre7 = pk;
+  }
+  // absl::Uniform(rng, 0u, n) for n <= 7 from the precomputed table, falling
+  // back to the exact two-word draw (os_rng.h) when the table cannot answer.
+  __device__ uint32_t uniform_small(uint32_t n) {
+    if (pos + 2 <= valid) {
+      const uint32_t pk = rl32(pre7, pos);
+      if (!(pk >> 31)) {
+        pos += 2;
+        words.add(2);
+        return (pk >> (3 * (n - 1))) & 7u;
+      }
+    }
+    return AbslUniform(*this, n);
   }
   __device__ void uniformize() {
     pos = __builtin_amdgcn_readfirstlane(pos);
     valid = __builtin_amdgcn_readfirstlane(valid);
     base = __builtin_amdgcn_readfirstlane(base);
-    words = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(words)));
   }
   __device__ uint32_t next() {
 #if OS_UNI_MT
@@ -192,7 +249,7 @@ struct WaveMt {
     if (pos >= valid) refill();
     const uint32_t w = rl32(cur, pos);
     ++pos;
-    ++words;
+    words.add(1);
     return w;
   }
 };
@@ -333,6 +390,17 @@ __device__ __forceinline__ int wave_argmax2(double v0, double v1) {
   return 64 + ctz64(ballot(v1 == m));
 }
 
+// Games whose rollout draws use WaveMt::uniform_small (|LegalActions| <= 7,
+// C++ policy): the evaluator stream then needs use7 = 1.
+template <class G>
+struct SmallAbsl {
+  static constexpr bool value = false;
+};
+template <>
+struct SmallAbsl<ConnectFour> {
+  static constexpr bool value = true;
+};
+
 // Lanes that can hold a child of a node (compile-time, per game): the UCT
 // argmax only reduces over those; TwoSlots when a node can have > 64 children.
 template <class G>
@@ -373,9 +441,13 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
 #endif
     if (G::terminal(s, g)) break;
     const typename G::Legal l = G::legal(s, g, ctx);
-    const uint32_t k = Policy == kPolicyCpp
-                           ? AbslUniform(ev, static_cast<uint32_t>(l.count))
-                           : NpChoice(ev, static_cast<uint32_t>(l.count));
+    uint32_t k;
+    if (Policy == kPolicyCpp && SmallAbsl<G>::value)
+      k = ev.uniform_small(static_cast<uint32_t>(l.count));
+    else if (Policy == kPolicyCpp)
+      k = AbslUniform(ev, static_cast<uint32_t>(l.count));
+    else
+      k = NpChoice(ev, static_cast<uint32_t>(l.count));
     G::apply(s, g, ctx, l.kth(static_cast<int>(k)));
   }
   return G::ret0(s, g, ctx);
@@ -397,6 +469,12 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   res.gc_runs = 0;
   res.max_depth = 0;
   res.scanned = res.backed = res.expanded = res.solver_scanned = 0;
+  LaneCount c_scanned, c_backed, c_expanded, c_solver, c_depth;  // VGPR-resident
+  c_scanned.reset();
+  c_backed.reset();
+  c_expanded.reset();
+  c_solver.reset();
+  c_depth.reset();
   const int P0 = G::to_move(root);
   if (l == 0) {
     nodes[0].first = 0;
@@ -525,7 +603,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           }
         }
         nodes_count += nc;
-        res.expanded += nc;
+        c_expanded.add(nc);
         cur_first = first;
         cur_nc = nc;
         chosen = 0;  // all children fresh: +inf, the first one wins
@@ -540,7 +618,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         // log(n) of its own child, which is log(N_parent) one level down if
         // that child is chosen, so the next level needs no dependent load.
         const int cp = P0 ^ (depth & 1);
-        res.scanned += cur_nc;
+        c_scanned.add(cur_nc);
         Node<R> c0 = zero_node, c1 = zero_node;
         double v0 = -inf, v1 = -inf, lg0 = 0.0, lg1 = 0.0;
         if (depth == 0) {  // root children: register-resident, no loads
@@ -601,7 +679,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         pe.w = c_w;
       }
     }
-    if (depth > res.max_depth) res.max_depth = depth;
+    c_depth.max(depth);
     __builtin_amdgcn_wave_barrier();
     OS_PH_ADD(ph.c[kPhSelect], t_ph);
     t_ph = OS_PH_NOW();
@@ -641,7 +719,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       OS_PH_ADD(ph.c[kPhRollout], t_ph);
       t_ph = OS_PH_NOW();
       // ---- backup: every path node at once (lane d <-> depth d) ----
-      res.backed += depth + 1;
+      c_backed.add(depth + 1);
       for (int d0 = 1; d0 <= depth; d0 += 64) {
         const int d = d0 + l;
         if (d <= depth) {
@@ -691,7 +769,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           }
           if (nnc == 0) continue;  // unreachable: path nodes below have children
           const int cpl = P0 ^ (d & 1);
-          res.solver_scanned += nnc;
+          c_solver.add(nnc);
           bool any_unsolved = false;
           int best_v = -128;
           for (int h = 0; h < 2; ++h) {
@@ -762,6 +840,11 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   }
 done:
   OS_PH_ADD(ph.c[kPhTotal], t_begin);
+  res.scanned = c_scanned.get();
+  res.backed = c_backed.get();
+  res.expanded = c_expanded.get();
+  res.solver_scanned = c_solver.get();
+  res.max_depth = static_cast<int32_t>(c_depth.get());
   res.nodes = nodes_count;
   res.used = used;
   return res;
