@@ -33,6 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "open_spiel-1_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+N_CUS = 256
+CLOCK_HZ = 2.4e9  # max engine clock (MI355X_MICROARCH.md)
 EVAL_OFFSET = 1 << 20
 
 # name: (mode, game string, units per GPU (or total for c5), sims, root plies)
@@ -163,7 +165,22 @@ def _roofline(kernel, game, alg_bytes, kernel_ms, units, unit_name):
       "kernel": kernel, "kernel_ms_per_launch": kernel_ms,
       "algorithmic_bytes_per_launch": alg_bytes,
       "algorithmic_bytes_per_%s" % unit_name: alg_bytes / max(units, 1),
+      "issue": _issue_roofline(kernel, game, units, kernel_ms),
   }
+
+
+def _issue_roofline(kernel, game, units, kernel_ms):
+  """The bound that does apply: scalar-instruction issue.  One
+  CU issues at most one SALU instruction per clock; SALU instructions per unit
+  come from the committed PMC summary of this kernel (SQ_INSTS_SALU per sim),
+  the rate from this run's live kernel time."""
+  per = pmc_per_unit(kernel, game, "SQ_INSTS_SALU")
+  if per is None:
+    return None
+  rate = per * units / (kernel_ms / 1e3)
+  peak = N_CUS * CLOCK_HZ
+  return {"bound": "salu-issue", "salu_per_unit": per, "achieved": rate / 1e9,
+          "peak": peak / 1e9, "unit": "G SALU instr/s", "frac": rate / peak}
 
 
 # ---------------------------------------------------------------------------
@@ -473,6 +490,15 @@ def pmc_traffic(kernel, game):
   with open(path) as f:
     d = json.load(f)
   return d.get("%s/%s" % (kernel, game), {}).get("hbm_bytes_per_launch")
+
+
+def pmc_per_unit(kernel, game, counter):
+  path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+  if not os.path.exists(path):
+    return None
+  with open(path) as f:
+    d = json.load(f)
+  return d.get("%s/%s" % (kernel, game), {}).get("per_sim", {}).get(counter)
 
 
 if __name__ == "__main__":
