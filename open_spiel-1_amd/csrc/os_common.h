@@ -74,6 +74,22 @@ struct B128 {
   uint64_t lo, hi;
 };
 OS_HD B128 b128(uint64_t lo, uint64_t hi) { B128 r; r.lo = lo; r.hi = hi; return r; }
+// Selects on B128 go word by word: a conditional of class type is emitted as
+// a select of the two operands' ADDRESSES, which pins both in scratch.
+OS_HD B128 sel128(bool c, B128 x, B128 y) {
+  const uint64_t lo = c ? x.lo : y.lo;
+  const uint64_t hi = c ? x.hi : y.hi;
+  return b128(lo, hi);
+}
+OS_HD B128 pick(const B128* a, int i) {
+  const uint64_t l0 = a[0].lo, h0 = a[0].hi, l1 = a[1].lo, h1 = a[1].hi;
+  return b128(i ? l1 : l0, i ? h1 : h0);
+}
+OS_HD void put(B128* a, int i, B128 v) {
+  const uint64_t l0 = a[0].lo, h0 = a[0].hi, l1 = a[1].lo, h1 = a[1].hi;
+  a[0] = b128(i ? l0 : v.lo, i ? h0 : v.hi);
+  a[1] = b128(i ? v.lo : l1, i ? v.hi : h1);
+}
 OS_HD B128 operator|(B128 a, B128 b) { return b128(a.lo | b.lo, a.hi | b.hi); }
 OS_HD B128 operator&(B128 a, B128 b) { return b128(a.lo & b.lo, a.hi & b.hi); }
 OS_HD B128 operator^(B128 a, B128 b) { return b128(a.lo ^ b.lo, a.hi ^ b.hi); }

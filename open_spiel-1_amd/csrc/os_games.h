@@ -389,8 +389,10 @@ struct Hex {
         if (nx == comp) break;
         comp = nx;
       }
-      if (a) put(s.ea, p, ea | comp);
-      else put(s.eb, p, eb | comp);
+      // Both pairs are written on this path (no store sinking through a
+      // pointer phi, which would pin the state in scratch).
+      put(s.ea, p, sel128(a, ea | comp, ea));
+      put(s.eb, p, sel128(a, eb, eb | comp));
     }
     s.to_play = static_cast<uint8_t>(1 - p);
     s.moves++;

@@ -122,14 +122,20 @@ struct WaveMt {
   uint64_t twist_cycles;
 #endif
 
+  // Every field is written on every path, and the last store of each path
+  // is to the same field: SimplifyCFG otherwise sinks the tail stores of two
+  // paths (pos = 0 / pre7 = ...) into one store through a phi of pointers,
+  // which leaves pos and pre7 in scratch for the whole kernel.
   __device__ void init_seeded() {  // state = init_genrand output, untwisted
-    base = kMtN;
-    valid = 0;
-    pos = 0;
     words.reset();
 #if OS_PHASE_TIMING
     twist_cycles = 0;
 #endif
+    cur = 0;
+    pre7 = 0x80000000u;
+    base = kMtN;
+    valid = 0;
+    pos = 0;
   }
   // numpy legacy (key, p): key is a fully twisted block, p words consumed.
   __device__ void init_import(int p) {
@@ -137,18 +143,13 @@ struct WaveMt {
 #if OS_PHASE_TIMING
     twist_cycles = 0;
 #endif
-    if (p >= kMtN) {
-      base = kMtN;
-      valid = 0;
-      pos = 0;
-      return;
-    }
-    base = p & ~63;
-    valid = kMtN - base < 64 ? kMtN - base : 64;
+    const bool live = p < kMtN;
+    base = live ? (p & ~63) : kMtN;
+    valid = live ? (kMtN - base < 64 ? kMtN - base : 64) : 0;
     const int i = base + lane_id();
     cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
-    pos = p - base;
-    if (use7) compute_small();
+    pre7 = use7 && live ? small7() : 0x80000000u;
+    pos = live ? p - base : 0;
   }
   __device__ int export_pos() const { return base >= kMtN ? kMtN : base + pos; }
 
@@ -188,8 +189,8 @@ struct WaveMt {
     valid = kMtN - base < 64 ? kMtN - base : 64;
     const int i = base + lane_id();
     cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    if (use7) pre7 = small7();
     pos = 0;
-    if (use7) compute_small();
   }
 
   // Small-range absl draws precomputed on the vector unit (connect_four
@@ -201,7 +202,7 @@ struct WaveMt {
   // rejection step -- uniform_small() then takes the exact scalar path.
   uint32_t pre7;
   int use7;
-  __device__ void compute_small() {
+  __device__ uint32_t small7() const {
     const int l = lane_id();
     const uint32_t hi = cur;
     const uint32_t lo = static_cast<uint32_t>(__shfl_down(static_cast<int>(cur), 1));
@@ -218,7 +219,7 @@ struct WaveMt {
       }
       pk |= r << (3 * (n - 1));
     }
-    pre7 = pk;
+    return pk;
   }
   // absl::Uniform(rng, 0u, n) for n <= 7 from the precomputed table, falling
   // back to the exact two-word draw (os_rng.h) when the table cannot answer.
