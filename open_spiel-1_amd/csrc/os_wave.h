@@ -430,8 +430,146 @@ __device__ __forceinline__ double uct_value(const Node<R>& c, int cp, double log
   return static_cast<double>(c.w) / dn + uct_c * __builtin_sqrt(logN / dn);
 }
 
+// Inclusive prefix (OR / sum) over the 16 lanes of each DPP row; lanes that
+// would read across the row boundary read 0 (bound_ctrl), the identity.
+template <int Shift>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x110 + Shift, 0xf, 0xf, true));
+}
+__device__ __forceinline__ uint32_t row_scan_add(uint32_t v) {
+  v += row_shr<1>(v);
+  v += row_shr<2>(v);
+  v += row_shr<4>(v);
+  v += row_shr<8>(v);
+  return v;
+}
+// OR over the lanes j <= i of the same parity as i (stride-2 prefix).
+__device__ __forceinline__ uint64_t row_scan_or_stride2(uint64_t v) {
+  uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
+  lo |= row_shr<2>(lo);
+  hi |= row_shr<2>(hi);
+  lo |= row_shr<4>(lo);
+  hi |= row_shr<4>(hi);
+  lo |= row_shr<8>(lo);
+  hi |= row_shr<8>(hi);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// connect_four random playout (mcts.cc:46-55), lane-parallel and speculative.
+// Between two column-fill events the legal set -- hence n = |LegalActions|
+// and the ascending action list -- does not change, so the absl draws of the
+// next K moves are known up front (WaveMt::small7 holds absl::Uniform(0, n)
+// for every word pair of the window).  Lane i plays move i of such a run:
+//   column   = legal[k_i(n)]
+//   row      = height of that column + earlier run moves into it (prefix sum
+//              of one-hot column nibbles over the lanes)
+//   board    = mover's stones + stones of the earlier same-parity lanes
+//              (stride-2 prefix OR)
+//   terminal = has_four(board) || move 42 (connect_four.cc:98-103)
+// The run ends at the first terminal lane, the first lane that fills a
+// column (the legal set changes after it), the end of the MT window or 16
+// moves (one DPP row); a pair the table cannot answer (window edge, possible
+// absl rejection) is drawn by the exact serial path as a 1-move run.  Every
+// move, word and outcome is the serial rollout's (tests/test_gpu_parity.py).
+template <class C>
+__device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
+  (void)ctx;
+  s = make_uniform(s);
+  ev.uniformize();
+  const int l = lane_id();
+  const int i = l & 15;  // run move index (every row computes the same run)
+  // Ascending legal columns as nibbles, and column heights as nibbles.
+  uint32_t cols = 0;
+  {
+    int q = 0;
+    for (uint32_t m = s.legal; m; m &= m - 1, ++q) cols |= static_cast<uint32_t>(ctz64(m)) << (4 * q);
+  }
+  uint32_t heights = 0;
+  {
+    const uint64_t occ = s.bb[0] | s.bb[1];
+    for (int c = 0; c < 7; ++c)
+      heights |= static_cast<uint32_t>(popc64((occ >> (7 * c)) & 0x3full)) << (4 * c);
+  }
+  int p = s.to_play;
+  int moves = s.moves;
+  uint32_t legal = s.legal;
+  uint64_t b0 = s.bb[0], b1 = s.bb[1];
+  for (;;) {
+    const int n = popc64(legal);
+    int K = (ev.valid - ev.pos) >> 1;
+    if (K > 16) K = 16;
+    if (K > 42 - moves) K = 42 - moves;
+    uint32_t k;
+    bool serial = false;
+    if (K > 0) {
+      const uint32_t pk = static_cast<uint32_t>(
+          __builtin_amdgcn_ds_bpermute((ev.pos + 2 * i) << 2, static_cast<int>(ev.pre7)));
+      const uint64_t fl = ballot(l < K && (pk >> 31) != 0);
+      if (fl) K = ctz64(fl);  // lanes before the first unanswerable pair
+      k = (pk >> (3 * (n - 1))) & 7u;
+    }
+    if (K == 0) {  // one exact serial draw (refills the window as needed)
+      k = ev.uniform_small(static_cast<uint32_t>(n));
+      K = 1;
+      serial = true;
+    }
+    const uint32_t col = (cols >> (4 * k)) & 15u;
+    const uint32_t onehot = 1u << (4 * col);
+    const uint32_t incl = row_scan_add(onehot);
+    const uint32_t h = ((heights + incl - onehot) >> (4 * col)) & 15u;
+    const uint64_t fills = ballot(l < K && h == 5);
+    int Kr = K;  // moves of this run
+    if (fills) {
+      const int f = ctz64(fills) + 1;
+      if (f < Kr) Kr = f;
+    }
+    const uint64_t stones = row_scan_or_stride2(1ull << (7 * col + h));
+    const uint64_t mine = ((i & 1) ? (p ? b0 : b1) : (p ? b1 : b0)) | stones;
+    const bool win = ConnectFour::has_four(mine);
+    const uint64_t term = ballot(l < Kr && (win || moves + i + 1 == 42));
+    if (term) {
+      const int t = ctz64(term);
+      if (!serial) {
+        ev.pos += 2 * (t + 1);
+        ev.words.add(2 * (t + 1));
+      }
+      const uint64_t wins = ballot(win);
+      const int winner = p ^ (t & 1);
+      return ((wins >> t) & 1) ? (winner == 0 ? 1 : -1) : 0;
+    }
+    if (!serial) {
+      ev.pos += 2 * Kr;
+      ev.words.add(2 * Kr);
+    }
+    const int last = Kr - 1;
+    const uint64_t blast = rl64(mine, last);
+    const int plast = p ^ (last & 1);
+    if (Kr >= 2) {
+      const uint64_t bprev = rl64(mine, last - 1);
+      b0 = plast == 0 ? blast : bprev;
+      b1 = plast == 0 ? bprev : blast;
+    } else {
+      if (plast == 0) b0 = blast;
+      else b1 = blast;
+    }
+    heights += rl32(incl, last);
+    if ((fills >> last) & 1) {
+      const uint32_t kl = rl32(k, last), cl = rl32(col, last);
+      legal &= ~(1u << cl);
+      const uint32_t below = kl == 0 ? 0u : (cols & ((1u << (4 * kl)) - 1u));
+      cols = below | ((cols >> (4 * (kl + 1))) << (4 * kl));
+    }
+    p ^= Kr & 1;
+    moves += Kr;
+  }
+}
+
 template <class G, int Policy, class Rng, class C>
 __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
+  if constexpr (Policy == kPolicyCpp && SmallAbsl<G>::value) {
+    if (ev.use7) return c4_rollout_lanes(s, ctx, ev);
+  }
 #if OS_UNI_ROLL == 2
   s = make_uniform(s);  // uniform on entry => the loop-carried state can stay in SGPRs
   ev.uniformize();
