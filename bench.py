@@ -141,9 +141,9 @@ def _resolved_layout(game, R, layout):
   from os_amd import _lib
   if layout != _lib.LAYOUT_AUTO:
     return "wave" if layout == _lib.LAYOUT_WAVE else "lane"
-  if game.startswith("hex") or R >= 64 * 1024:
+  if R >= 64 * 1024:
     return "lane"
-  return "wave"
+  return "wave"  # hex included: C++ policy, board_size 11
 
 
 def _base_line(args, ctx, metric, value, unit, elapsed, config):

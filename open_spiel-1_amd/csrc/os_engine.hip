@@ -943,12 +943,14 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
 }
 
 // OS_LAYOUT_AUTO: one wave per search unless the batch alone fills the chip
-// with lane-per-search waves, or the game's per-ply work is wide (hex: the
-// lane layout was 3.5x faster at 4096 roots; profiles/r01/layout_probe.txt).
-int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R) {
+// with lane-per-search waves (>= 1024 waves).  hex takes the wave layout only
+// where its playouts run lane-parallel (C++ policy, n >= 3; os_wave.h
+// hex_rollout_lanes: 6.5e7 vs 1.4e7 sims/s at 4096 roots, profiles/r01).
+int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
   if (layout != OS_LAYOUT_AUTO) return layout;
-  if (cfg.kind == kHex) return OS_LAYOUT_LANE;
-  if (R >= 64 * 1024) return OS_LAYOUT_LANE;  // >= 1024 waves: one per SIMD
+  if (R >= 64 * 1024) return OS_LAYOUT_LANE;
+  if (cfg.kind == kHex)
+    return policy == OS_POLICY_CPP && cfg.rows >= 3 ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
   return OS_LAYOUT_WAVE;
 }
 
@@ -961,7 +963,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   if (R < 0) return Fail(OS_ERR_INVALID, "num_roots < 0");
   HIP_TRY(hipSetDevice(e->device));
   e->params = *p;
-  e->params.layout = ResolveLayout(e->game.cfg, p->layout, R);
+  e->params.layout = ResolveLayout(e->game.cfg, p->layout, R, p->policy);
   e->num_roots = R;
   const GameCfg& cfg = e->game.cfg;
   e->max_children = cfg.max_children;

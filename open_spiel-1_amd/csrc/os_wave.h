@@ -234,6 +234,39 @@ struct WaveMt {
     }
     return AbslUniform(*this, n);
   }
+  // Stream offset of the next word, counted from the start of the block in s
+  // (kMtN when that block is used up and the next draw twists).
+  __device__ int offset() const { return base >= kMtN ? kMtN : base + pos; }
+  // Untempered word q (q < kMtN + 454) of the stream counted like offset(),
+  // read without changing the block: the next block's word i follows the
+  // in-place twist (it reads s[i], s[i+1] and s[i+397], which is already new
+  // for i >= 227), so words of the next block are recomputed from the old.
+  __device__ static uint32_t mix(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+  __device__ uint32_t peek_raw(int q) const {
+    if (q < kMtN) return s[q];
+    const int i = q - kMtN;
+    const uint32_t v = mix(s[i], s[i + 1]);
+    if (i < kMtN - kMtM) return v ^ s[i + kMtM];
+    const int i2 = i - (kMtN - kMtM);
+    return v ^ mix(s[i2], s[i2 + 1]) ^ s[i2 + kMtM];
+  }
+  // Moves the stream to offset q (< 2 kMtN; counted like offset()), twisting
+  // the block when q has left it; the window is re-read as refill() would.
+  __device__ void seek(int q) {
+    if (q >= kMtN) {
+      twist();
+      q -= kMtN;
+    }
+    base = q & ~63;
+    valid = kMtN - base < 64 ? kMtN - base : 64;
+    const int i = base + lane_id();
+    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    pre7 = use7 ? small7() : 0x80000000u;
+    pos = q - base;
+  }
   __device__ void uniformize() {
     pos = __builtin_amdgcn_readfirstlane(pos);
     valid = __builtin_amdgcn_readfirstlane(valid);
@@ -565,10 +598,157 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
   }
 }
 
+// Inclusive OR scan over the 64 lanes: the DPP row scan, then row_bcast15 /
+// row_bcast31 carry rows 0-1 into rows 1-3 (as wave_max_f64).
+__device__ __forceinline__ uint32_t wave_scan_or32(uint32_t v) {
+  v |= row_shr<1>(v);
+  v |= row_shr<2>(v);
+  v |= row_shr<4>(v);
+  v |= row_shr<8>(v);
+  v |= static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v |= static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_scan_or64(uint64_t v) {
+  const uint32_t lo = wave_scan_or32(static_cast<uint32_t>(v));
+  const uint32_t hi = wave_scan_or32(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+// Set bits of the wave-uniform mask m in the lanes below this one.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
+// Not a playout return value: the lane-parallel playout declines and the
+// exact serial loop runs instead (the stream has not moved).
+constexpr int kLanesDecline = 2;
+
+// hex random playout (mcts.cc:46-55), lane-parallel.  Hex only ever fills
+// empty cells and a filled board always has exactly one connected player
+// (hex.cc:149-184 labels; no draws), so the serial playout is recovered from
+// three data-parallel steps:
+//   draws  |LegalActions| before move j is n0 - j whatever was played, so
+//          lane j draws absl::Uniform(0, n0 - j) from the word pair at
+//          offset 2j (os_rng.h AbslUniform; words past the block come from
+//          WaveMt::peek_raw).  A pair absl might reject (P mod 2^64 < n)
+//          declines the whole playout to the serial path.
+//   cells  move j takes the k_j-th empty cell, ascending: one rank-select
+//          per move (mbcnt ranks, ballot, s_ff1) -- the only serial chain.
+//   end    connection is monotone, so the winner W is the player connected
+//          on the filled board and the playout ends at W's first connecting
+//          move (the reference stops at the stone whose group reaches both
+//          edges).  Lane m flood-fills W's stones after W's m-th move (a
+//          prefix OR over the lanes); the lowest connected lane is that move.
+// The stream then advances by the 2 (T + 1) words the serial playout draws.
+template <class C>
+__device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
+  (void)ctx;
+  s = make_uniform(s);
+  ev.uniformize();
+  if (Hex::terminal(s, g)) return s.result;
+  const int l = lane_id();
+  const int n = g.rows;
+  const B128 empty = g.board & ~(s.st[0] | s.st[1]);
+  const int n0 = popc(empty);
+  const int q0 = ev.offset();
+  uint32_t k0 = 0, k1 = 0;  // draws of moves l and l + 64
+  bool risky = false;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = l + 64 * h;
+    uint32_t k = 0;
+    if (j < n0) {
+      const uint32_t hi = MtStream::temper(ev.peek_raw(q0 + 2 * j));
+      const uint32_t lo = MtStream::temper(ev.peek_raw(q0 + 2 * j + 1));
+      const uint32_t m = static_cast<uint32_t>(n0 - j);
+      if ((m & (m - 1u)) == 0) {
+        k = lo & (m - 1u);
+      } else {
+        const uint64_t b = static_cast<uint64_t>(lo) * m;
+        const uint64_t mid = static_cast<uint64_t>(hi) * m + (b >> 32);
+        risky |= static_cast<uint32_t>(mid) == 0 && static_cast<uint32_t>(b) < m;
+        k = static_cast<uint32_t>(mid >> 32);
+      }
+    }
+    if (h == 0) k0 = k;
+    else k1 = k;
+  }
+  if (ballot(risky)) return kLanesDecline;
+  // Cells of the fill: move j's cell in lane j % 64 of cell0 / cell1.
+  uint64_t e0 = empty.lo, e1 = empty.hi;
+  uint32_t cell0 = 0, cell1 = 0;
+  for (int j = 0; j < n0; ++j) {
+    const uint32_t k = j < 64 ? rl32(k0, j) : rl32(k1, j - 64);
+    const uint32_t c = static_cast<uint32_t>(popc64(e0));
+    const bool low = k < c;
+    const uint64_t e = low ? e0 : e1;
+    const uint32_t kk = low ? k : k - c;
+    const uint64_t at = ballot(lanes_below(e) == kk) & e;  // the kk-th set bit
+    e0 = low ? e0 & ~at : e0;
+    e1 = low ? e1 : e1 & ~at;
+    const int cell = ctz64(at) + (low ? 0 : 64);
+    if (j < 64) cell0 = wl32(static_cast<uint32_t>(cell), j, cell0);
+    else cell1 = wl32(static_cast<uint32_t>(cell), j - 64, cell1);
+  }
+  // Edge rows / columns (hex.cc:55-90 PlayerAndActionToState: north row
+  // < n, south row >= n(n-1), west col 0, east col n-1).
+  const int nn = n * n;
+  const int ca = l, cb = l + 64;
+  const B128 north = b128(ballot(ca < n), ballot(cb < n));
+  const B128 south = b128(ballot(ca < nn && ca >= nn - n), ballot(cb < nn && cb >= nn - n));
+  const B128 west = b128(ballot(ca < nn && ca % n == 0), ballot(cb < nn && cb % n == 0));
+  const B128 east = b128(ballot(ca < nn && ca % n == n - 1), ballot(cb < nn && cb % n == n - 1));
+  int T = -1, winner = 0;
+  for (int par = 0; par < 2; ++par) {
+    const int X = s.to_play ^ par;
+    const int cnt = (n0 - par + 1) >> 1;  // X's moves in the fill
+    const int j = par + 2 * l;            // lane l <-> X's l-th move
+    const bool mine = l < cnt;
+    const int src = (j & 63) << 2;
+    const uint32_t c_lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(cell0)));
+    const uint32_t c_hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(cell1)));
+    const uint32_t cell = j < 64 ? c_lo : c_hi;
+    const uint64_t olo = mine && cell < 64 ? 1ull << cell : 0ull;
+    const uint64_t ohi = mine && cell >= 64 ? 1ull << (cell - 64) : 0ull;
+    const B128 st = b128(wave_scan_or64(olo), wave_scan_or64(ohi)) | pick(s.st, X);
+    const B128 ea = sel128(X == 0, north, west), eb = sel128(X == 0, south, east);
+    B128 comp = st & ea;
+    bool conn = any(comp & eb);
+    for (;;) {
+      const B128 nx = comp | (Hex::nbr6(comp, g) & st);
+      const bool grow = nx != comp;
+      comp = nx;
+      conn = any(comp & eb);
+      if (!ballot(mine && grow && !conn)) break;
+    }
+    const uint64_t hit = ballot(mine && conn);
+    if (hit) {
+      T = par + 2 * ctz64(hit);
+      winner = X;
+      break;
+    }
+  }
+  if (T < 0) return kLanesDecline;  // unreachable: a filled board has a winner
+  ev.seek(q0 + 2 * (T + 1));
+  ev.words.add(2 * (T + 1));
+  return winner == 0 ? 1 : -1;
+}
+
 template <class G, int Policy, class Rng, class C>
 __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
   if constexpr (Policy == kPolicyCpp && SmallAbsl<G>::value) {
     if (ev.use7) return c4_rollout_lanes(s, ctx, ev);
+  }
+  if constexpr (Policy == kPolicyCpp && std::is_same<G, Hex>::value) {
+    // n >= 3: on n <= 2 the reference's wrap filter (hex.cc:206-222) leaves
+    // filled boards without a winner, so the end-of-fill argument fails.
+    if (g.rows >= 3) {
+      const int r = hex_rollout_lanes(s, g, ctx, ev);
+      if (r != kLanesDecline) return r;
+    }
   }
 #if OS_UNI_ROLL == 2
   s = make_uniform(s);  // uniform on entry => the loop-carried state can stay in SGPRs

@@ -112,6 +112,39 @@ def test_recorded_reference_outputs_on_device(E):
   assert o["root_w"][0] == case["root_w"]
 
 
+# The wave layout plays hex playouts lane-parallel (os_wave.h
+# hex_rollout_lanes): every board size it takes, roots deep and shallow, MT
+# blocks crossed mid-playout by long searches, n_rollouts > 1.
+@pytest.mark.parametrize("gs,R,sims,plies,nr", [
+    ("hex(board_size=3)", 32, 300, 2, 1),
+    ("hex(board_size=5)", 32, 400, 6, 1), ("hex(board_size=7)", 16, 500, 10, 2),
+    ("hex", 16, 600, 4, 1), ("hex", 4, 2048, 0, 1), ("hex", 8, 300, 60, 3)])
+def test_hex_wave_lane_playouts_bit_exact(E, gs, R, sims, plies, nr):
+  from os_amd import _lib
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, R, 1000, plies)
+  bs = np.arange(R, dtype=np.uint32) + 11
+  es = bs + np.uint32(1 << 20)
+  kw = dict(uct_c=2.0, max_simulations=sims, n_rollouts=nr)
+  got = eng.mcts_batch(acts, offs, bs, es, layout=_lib.LAYOUT_WAVE, **kw)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children,
+                              threads=8, **kw)
+  _cmp(E, got, ref)
+
+
+@pytest.mark.parametrize("gs,plies", [("hex", 0), ("hex", 40), ("hex(board_size=4)", 3),
+                                      ("hex(board_size=3)", 0)])
+def test_hex_wave_rollouts_bit_exact(E, gs, plies):
+  from os_amd import _lib
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, 1, 77, plies)
+  seeds = np.arange(4096, dtype=np.uint32) * 7 + 3
+  for nr in (1, 4):
+    got = eng.rollouts(acts, seeds, n_rollouts=nr, layout=_lib.LAYOUT_WAVE)
+    ref = O.Game(gs).rollouts(acts, seeds, n_rollouts=nr)
+    assert np.array_equal(got, ref), nr
+
+
 @pytest.mark.parametrize("gs,plies", [("connect_four", 10), ("breakthrough", 20),
                                       ("hex", 30), ("go(board_size=9)", 0),
                                       ("go(board_size=9)", 40)])
