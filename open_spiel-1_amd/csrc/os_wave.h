@@ -626,23 +626,58 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // exact serial loop runs instead (the stream has not moved).
 constexpr int kLanesDecline = 2;
 
+// Pairs of u16 packed in a dword: the two cells a lane holds (cell l in the
+// low half, cell l + 64 in the high half) -- v_pk_min_u16 / v_pk_max_u16.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                __builtin_bit_cast(u16x2, b)));
+}
+// Lanes whose bit is set in the wave-uniform mask m (v_cndmask on an SGPR pair).
+__device__ __forceinline__ bool in_mask(uint64_t m) {
+  return __builtin_amdgcn_inverse_ballot_w64(m);
+}
+
+// Move of the fill: the k-th empty cell (ascending) of e0 (cells 0-63) / e1
+// (cells 64-127) gets fill time tau.  Lane l ranks cells l and l + 64 among
+// the empty cells by mbcnt; the empty cell whose rank is k is the move.
+__device__ __forceinline__ void hex_take(uint64_t& e0, uint64_t& e1, uint32_t k, uint32_t tau,
+                                         uint32_t& t0, uint32_t& t1) {
+  const uint32_t c0 = static_cast<uint32_t>(popc64(e0));
+  const uint64_t h0 = ballot(lanes_below(e0) == k) & e0;
+  const uint64_t h1 = ballot(lanes_below(e1) + c0 == k) & e1;
+  e0 &= ~h0;
+  e1 &= ~h1;
+  t0 = in_mask(h0) ? tau : t0;
+  t1 = in_mask(h1) ? tau : t1;
+}
+
 // hex random playout (mcts.cc:46-55), lane-parallel.  Hex only ever fills
-// empty cells and a filled board always has exactly one connected player
-// (hex.cc:149-184 labels; no draws), so the serial playout is recovered from
-// three data-parallel steps:
+// empty cells, and on n >= 3 a filled board has exactly one player whose
+// stones join their two edges (hex.cc:55-184 labels; no draws), so the serial
+// playout is recovered from three data-parallel steps:
 //   draws  |LegalActions| before move j is n0 - j whatever was played, so
 //          lane j draws absl::Uniform(0, n0 - j) from the word pair at
 //          offset 2j (os_rng.h AbslUniform; words past the block come from
 //          WaveMt::peek_raw).  A pair absl might reject (P mod 2^64 < n)
 //          declines the whole playout to the serial path.
-//   cells  move j takes the k_j-th empty cell, ascending: one rank-select
-//          per move (mbcnt ranks, ballot, s_ff1) -- the only serial chain.
-//   end    connection is monotone, so the winner W is the player connected
-//          on the filled board and the playout ends at W's first connecting
-//          move (the reference stops at the stone whose group reaches both
-//          edges).  Lane m flood-fills W's stones after W's m-th move (a
-//          prefix OR over the lanes); the lowest connected lane is that move.
-// The stream then advances by the 2 (T + 1) words the serial playout draws.
+//   fill   move j takes the k_j-th empty cell, ascending: one rank-select per
+//          move (mbcnt ranks, ballot) -- the only serial chain; each cell
+//          records its fill time tau = j + 1 (0 for stones already placed).
+//   end    connection is monotone, so the playout ends at the first move
+//          after which some player's stones join both edges: the minimum,
+//          over far-edge cells, of the bottleneck time d(c) = min over
+//          same-colour paths from the near edge of the largest tau on the
+//          path.  d is relaxed for both players at once (neighbours of the
+//          other colour are cut) until no lane changes: d = min(d,
+//          max(tau, min over the six neighbours)), neighbours fetched with
+//          ds_bpermute, both cells of a lane in one packed-u16 dword.
+// The winner owns the minimising cell; the stream advances by the 2 (T + 1)
+// words the serial playout draws for its T + 1 moves.
 template <class C>
 __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
   (void)ctx;
@@ -677,63 +712,88 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
     else k1 = k;
   }
   if (ballot(risky)) return kLanesDecline;
-  // Cells of the fill: move j's cell in lane j % 64 of cell0 / cell1.
+  // Fill times of cells l (t0) and l + 64 (t1).
   uint64_t e0 = empty.lo, e1 = empty.hi;
-  uint32_t cell0 = 0, cell1 = 0;
-  for (int j = 0; j < n0; ++j) {
-    const uint32_t k = j < 64 ? rl32(k0, j) : rl32(k1, j - 64);
-    const uint32_t c = static_cast<uint32_t>(popc64(e0));
-    const bool low = k < c;
-    const uint64_t e = low ? e0 : e1;
-    const uint32_t kk = low ? k : k - c;
-    const uint64_t at = ballot(lanes_below(e) == kk) & e;  // the kk-th set bit
-    e0 = low ? e0 & ~at : e0;
-    e1 = low ? e1 : e1 & ~at;
-    const int cell = ctz64(at) + (low ? 0 : 64);
-    if (j < 64) cell0 = wl32(static_cast<uint32_t>(cell), j, cell0);
-    else cell1 = wl32(static_cast<uint32_t>(cell), j - 64, cell1);
-  }
-  // Edge rows / columns (hex.cc:55-90 PlayerAndActionToState: north row
-  // < n, south row >= n(n-1), west col 0, east col n-1).
+  uint32_t t0 = 0, t1 = 0;
+  const int nlo = n0 < 64 ? n0 : 64;
+  for (int j = 0; j < nlo; ++j) hex_take(e0, e1, rl32(k0, j), static_cast<uint32_t>(j + 1), t0, t1);
+  for (int j = 64; j < n0; ++j)
+    hex_take(e0, e1, rl32(k1, j - 64), static_cast<uint32_t>(j + 1), t0, t1);
+  // Per cell: colour (stones already placed by the state, move j by the
+  // player to move ^ (j & 1)), near / far edge (hex.cc:55-90: black north row
+  // -> south row, white west column -> east column), column.
   const int nn = n * n;
-  const int ca = l, cb = l + 64;
-  const B128 north = b128(ballot(ca < n), ballot(cb < n));
-  const B128 south = b128(ballot(ca < nn && ca >= nn - n), ballot(cb < nn && cb >= nn - n));
-  const B128 west = b128(ballot(ca < nn && ca % n == 0), ballot(cb < nn && cb % n == 0));
-  const B128 east = b128(ballot(ca < nn && ca % n == n - 1), ballot(cb < nn && cb % n == n - 1));
-  int T = -1, winner = 0;
-  for (int par = 0; par < 2; ++par) {
-    const int X = s.to_play ^ par;
-    const int cnt = (n0 - par + 1) >> 1;  // X's moves in the fill
-    const int j = par + 2 * l;            // lane l <-> X's l-th move
-    const bool mine = l < cnt;
-    const int src = (j & 63) << 2;
-    const uint32_t c_lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(cell0)));
-    const uint32_t c_hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(cell1)));
-    const uint32_t cell = j < 64 ? c_lo : c_hi;
-    const uint64_t olo = mine && cell < 64 ? 1ull << cell : 0ull;
-    const uint64_t ohi = mine && cell >= 64 ? 1ull << (cell - 64) : 0ull;
-    const B128 st = b128(wave_scan_or64(olo), wave_scan_or64(ohi)) | pick(s.st, X);
-    const B128 ea = sel128(X == 0, north, west), eb = sel128(X == 0, south, east);
-    B128 comp = st & ea;
-    bool conn = any(comp & eb);
-    for (;;) {
-      const B128 nx = comp | (Hex::nbr6(comp, g) & st);
-      const bool grow = nx != comp;
-      comp = nx;
-      conn = any(comp & eb);
-      if (!ballot(mine && grow && !conn)) break;
-    }
-    const uint64_t hit = ballot(mine && conn);
-    if (hit) {
-      T = par + 2 * ctz64(hit);
-      winner = X;
-      break;
-    }
+  const int p = s.to_play;
+  uint32_t tt = 0, dd = 0, far = 0, own = 0;
+  int qa = 0, qb = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = l + 64 * h;
+    const uint32_t t = h ? t1 : t0;
+    const bool on = c < nn;
+    const int q = on ? c % n : 0;
+    const int r = on ? c / n : 0;
+    const uint64_t w1 = h ? s.st[1].hi : s.st[1].lo;
+    const int o = t ? (p ^ static_cast<int>((t - 1) & 1)) : static_cast<int>((w1 >> l) & 1);
+    const bool nearE = on && (o == 0 ? r == 0 : q == 0);
+    const bool farE = on && (o == 0 ? r == n - 1 : q == n - 1);
+    const uint32_t tv = on ? t : 0xFFFFu;
+    tt |= tv << (16 * h);
+    dd |= (nearE ? tv : 0xFFFFu) << (16 * h);
+    far |= (farE ? 0u : 0xFFFFu) << (16 * h);
+    own |= static_cast<uint32_t>(o) << (16 * h);
+    if (h) qb = q;
+    else qa = q;
   }
-  if (T < 0) return kLanesDecline;  // unreachable: a filled board has a winner
-  ev.seek(q0 + 2 * (T + 1));
-  ev.words.add(2 * (T + 1));
+  // The six neighbours (hex.cc:206-222), as lane offsets d: the source lane
+  // is (l + d) & 63; the half and the cut (off the board, a row wrap, or the
+  // other colour) are per lane and fixed for the whole relaxation.
+  const int dl[6] = {-n, -n + 1, -1, 1, n - 1, n};
+  int addr[6];
+  uint32_t sel[6], cut[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int d = dl[i];
+    const int x = l + d;
+    addr[i] = (x & 63) << 2;
+    // byte selector for v_perm_b32(r, r, sel): low half <- r.hi if x >= 64,
+    // high half <- r.lo if x < 0.
+    const uint32_t slo = x >= 64 ? 0x0302u : 0x0100u;
+    const uint32_t shi = x < 0 ? 0x0100u : 0x0302u;
+    sel[i] = slo | (shi << 16);
+    const bool wrap_r = (i == 1 || i == 3);  // +col: cut on the last column
+    const bool wrap_l = (i == 2 || i == 4);  // -col: cut on the first column
+    const int ca = l + d, cb = l + 64 + d;
+    const bool xa = ca < 0 || ca >= nn || (wrap_r && qa == n - 1) || (wrap_l && qa == 0);
+    const bool xb = cb < 0 || cb >= nn || (wrap_r && qb == n - 1) || (wrap_l && qb == 0);
+    const uint32_t r = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(addr[i], static_cast<int>(own)));
+    const uint32_t diff = __builtin_amdgcn_perm(r, r, sel[i]) ^ own;  // 0 / 1 per half
+    cut[i] = (diff * 0xFFFFu) | (xa ? 0xFFFFu : 0u) | (xb ? 0xFFFF0000u : 0u);
+  }
+  for (;;) {
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const uint32_t r = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(addr[i], static_cast<int>(dd)));
+      m = pk_min16(m, __builtin_amdgcn_perm(r, r, sel[i]) | cut[i]);
+    }
+    const uint32_t nd = pk_min16(dd, pk_max16(tt, m));
+    const bool changed = nd != dd;
+    dd = nd;
+    if (!ballot(changed)) break;
+  }
+  // End: the smallest d on a far-edge cell (the loser has none finite).
+  const uint32_t fv = dd | far;
+  uint32_t v = pk_min16(fv, fv >> 16) & 0xFFFFu;
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), off));
+    v = o < v ? o : v;
+  }
+  const uint32_t tend = rl32(v, 0);
+  if (tend == 0 || tend > static_cast<uint32_t>(n0)) return kLanesDecline;  // unreachable
+  const int winner = p ^ static_cast<int>((tend - 1) & 1);  // the mover of the last stone
+  ev.seek(q0 + 2 * static_cast<int>(tend));
+  ev.words.add(2 * tend);
   return winner == 0 ? 1 : -1;
 }
 
