@@ -224,8 +224,21 @@ __host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
          (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
 }
 
+// Minimum waves per SIMD requested from the register allocator (A/B knob).
+#ifndef OS_HEX_OCC
+#define OS_HEX_OCC 1
+#endif
+template <class G>
+struct WaveOcc {
+  static constexpr int value = 1;
+};
+template <>
+struct WaveOcc<Hex> {
+  static constexpr int value = OS_HEX_OCC;
+};
+
 template <class G, class R, int Policy>
-__global__ __launch_bounds__(64) void k_wsearch(DevArgs a) {
+__global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int64_t lr = blockIdx.x;
   if (lr >= a.num_roots) return;
   const int64_t gr = a.root_base + lr;

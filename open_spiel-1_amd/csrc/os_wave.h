@@ -41,6 +41,11 @@
 #ifndef OS_PHASE_TIMING
 #define OS_PHASE_TIMING 0
 #endif
+// Timing-only A/B switch (results not bit-exact): 1 skips the hex end-of-fill
+// relaxation, 2 the hex fill-order rank-select loop.
+#ifndef OS_AB_HEX
+#define OS_AB_HEX 0
+#endif
 
 namespace osm {
 
@@ -642,18 +647,15 @@ __device__ __forceinline__ bool in_mask(uint64_t m) {
   return __builtin_amdgcn_inverse_ballot_w64(m);
 }
 
-// Move of the fill: the k-th empty cell (ascending) of e0 (cells 0-63) / e1
-// (cells 64-127) gets fill time tau.  Lane l ranks cells l and l + 64 among
-// the empty cells by mbcnt; the empty cell whose rank is k is the move.
-__device__ __forceinline__ void hex_take(uint64_t& e0, uint64_t& e1, uint32_t k, uint32_t tau,
-                                         uint32_t& t0, uint32_t& t1) {
-  const uint32_t c0 = static_cast<uint32_t>(popc64(e0));
-  const uint64_t h0 = ballot(lanes_below(e0) == k) & e0;
-  const uint64_t h1 = ballot(lanes_below(e1) + c0 == k) & e1;
-  e0 &= ~h0;
-  e1 &= ~h1;
-  t0 = in_mask(h0) ? tau : t0;
-  t1 = in_mask(h1) ? tau : t1;
+// Move of the fill: the k-th empty cell (ascending) gets fill time tau.  r
+// holds each cell's rank among the empty cells (huge for filled or
+// off-board cells), so the move is the cell whose rank is k and the cells
+// after it move down one rank -- both are "r > k", since ranks follow cell
+// order.  Vector-only: no scalar mask per move.
+__device__ __forceinline__ void hex_take(uint32_t& r, uint32_t k, uint32_t tau, uint32_t& t) {
+  const bool hit = r == k;
+  t = hit ? tau : t;
+  r = hit ? 0x40000000u : r - (r > k ? 1u : 0u);
 }
 
 // hex random playout (mcts.cc:46-55), lane-parallel.  Hex only ever fills
@@ -712,13 +714,29 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
     else k1 = k;
   }
   if (ballot(risky)) return kLanesDecline;
-  // Fill times of cells l (t0) and l + 64 (t1).
-  uint64_t e0 = empty.lo, e1 = empty.hi;
+  // Fill times of cells l (t0) and l + 64 (t1); ranks among the empty cells.
   uint32_t t0 = 0, t1 = 0;
+  uint32_t r0 = ((empty.lo >> l) & 1) ? lanes_below(empty.lo) : 0x40000000u;
+  uint32_t r1 = ((empty.hi >> l) & 1) ? lanes_below(empty.hi) + popc64(empty.lo) : 0x40000000u;
   const int nlo = n0 < 64 ? n0 : 64;
-  for (int j = 0; j < nlo; ++j) hex_take(e0, e1, rl32(k0, j), static_cast<uint32_t>(j + 1), t0, t1);
-  for (int j = 64; j < n0; ++j)
-    hex_take(e0, e1, rl32(k1, j - 64), static_cast<uint32_t>(j + 1), t0, t1);
+#if OS_AB_HEX == 2  // timing A/B only: fill order = cell order
+  t0 = l < n0 ? l + 1 : 0;
+  t1 = l + 64 < n0 ? l + 65 : 0;
+  if (n0 < 0)
+#endif
+  for (int j = 0; j < nlo; ++j) {
+    const uint32_t k = rl32(k0, j);
+    hex_take(r0, k, static_cast<uint32_t>(j + 1), t0);
+    hex_take(r1, k, static_cast<uint32_t>(j + 1), t1);
+  }
+#if OS_AB_HEX == 2
+  if (n0 < 0)
+#endif
+  for (int j = 64; j < n0; ++j) {
+    const uint32_t k = rl32(k1, j - 64);
+    hex_take(r0, k, static_cast<uint32_t>(j + 1), t0);
+    hex_take(r1, k, static_cast<uint32_t>(j + 1), t1);
+  }
   // Per cell: colour (stones already placed by the state, move j by the
   // player to move ^ (j & 1)), near / far edge (hex.cc:55-90: black north row
   // -> south row, white west column -> east column), column.
@@ -770,6 +788,9 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
     const uint32_t diff = __builtin_amdgcn_perm(r, r, sel[i]) ^ own;  // 0 / 1 per half
     cut[i] = (diff * 0xFFFFu) | (xa ? 0xFFFFu : 0u) | (xb ? 0xFFFF0000u : 0u);
   }
+#if OS_AB_HEX == 1  // timing A/B only: no relaxation
+  if (n0 < 0)
+#endif
   for (;;) {
     uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
