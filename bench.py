@@ -170,17 +170,24 @@ def _roofline(kernel, game, alg_bytes, kernel_ms, units, unit_name):
 
 
 def _issue_roofline(kernel, game, units, kernel_ms):
-  """The bound that does apply: scalar-instruction issue.  One
-  CU issues at most one SALU instruction per clock; SALU instructions per unit
-  come from the committed PMC summary of this kernel (SQ_INSTS_SALU per sim),
-  the rate from this run's live kernel time."""
-  per = pmc_per_unit(kernel, game, "SQ_INSTS_SALU")
-  if per is None:
-    return None
-  rate = per * units / (kernel_ms / 1e3)
-  peak = N_CUS * CLOCK_HZ
-  return {"bound": "salu-issue", "salu_per_unit": per, "achieved": rate / 1e9,
-          "peak": peak / 1e9, "unit": "G SALU instr/s", "frac": rate / peak}
+  """The bound that does apply: instruction issue.  One CU
+  issues at most one SALU instruction per clock and, over its four SIMDs, two
+  wave64 VALU instructions per clock (each takes 2 cycles on its SIMD).
+  Instructions per unit come from the committed PMC summary of this kernel
+  (SQ_INSTS_SALU / SQ_INSTS_VALU per sim), the rate from this run's live kernel
+  time; `bound` names whichever pipe is closer to its peak."""
+  out = {}
+  for pipe, counter, per_clock in (("salu", "SQ_INSTS_SALU", 1.0),
+                                   ("valu", "SQ_INSTS_VALU", 2.0)):
+    per = pmc_per_unit(kernel, game, counter)
+    if per is None:
+      return None
+    rate = per * units / (kernel_ms / 1e3)
+    peak = N_CUS * CLOCK_HZ * per_clock
+    out[pipe] = {"per_unit": per, "achieved": rate / 1e9, "peak": peak / 1e9,
+                 "unit": "G instr/s", "frac": rate / peak}
+  top = max(out, key=lambda p: out[p]["frac"])
+  return dict(out, bound="%s-issue" % top, frac=out[top]["frac"])
 
 
 # ---------------------------------------------------------------------------
