@@ -496,7 +496,7 @@ def pmc_traffic(kernel, game):
     return None
   with open(path) as f:
     d = json.load(f)
-  return d.get("%s/%s" % (kernel, game), {}).get("hbm_bytes_per_launch")
+  return d.get("%s/%s" % (kernel, game.split("(")[0]), {}).get("hbm_bytes_per_launch")
 
 
 def pmc_per_unit(kernel, game, counter):
@@ -505,7 +505,7 @@ def pmc_per_unit(kernel, game, counter):
     return None
   with open(path) as f:
     d = json.load(f)
-  return d.get("%s/%s" % (kernel, game), {}).get("per_sim", {}).get(counter)
+  return d.get("%s/%s" % (kernel, game.split("(")[0]), {}).get("per_sim", {}).get(counter)
 
 
 if __name__ == "__main__":
