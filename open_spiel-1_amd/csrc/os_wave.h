@@ -1020,31 +1020,41 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         const int cp = P0 ^ (depth & 1);
         c_scanned.add(cur_nc);
         Node<R> c0 = zero_node, c1 = zero_node;
-        double v0 = -inf, v1 = -inf, lg0 = 0.0, lg1 = 0.0;
+        double lg0 = 0.0, lg1 = 0.0;
+        const bool in0 = l < cur_nc, in1 = WW::kTwoSlots && l + 64 < cur_nc;
         if (depth == 0) {  // root children: register-resident, no loads
-          if (l < cur_nc) {
+          if (in0) {
             c0 = rc0;
             lg0 = rlg0;
-            v0 = uct_value(c0, cp, cur_logN, sp.uct_c);
           }
-          if (WW::kTwoSlots && l + 64 < cur_nc) {
+          if (in1) {
             c1 = rc1;
             lg1 = rlg1;
-            v1 = uct_value(c1, cp, cur_logN, sp.uct_c);
           }
         } else {
-          if (l < cur_nc) {
+          if (in0) {
             c0 = nodes[cur_first + l];
             lg0 = sp.log_lut[c0.n];
-            v0 = uct_value(c0, cp, cur_logN, sp.uct_c);
           }
-          if (WW::kTwoSlots && l + 64 < cur_nc) {
+          if (in1) {
             c1 = nodes[cur_first + l + 64];
             lg1 = sp.log_lut[c1.n];
-            v1 = uct_value(c1, cp, cur_logN, sp.uct_c);
           }
         }
-        chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
+        // An unvisited unsolved child scores +inf, above every finite UCT
+        // value and solver outcome, so the first one in index order wins the
+        // strict '>' scan outright: one ballot instead of the f64 UCT values
+        // and the wave max.
+        const uint64_t f0 = ballot(in0 && c0.out == kUnsolved && c0.n == 0);
+        const uint64_t f1 =
+            WW::kTwoSlots ? ballot(in1 && c1.out == kUnsolved && c1.n == 0) : 0ull;
+        if (f0 | f1) {
+          chosen = f0 ? ctz64(f0) : 64 + ctz64(f1);
+        } else {
+          const double v0 = in0 ? uct_value(c0, cp, cur_logN, sp.uct_c) : -inf;
+          const double v1 = in1 ? uct_value(c1, cp, cur_logN, sp.uct_c) : -inf;
+          chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
+        }
         if (depth == 0) root_k = chosen;
         const int src = chosen & 63;
         const bool hi = WW::kTwoSlots && chosen >= 64;  // wave-uniform
