@@ -19,10 +19,20 @@ already resident in HBM).  Rank 0 prints ONE JSON line.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+`--gpus N` (N > 1) without a torch.distributed environment starts the N rank
+processes itself (torch.distributed.run as a child process, before anything
+touches the GPU) and exits with its status; with WORLD_SIZE set, N must equal
+it.  `--rehearse-host` is for the CPU test-suite only: the same rank/seed
+assignment and all-reduces under gloo, with a host-compiled engine from
+tests/ (never a measurement; its line says so).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -67,7 +77,29 @@ def parse():
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
                   help="target CPU-baseline sample duration")
   ap.add_argument("--parity-roots", type=int, default=32)
+  ap.add_argument("--rehearse-host", action="store_true",
+                  help="CPU test-suite rehearsal of the rank plumbing (gloo, host "
+                       "engine from tests/); not a measurement")
   return ap.parse_args()
+
+
+def _free_port():
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    return s.getsockname()[1]
+
+
+def launch_ranks(args):
+  """--gpus N > 1 outside torch.distributed: run N ranks of this script under
+  torch.distributed.run (one process per GPU) as a CHILD process and return
+  its exit status.  Nothing here touches the GPU, so the parent never holds a
+  device context (no exec from a GPU-initialised process)."""
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+         "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+         "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+  env = dict(os.environ)
+  env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+  return subprocess.call(cmd, env=env)
 
 
 class Ctx:
@@ -80,49 +112,89 @@ class Ctx:
     self.world = int(os.environ.get("WORLD_SIZE", "1"))
     self.rank = int(os.environ.get("RANK", "0"))
     self.local = int(os.environ.get("LOCAL_RANK", "0"))
-    if self.world != args.gpus and self.world > 1:
-      raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, self.world))
+    if self.world != args.gpus:
+      raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, self.world))
+    self.rehearse = args.rehearse_host
+    if self.rehearse:  # CPU test-suite: gloo + host engine, no GPU call
+      self.dev = torch.device("cpu")
+      self.stream = None
+      if self.world > 1:
+        dist.init_process_group("gloo")
+      return
+    self.dev = torch.device("cuda", self.local)
     torch.cuda.set_device(self.local)
     if self.world > 1:
-      dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+      dist.init_process_group("nccl", device_id=self.dev)
     self.stream = torch.cuda.current_stream()
+
+  @property
+  def handle(self):
+    return None if self.stream is None else self.stream.cuda_stream
+
+  def engine(self, game):
+    """The search engine of this rank: libos_mcts.so on this rank's GPU."""
+    if self.rehearse:
+      sys.path.insert(0, os.path.join(ROOT, "tests"))
+      import bench_rehearsal
+      return bench_rehearsal.HostEngine(game)
+    from os_amd import engine as E
+    return E.Engine(game, device=self.local)
+
+  def backend(self, game):
+    from os_amd import dist as D
+    if self.rehearse:
+      return D.HipBackend(game, engine=self.engine(game))
+    return D.HipBackend(game, self.local)
 
   def barrier(self):
     if self.world > 1:
       self.dist.barrier()
 
+  def sync(self):
+    if not self.rehearse:
+      self.torch.cuda.synchronize()
+
   def timed(self, step, steps):
-    """Barrier + sync, K steps, sync + barrier; (wall max over ranks, event ms)."""
+    """Barrier + sync, K steps, sync + barrier; (wall max over ranks, event ms).
+
+    The events are recorded on the stream the kernels are launched on."""
     torch = self.torch
     self.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    self.sync()
+    if not self.rehearse:
+      ev0 = torch.cuda.Event(enable_timing=True)
+      ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(self.stream)
+    if not self.rehearse:
+      ev0.record(self.stream)
     for _ in range(steps):
       step()
-    ev1.record(self.stream)
-    torch.cuda.synchronize()
+    if not self.rehearse:
+      ev1.record(self.stream)
+    self.sync()
     self.barrier()
     elapsed = time.perf_counter() - t0
     if self.world > 1:
-      t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+      t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
       self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
       elapsed = float(t.item())
+    if self.rehearse:
+      return elapsed, elapsed * 1e3 / max(steps, 1)
     return elapsed, ev0.elapsed_time(ev1) / max(steps, 1)
 
   def total(self, x):
     """Sum of a per-rank count over all ranks."""
     if self.world == 1:
       return x
-    t = self.torch.tensor([float(x)], dtype=self.torch.float64, device="cuda")
+    t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.dev)
     self.dist.all_reduce(t)
     return float(t.item())
 
 
 def main():
   args = parse()
+  if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    sys.exit(launch_ranks(args))
   ctx = Ctx(args)
   from os_amd import _lib
   layouts = {"auto": _lib.LAYOUT_AUTO, "wave": _lib.LAYOUT_WAVE, "lane": _lib.LAYOUT_LANE}
@@ -131,6 +203,9 @@ def main():
         "playouts": bench_playouts, "selfplay": bench_selfplay}[mode]
   line = fn(args, ctx, layouts[args.layout])
   if ctx.rank == 0:
+    if ctx.rehearse:
+      line["data"] = "REHEARSAL: host-compiled engine under gloo (tests only, not a measurement)"
+      line["roofline"] = None
     print(json.dumps(line), flush=True)
   if ctx.world > 1:
     ctx.dist.destroy_process_group()
@@ -158,28 +233,40 @@ def _base_line(args, ctx, metric, value, unit, elapsed, config):
 
 
 def _roofline(kernel, game, alg_bytes, kernel_ms, units, unit_name):
+  """HBM roofline of the dominant kernel (the contract's bound/achieved/peak/
+  frac/traffic), plus the instruction-issue roofline that actually binds these
+  integer kernels, named in `binding`."""
   achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+  pmc = pmc_record(kernel, game)
+  issue = _issue_roofline(pmc, units, kernel_ms)
+  hbm_frac = achieved / HBM_PEAK_GBS
+  binding = ("hbm" if issue is None or hbm_frac >= issue["frac"] else issue["bound"])
   return {
       "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(kernel, game),
+      "frac": hbm_frac, "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+      "binding": binding,
+      "binding_frac": hbm_frac if binding == "hbm" else issue["frac"],
       "kernel": kernel, "kernel_ms_per_launch": kernel_ms,
       "algorithmic_bytes_per_launch": alg_bytes,
       "algorithmic_bytes_per_%s" % unit_name: alg_bytes / max(units, 1),
-      "issue": _issue_roofline(kernel, game, units, kernel_ms),
+      "issue": issue,
+      "pmc_source": _pmc_provenance(pmc),
   }
 
 
-def _issue_roofline(kernel, game, units, kernel_ms):
+def _issue_roofline(pmc, units, kernel_ms):
   """The bound that does apply: instruction issue.  One CU
   issues at most one SALU instruction per clock and, over its four SIMDs, two
   wave64 VALU instructions per clock (each takes 2 cycles on its SIMD).
   Instructions per unit come from the committed PMC summary of this kernel
   (SQ_INSTS_SALU / SQ_INSTS_VALU per sim), the rate from this run's live kernel
   time; `bound` names whichever pipe is closer to its peak."""
+  if not pmc:
+    return None
   out = {}
   for pipe, counter, per_clock in (("salu", "SQ_INSTS_SALU", 1.0),
                                    ("valu", "SQ_INSTS_VALU", 2.0)):
-    per = pmc_per_unit(kernel, game, counter)
+    per = pmc.get("per_sim", {}).get(counter)
     if per is None:
       return None
     rate = per * units / (kernel_ms / 1e3)
@@ -205,9 +292,9 @@ def bench_search(args, ctx, layout):
   gid = np.arange(base, base + R, dtype=np.uint32)
   bot_seeds, eval_seeds = gid, gid + np.uint32(EVAL_OFFSET)
 
-  eng = E.Engine(game, device=ctx.local)
+  eng = ctx.engine(game)
   eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
-  handle = ctx.stream.cuda_stream
+  handle = ctx.handle
   for _ in range(args.warmup):
     eng.run_async(handle)
   out = eng.fetch()  # synchronises; validates per-root status
@@ -262,7 +349,7 @@ def bench_root_parallel(args, ctx, layout):
   params = dict(uct_c=2.0, max_simulations=sims, n_rollouts=1, max_memory_mb=1000,
                 solve=True, block_size=args.block, arena_nodes=args.arena_nodes,
                 layout=layout)
-  be = D.HipBackend(game, ctx.local)
+  be = ctx.backend(game)
   ids = np.arange(ctx.rank * T, (ctx.rank + 1) * T, dtype=np.uint32)
   be.prepare_root_parallel([], ids, ids + np.uint32(EVAL_OFFSET), **params)
   torch = ctx.torch
@@ -285,7 +372,7 @@ def bench_root_parallel(args, ctx, layout):
   for r in range(T):
     for k in range(int(out["nchild"][r])):
       local_v[out["child_action"][r, k]] += out["child_n"][r, k]
-  lv = torch.from_numpy(local_v).cuda()
+  lv = torch.from_numpy(local_v).to(ctx.dev)
   if ctx.world > 1:
     ctx.dist.all_reduce(lv)
   reduce_ok = bool(torch.equal(lv, v))
@@ -339,7 +426,7 @@ def bench_playouts(args, ctx, layout):
   N = args.roots or N
   start, count = D.shard(N, ctx.world, ctx.rank)
   seeds = np.arange(start, start + count, dtype=np.uint32)
-  be = D.HipBackend(game, ctx.local)
+  be = ctx.backend(game)
   be.prepare_playouts([], seeds)
 
   def step():
@@ -353,7 +440,7 @@ def bench_playouts(args, ctx, layout):
   returns = be.eng.rollouts_fetch()
   ret0 = returns[:, 0]
   local = np.array([(ret0 > 0).sum(), (ret0 < 0).sum(), (ret0 == 0).sum()], np.int64)
-  lc = ctx.torch.from_numpy(local).cuda()
+  lc = ctx.torch.from_numpy(local).to(ctx.dev)
   if ctx.world > 1:
     ctx.dist.all_reduce(lc)
   parity = None
@@ -395,11 +482,11 @@ def bench_selfplay(args, ctx, layout):
   gid = np.arange(base, base + G, dtype=np.uint32)
   bot = np.stack([2 * gid, 2 * gid + 1], axis=1).astype(np.uint32)
   ev = gid + np.uint32(EVAL_OFFSET)
-  eng = E.Engine(game, device=ctx.local)
+  eng = E.Engine(game, device=ctx.local)  # self-play: GPU only
   L = eng.max_game_length
   eng.selfplay_prepare(acts, offs, bot, ev, max_len=L, record_visits=True,
                        max_simulations=sims, uct_c=2.0)
-  handle = ctx.stream.cuda_stream
+  handle = ctx.handle
   for _ in range(args.warmup):
     eng.selfplay_run_async(handle)
   out = eng.selfplay_fetch()
@@ -444,28 +531,56 @@ def _oracle(game):
   return oracle_lib.Game(game)
 
 
+CALIBRATION = ("uncalibrated restatement: the reference mcts.cc cannot be built "
+               "here (abseil absent), so no reference/restatement speed ratio exists")
+
+
+def host_cores():
+  """CPUs this process may actually run on: the affinity mask, capped by the
+  cgroup CPU quota when one is set (a GPU box shares its host; nproc there
+  shows the whole machine).  Returns (threads, description)."""
+  aff = len(os.sched_getaffinity(0))
+  quota = None
+  try:
+    with open("/sys/fs/cgroup/cpu.max") as f:
+      q, period = f.read().split()
+    if q != "max":
+      quota = max(1, int(int(q) // int(period)))
+  except (OSError, ValueError):
+    pass
+  threads = aff if quota is None else min(aff, quota)
+  desc = "nproc %d, affinity %d, cgroup quota %s -> %d threads" % (
+      os.cpu_count() or 0, aff, "none" if quota is None else "%d CPUs" % quota, threads)
+  return threads, desc
+
+
 def cpu_baseline_search(game, acts, offs, bot_seeds, eval_seeds, sims, seconds):
-  """Oracle (reference-faithful restatement, "port") on the host cores."""
+  """Oracle (reference-faithful restatement, "port") on every usable host core;
+  the batch (or a prefix of it) is repeated until >= `seconds` are timed."""
   og = _oracle(game)
-  threads = max(1, min(16, len(os.sched_getaffinity(0))))
+  threads, cores_desc = host_cores()
   R = len(offs) - 1
-  # Calibrate on a small prefix, then size the sample to ~`seconds`.
+  # Calibrate on a small prefix, then size one pass to ~`seconds` (<= R roots).
   probe = min(R, 2 * threads)
   secs, n = og.time_mcts_batch(acts[:offs[probe]], offs[:probe + 1], bot_seeds[:probe],
                                eval_seeds[:probe], max_simulations=sims, threads=threads)
   per_root = max(secs, 1e-9) / probe * threads  # seconds per root on one thread
   want = int(min(R, max(probe, seconds * threads / per_root)))
-  secs, n = og.time_mcts_batch(acts[:offs[want]], offs[:want + 1], bot_seeds[:want],
-                               eval_seeds[:want], max_simulations=sims, threads=threads)
-  return {"value": n / secs, "unit": "sims/s", "cores": threads, "kind": "port",
-          "sample": "%d of the %d roots x %d sims (%d sims, %.1f s), oracle "
-                    "restatement of mcts.cc, %d threads" %
-                    (want, R, sims, n, secs, threads)}
+  total_s, total_n, passes = 0.0, 0, 0
+  while total_s < seconds or passes == 0:
+    secs, n = og.time_mcts_batch(acts[:offs[want]], offs[:want + 1], bot_seeds[:want],
+                                 eval_seeds[:want], max_simulations=sims, threads=threads)
+    total_s, total_n, passes = total_s + secs, total_n + n, passes + 1
+  return {"value": total_n / total_s, "unit": "sims/s", "cores": threads, "kind": "port",
+          "calibration": CALIBRATION,
+          "sample": "%d pass(es) over %d of the %d roots x %d sims (%d sims, %.1f s), "
+                    "oracle restatement of mcts.cc; %s" %
+                    (passes, want, R, sims, total_n, total_s, cores_desc)}
 
 
 def cpu_baseline_playouts(game, seconds):
   """Oracle RandomRolloutEvaluator::Evaluate on host threads (ctypes drops the GIL)."""
-  threads = max(1, min(16, len(os.sched_getaffinity(0))))
+  threads, cores_desc = host_cores()
   t0 = time.perf_counter()
   _oracle(game).rollouts([], np.arange(64, dtype=np.uint32))
   per = (time.perf_counter() - t0) / 64
@@ -483,29 +598,41 @@ def cpu_baseline_playouts(game, seconds):
     t.join()
   secs = time.perf_counter() - t0
   return {"value": threads * n_per / secs, "unit": "playouts/s", "cores": threads,
-          "kind": "port", "sample": "%d playouts (seeds 0..%d) on %d threads, %.1f s, "
-          "oracle restatement of RandomRolloutEvaluator" % (threads * n_per,
-                                                           threads * n_per - 1, threads, secs)}
+          "kind": "port", "calibration": CALIBRATION,
+          "sample": "%d playouts (seeds 0..%d), %.1f s, oracle restatement of "
+                    "RandomRolloutEvaluator; %s" % (threads * n_per, threads * n_per - 1,
+                                                    secs, cores_desc)}
 
 
-def pmc_traffic(kernel, game):
-  """HBM bytes per launch of `kernel` on `game` from the committed rocprofv3
-  PMC summary (profiles/pmc_traffic.json, written by tools/pmc_summary.py)."""
+def kernel_source_hash():
+  """sha256 over the kernel sources (csrc/*): ties a PMC record to the code
+  it was collected on (tools/pmc_summary.py stores the same hash)."""
+  h = hashlib.sha256()
+  src = os.path.join(ROOT, "open_spiel-1_amd", "csrc")
+  for name in sorted(os.listdir(src)):
+    if name.endswith((".h", ".hip", ".cpp")):
+      with open(os.path.join(src, name), "rb") as f:
+        h.update(name.encode() + b"\0" + f.read())
+  return h.hexdigest()[:16]
+
+
+def pmc_record(kernel, game):
+  """rocprofv3 PMC summary of `kernel` on `game` (profiles/pmc_traffic.json,
+  written by tools/pmc_summary.py), or None."""
   path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
   if not os.path.exists(path):
     return None
   with open(path) as f:
     d = json.load(f)
-  return d.get("%s/%s" % (kernel, game.split("(")[0]), {}).get("hbm_bytes_per_launch")
+  return d.get("%s/%s" % (kernel, game.split("(")[0]))
 
 
-def pmc_per_unit(kernel, game, counter):
-  path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-  if not os.path.exists(path):
+def _pmc_provenance(pmc):
+  if not pmc:
     return None
-  with open(path) as f:
-    d = json.load(f)
-  return d.get("%s/%s" % (kernel, game.split("(")[0]), {}).get("per_sim", {}).get(counter)
+  src = pmc.get("source_hash")
+  return {"source_hash": src, "current_source_hash": kernel_source_hash(),
+          "stale": src != kernel_source_hash()}
 
 
 if __name__ == "__main__":

@@ -1,23 +1,32 @@
-"""Bot-vs-bot game loop (python/algorithms/evaluate_bots.py:24-49 semantics)."""
+"""`evaluate_bots(state, bots, rng)`: plays one game between `bots` from
+`state` and returns the final returns (API of the reference
+python/algorithms/evaluate_bots.py:24-49).
+
+Every bot is restarted at `state`; on each turn the mover's `step` picks the
+action (a chance node samples from `rng` instead, mover = PlayerId.CHANCE) and
+every other bot is told the action through `inform_action` before it is
+applied.
+"""
 from os_amd import pyspiel
 
 
+def _choose(state, bots, rng):
+  """(mover, action) for the current node."""
+  if state.is_chance_node():
+    outcomes = state.chance_outcomes()
+    pick = rng.choice(len(outcomes), p=[p for _, p in outcomes])
+    return pyspiel.PlayerId.CHANCE, outcomes[pick][0]
+  mover = state.current_player()
+  return mover, bots[mover].step(state)
+
+
 def evaluate_bots(state, bots, rng):
-  """Plays `bots` against each other from `state`; returns the returns."""
   for bot in bots:
     bot.restart_at(state)
   while not state.is_terminal():
-    if state.is_chance_node():
-      outcomes, probs = zip(*state.chance_outcomes())
-      action = rng.choice(outcomes, p=probs)
-      for bot in bots:
-        bot.inform_action(state, pyspiel.PlayerId.CHANCE, action)
-      state.apply_action(action)
-      continue
-    mover = state.current_player()
-    action = bots[mover].step(state)
-    for i, bot in enumerate(bots):
-      if i != mover:
+    mover, action = _choose(state, bots, rng)
+    for seat, bot in enumerate(bots):
+      if seat != mover:
         bot.inform_action(state, mover, action)
     state.apply_action(action)
   return state.returns()

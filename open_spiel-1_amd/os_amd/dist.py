@@ -121,17 +121,27 @@ def sharded_playouts(backend, history, total, group=None, n_rollouts=1):
 
 
 class HipBackend:
-  """libos_mcts.so on one GPU; results stay in HBM until the collective."""
+  """libos_mcts.so on one GPU; results stay in HBM until the collective.
 
-  def __init__(self, game_string, device=0):
+  `engine` replaces the device engine only in the CPU rehearsal of bench.py
+  (tests/bench_rehearsal.py); then tensors live on the CPU for gloo.
+  """
+
+  def __init__(self, game_string, device=0, engine=None):
     import torch
     from . import engine as E
     self.torch = torch
-    self.eng = E.Engine(game_string, device)
-    self.device = torch.device("cuda", device)
+    if engine is None:
+      self.eng = E.Engine(game_string, device)
+      self.device = torch.device("cuda", device)
+    else:
+      self.eng = engine
+      self.device = torch.device("cpu")
     self.num_actions = self.eng.num_distinct_actions
 
   def _stream(self):
+    if self.device.type != "cuda":
+      return None
     return self.torch.cuda.current_stream(self.device).cuda_stream
 
   def search(self, acts, offs, bot_seeds, eval_seeds, **params):

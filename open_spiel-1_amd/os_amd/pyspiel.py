@@ -61,35 +61,48 @@ class GameType:
     REWARDS = 0
     TERMINAL = 1
 
-  def __init__(self, short_name, long_name, parameter_specification,
-               provides_information_state_string=True):
+  def __init__(self, short_name, long_name, dynamics, chance_mode, information,
+               utility, reward_model, max_num_players, min_num_players,
+               provides_information_state_string, provides_information_state_tensor,
+               provides_observation_string, provides_observation_tensor,
+               parameter_specification):
+    """Keyword names and order of the pybind constructor (pyspiel.cc:218-229),
+    so Python-defined games (python/games/tic_tac_toe.py:293-307) build theirs."""
     self.short_name = short_name
     self.long_name = long_name
-    self.dynamics = GameType.Dynamics.SEQUENTIAL
-    self.chance_mode = GameType.ChanceMode.DETERMINISTIC
-    self.information = GameType.Information.PERFECT_INFORMATION
-    self.utility = GameType.Utility.ZERO_SUM
-    self.reward_model = GameType.RewardModel.TERMINAL
-    self.max_num_players = 2
-    self.min_num_players = 2
+    self.dynamics = dynamics
+    self.chance_mode = chance_mode
+    self.information = information
+    self.utility = utility
+    self.reward_model = reward_model
+    self.max_num_players = max_num_players
+    self.min_num_players = min_num_players
     self.provides_information_state_string = provides_information_state_string
-    self.provides_information_state_tensor = False
-    self.provides_observation_string = True
-    self.provides_observation_tensor = True
-    self.parameter_specification = parameter_specification
+    self.provides_information_state_tensor = provides_information_state_tensor
+    self.provides_observation_string = provides_observation_string
+    self.provides_observation_tensor = provides_observation_tensor
+    self.parameter_specification = dict(parameter_specification)
     self.default_loadable = True
 
   def __repr__(self):
     return "<GameType '%s'>" % self.short_name
 
 
+def _two_player_type(short_name, long_name, params, info_string=True):
+  return GameType(short_name, long_name, GameType.Dynamics.SEQUENTIAL,
+                  GameType.ChanceMode.DETERMINISTIC,
+                  GameType.Information.PERFECT_INFORMATION,
+                  GameType.Utility.ZERO_SUM, GameType.RewardModel.TERMINAL, 2, 2,
+                  info_string, False, True, True, params)
+
+
 _TYPES = {
-    0: GameType("tic_tac_toe", "Tic Tac Toe", {}),
-    1: GameType("connect_four", "Connect Four", {}),
-    2: GameType("breakthrough", "Breakthrough", {"rows": 8, "columns": 8},
-                provides_information_state_string=False),
-    3: GameType("hex", "Hex", {"board_size": 11}),
-    4: GameType("go", "Go", {"komi": 7.5, "board_size": 19, "handicap": 0}),
+    0: _two_player_type("tic_tac_toe", "Tic Tac Toe", {}),
+    1: _two_player_type("connect_four", "Connect Four", {}),
+    2: _two_player_type("breakthrough", "Breakthrough", {"rows": 8, "columns": 8},
+                        info_string=False),
+    3: _two_player_type("hex", "Hex", {"board_size": 11}),
+    4: _two_player_type("go", "Go", {"komi": 7.5, "board_size": 19, "handicap": 0}),
 }
 
 

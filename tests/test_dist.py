@@ -187,3 +187,60 @@ def test_gpu_playout_counts(require_gpu):
   r = oracle_lib.Game("go(board_size=9)").rollouts(
       [], np.arange(seeds_total, dtype=np.uint32))[:, 0]
   assert c.cpu().tolist() == [(r > 0).sum(), (r < 0).sum(), (r == 0).sum()]
+
+
+# ---------------------------------------------------------------------------
+# bench.py's own multi-rank path (launcher, rank/seed assignment, all-reduces),
+# rehearsed on the CPU: `--gpus 2` spawns two ranks under torch.distributed.run,
+# `--rehearse-host` swaps gloo + the host-compiled engine in for RCCL + the GPU.
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+
+
+def _bench(*args, env=None):
+  import json
+  import subprocess
+  import sys
+  e = dict(os.environ)
+  e.pop("WORLD_SIZE", None)
+  e.update(env or {})
+  p = subprocess.run([sys.executable, BENCH, "--rehearse-host", "--steps", "1", "--warmup",
+                      "1", "--no-cpu-baseline"] + list(args),
+                     capture_output=True, text=True, timeout=600, env=e)
+  lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+  return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_gpus2_spawns_ranks_root_parallel():
+  rc, line, err = _bench("--gpus", "2", "--config", "c4", "--roots", "3", "--sims",
+                         str(SIMS), "--parity-roots", "3")
+  assert rc == 0, err[-2000:]
+  assert line["n_gpus"] == 2 and line["data"].startswith("REHEARSAL")
+  assert line["parity"]["bit_exact"] and line["parity"]["allreduce_equals_sum_of_trees"]
+  # rank g grew trees g*3 .. g*3+2: the all-reduced visits are those of 6 trees.
+  ov, _ = _oracle_root_parallel("hex(board_size=11)", [], 6, SIMS)
+  top = sorted(((int(n), a) for a, n in enumerate(ov.tolist())), reverse=True)[:5]
+  assert [tuple(x) for x in line["root_visits_top5"]] == top
+
+
+def test_bench_gpus2_spawns_ranks_playouts():
+  rc, line, err = _bench("--gpus", "2", "--config", "c5", "--roots", "9")
+  assert rc == 0, err[-2000:]
+  assert line["n_gpus"] == 2 and line["parity"]["counts_equal_returns"]
+  r = oracle_lib.Game("go(board_size=9)").rollouts([], np.arange(9, dtype=np.uint32))[:, 0]
+  o = line["outcomes"]
+  assert [o["p0_wins"], o["p1_wins"], o["draws"]] == \
+      [int((r > 0).sum()), int((r < 0).sum()), int((r == 0).sum())]
+
+
+def test_bench_gpus2_spawns_ranks_search():
+  rc, line, err = _bench("--gpus", "2", "--config", "c2", "--roots", "4", "--sims",
+                         str(SIMS), "--parity-roots", "4")
+  assert rc == 0, err[-2000:]
+  assert line["n_gpus"] == 2 and line["parity"]["bit_exact"]
+  assert "dp2" in line["config"]["parallelism"]
+
+
+def test_bench_rejects_world_size_mismatch():
+  rc, line, err = _bench("--gpus", "2", "--config", "c2", "--roots", "2", "--sims", "8",
+                         env={"WORLD_SIZE": "1"})
+  assert rc != 0 and line is None and "WORLD_SIZE" in err

@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Generates tests/golden/python_mcts_<game>.json by running the UNMODIFIED
+reference `open_spiel/python/algorithms/mcts.py` (and, for tic_tac_toe, the
+reference pure-Python game `open_spiel/python/games/tic_tac_toe.py`).
+
+Run in the build container only (it reads /root/reference, which does not
+exist on the GPU box); the JSON it writes is data: inputs and the reference's
+outputs, no reference source.
+
+    python tools/gen_python_mcts_goldens.py [--reference /root/reference]
+
+How the reference runs here:
+  * `import pyspiel` inside the reference module resolves to this repo's
+    drop-in (`open_spiel-1_amd/pyspiel.py` -> `os_amd.pyspiel`), which provides
+    every name mcts.py uses (`Bot`, `GameType`, `PlayerId`; mcts.py:26,199,
+    241-245,410,415).  No stub module is involved.
+  * The reference module's own `RandomRolloutEvaluator` and `MCTSBot` classes
+    run the search on the host (mcts.py:46-82, 199-443): every state operation
+    goes through `os_amd.pyspiel.State` (the host C++ game code in
+    libos_mcts.so; no GPU is used or needed).
+  * tic_tac_toe is also searched on the reference's pure-Python game, which
+    does not touch this repo's game code at all; the generator asserts both
+    give the same tree.
+
+Recorded per case (mcts_test.py:41-54 style; `shared` = one RandomState for
+bot and evaluator, else bot RandomState(seed), evaluator RandomState(seed2)):
+  children in tree order: [action, explore_count, total_reward, outcome-or-None]
+  root explore_count / total_reward / outcome, best_child action,
+  each RandomState's position and a sha256 of its key after the search.
+"""
+import argparse
+import hashlib
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "open_spiel-1_amd")
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def load_module(name, path):
+  spec = importlib.util.spec_from_file_location(name, path)
+  mod = importlib.util.module_from_spec(spec)
+  spec.loader.exec_module(mod)
+  return mod
+
+
+def rs_fingerprint(rs):
+  st = rs.get_state()
+  return {"pos": int(st[2]),
+          "key_sha256": hashlib.sha256(np.asarray(st[1], np.uint32).tobytes()).hexdigest()}
+
+
+def random_history(game, plies, seed):
+  """Root position: up to `plies` uniformly random moves drawn with numpy
+  RandomState(seed); only the resulting action list is recorded."""
+  rs = np.random.RandomState(seed)
+  st = game.new_initial_state()
+  hist = []
+  for _ in range(plies):
+    if st.is_terminal():
+      break
+    a = int(rs.choice(st.legal_actions()))
+    st.apply_action(a)
+    hist.append(a)
+  return hist if not st.is_terminal() else hist[:-1]
+
+
+def run_case(mcts, game, history, seed, seed2, uct_c, sims, n_rollouts, solve):
+  st = game.new_initial_state()
+  for a in history:
+    st.apply_action(a)
+  bot_rs = np.random.RandomState(seed)
+  ev_rs = bot_rs if seed2 is None else np.random.RandomState(seed2)
+  bot = mcts.MCTSBot(game, uct_c, max_simulations=sims, solve=solve,
+                     random_state=bot_rs,
+                     evaluator=mcts.RandomRolloutEvaluator(n_rollouts=n_rollouts,
+                                                           random_state=ev_rs))
+  t0 = time.time()
+  root = bot.mcts_search(st)
+  secs = time.time() - t0
+  out = lambda o: None if o is None else [float(x) for x in o]
+  rec = {
+      "history": [int(a) for a in history], "seed": seed, "seed2": seed2,
+      "shared": seed2 is None, "uct_c": uct_c, "max_simulations": sims,
+      "n_rollouts": n_rollouts, "solve": solve,
+      "root": {"player": int(root.player), "explore_count": int(root.explore_count),
+               "total_reward": float(root.total_reward), "outcome": out(root.outcome)},
+      "children": [[int(c.action), int(c.explore_count), float(c.total_reward),
+                    out(c.outcome)] for c in root.children],
+      "best_action": int(root.best_child().action),
+      "bot_rng_after": rs_fingerprint(bot_rs),
+      "eval_rng_after": None if seed2 is None else rs_fingerprint(ev_rs),
+  }
+  return rec, secs
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--reference", default="/root/reference")
+  ap.add_argument("--only", default="")
+  args = ap.parse_args()
+  sys.path.insert(0, PKG)
+  import pyspiel  # noqa: F401  (the drop-in; the reference module imports it)
+  ref = args.reference
+  mcts = load_module("ref_mcts_py", os.path.join(ref, "open_spiel/python/algorithms/mcts.py"))
+  assert mcts.pyspiel is sys.modules["pyspiel"]
+  pyttt = load_module("ref_py_ttt", os.path.join(ref, "open_spiel/python/games/tic_tac_toe.py"))
+
+  C = 2.0
+  plan = {
+      # game string: root positions ([] = initial, ("random", plies, seed)),
+      # shared-RandomState seeds, simulations per search
+      "tic_tac_toe": dict(
+          positions=[[]], seeds=list(range(16)) + [42], sims=1000),
+      "connect_four": dict(positions=[[], ("random", 6, 7), ("random", 12, 8)],
+                           seeds=[0, 1, 42], sims=1024),
+      "breakthrough(rows=8,columns=8)": dict(positions=[[], ("random", 10, 3)],
+                                             seeds=[0, 42], sims=400),
+      "hex(board_size=11)": dict(positions=[[], ("random", 20, 4)], seeds=[0, 42], sims=400),
+      "hex(board_size=5)": dict(positions=[[], ("random", 6, 5)], seeds=[0, 42], sims=1000),
+      "go(board_size=9)": dict(positions=[[], ("random", 15, 6)], seeds=[0, 42], sims=200),
+  }
+  for gs, p in plan.items():
+    base = gs.split("(")[0] + ("" if "(" not in gs else "_" + gs.split("=")[-1].rstrip(")"))
+    if args.only and args.only not in gs:
+      continue
+    game = pyspiel.load_game(gs)
+    cases = []
+    total = 0.0
+    for pos in p["positions"]:
+      hist = pos if isinstance(pos, list) else random_history(game, pos[1], pos[2])
+      for seed in p["seeds"]:
+        rec, secs = run_case(mcts, game, hist, seed, None, C, p["sims"], 1, True)
+        cases.append(rec)
+        total += secs
+      # one case with two RandomStates, and one with n_rollouts=2 / solve off
+      rec, secs = run_case(mcts, game, hist, 7, 1007, C, p["sims"], 1, True)
+      cases.append(rec)
+      total += secs
+      rec, secs = run_case(mcts, game, hist, 11, None, 1.4, max(10, p["sims"] // 2), 2, False)
+      cases.append(rec)
+      total += secs
+    if gs == "tic_tac_toe":
+      # mcts_test.py:41-54 / :115-153 solver positions (10000 sims, 20 rollouts).
+      for hist in ([4, 0, 8], [4, 0, 8, 1, 2], [1, 8]):
+        rec, secs = run_case(mcts, game, hist, 42, None, 2 ** 0.5, 10000, 20, True)
+        cases.append(rec)
+        total += secs
+      # The reference pure-Python game must give identical trees.
+      pg = pyttt.TicTacToeGame()
+      for rec in cases:
+        got, _ = run_case(mcts, pg, rec["history"], rec["seed"], rec["seed2"], rec["uct_c"],
+                          rec["max_simulations"], rec["n_rollouts"], rec["solve"])
+        assert got == rec, "python_tic_tac_toe differs on %s" % rec["history"]
+    doc = {
+        "_source": "tools/gen_python_mcts_goldens.py: unmodified reference "
+                   "open_spiel/python/algorithms/mcts.py (MCTSBot, RandomRolloutEvaluator) "
+                   "run on the host; numpy %s" % np.__version__,
+        "game": gs, "cases": cases,
+    }
+    path = os.path.join(GOLD, "python_mcts_%s.json" % base)
+    with open(path, "w") as f:
+      json.dump(doc, f, separators=(",", ":"))
+    print("%-34s %3d cases %7.1f s -> %s" % (gs, len(cases), total, os.path.relpath(path, ROOT)))
+
+
+if __name__ == "__main__":
+  main()

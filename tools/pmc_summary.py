@@ -9,7 +9,10 @@ per launch as MI355X_MICROARCH.md §HBM prescribes for gfx950:
   traffic = 2 x FETCH_SIZE (reported at half the bytes of 128-B requests)
             + WRITE_SIZE, both KB -> bytes.
 The result is merged into profiles/pmc_traffic.json under "<kernel>/<game>",
-which bench.py reads for its roofline.traffic field.
+which bench.py reads for its roofline.traffic field.  The record carries the
+hash of the kernel sources it was collected on (bench.kernel_source_hash, so
+summarise right after collecting); bench.py flags the record `stale` once the
+sources change.
 """
 import collections
 import csv
@@ -45,8 +48,10 @@ def main():
       for line in open(log):
         if line.startswith("{"):
           sims = json.loads(line)["config"]["sims_per_step_per_gpu"]
+  sys.path.insert(0, ROOT)
+  import bench
   rec = {"kernel": kernel, "game": game, "sims_per_launch": sims,
-         "counters_per_launch": counters}
+         "counters_per_launch": counters, "source_hash": bench.kernel_source_hash()}
   if sims:
     rec["per_sim"] = {c: v / sims for c, v in counters.items()
                       if c.startswith("SQ_INSTS") or c in ("FETCH_SIZE", "WRITE_SIZE")}
