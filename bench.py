@@ -216,8 +216,6 @@ def _resolved_layout(game, R, layout):
   from os_amd import _lib
   if layout != _lib.LAYOUT_AUTO:
     return "wave" if layout == _lib.LAYOUT_WAVE else "lane"
-  if R >= 64 * 1024:
-    return "lane"
   return "wave"  # hex included: C++ policy, board_size 11
 
 

@@ -955,13 +955,14 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
   return OS_OK;
 }
 
-// OS_LAYOUT_AUTO: one wave per search unless the batch alone fills the chip
-// with lane-per-search waves (>= 1024 waves).  hex takes the wave layout only
-// where its playouts run lane-parallel (C++ policy, n >= 3; os_wave.h
+// OS_LAYOUT_AUTO: one wave per search.  hex takes the wave layout only where
+// its playouts run lane-parallel (C++ policy, n >= 3; os_wave.h
 // hex_rollout_lanes: 6.5e7 vs 1.4e7 sims/s at 4096 roots, profiles/r01).
+// Breakthrough at C3's 65536 roots: wave 8.3e7 vs lane 3.3e7 sims/s
+// (profiles/r02), so a large batch no longer switches to the lane layout.
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
+  (void)R;
   if (layout != OS_LAYOUT_AUTO) return layout;
-  if (R >= 64 * 1024) return OS_LAYOUT_LANE;
   if (cfg.kind == kHex)
     return policy == OS_POLICY_CPP && cfg.rows >= 3 ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
   return OS_LAYOUT_WAVE;

@@ -323,8 +323,12 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
           rv0 = static_cast<R>(r0);
           rv1 = static_cast<R>(-r0);
         } else {
+          // Every rollout starts from a clone of the leaf (mcts.cc:46-47), so
+          // go's position log is rewound to the leaf before each one.
+          const auto leaf_ctx = ctx;
           double s0 = 0.0, s1 = 0.0;
           for (int k = 0; k < sp.n_rollouts; ++k) {
+            if (k) ctx = leaf_ctx;
             const int r0 = rollout_ret0<G, Policy>(s, g, ctx, ev);
             s0 += static_cast<double>(r0);
             s1 += static_cast<double>(-r0);

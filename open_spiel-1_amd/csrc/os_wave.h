@@ -818,8 +818,86 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
   return winner == 0 ? 1 : -1;
 }
 
+// breakthrough random playout (mcts.cc:46-55) with lanes as board squares.
+// The legal set changes every move, so the moves stay serial, but each move's
+// LegalActions()[k] (breakthrough.cc:217-256: ascending action = source
+// square, then direction) is found without a scalar search: lane q holds
+// square q, and the number of legal actions from sources below q is the
+// mbcnt of the three per-direction source masks.  The source of action k is
+// the highest square with a move whose count-below is <= k (counts are
+// non-decreasing); its k - count-below picks the direction among the set
+// bits, in (left, forward, right) order.  Draws (absl or numpy), the move and
+// the win test (breakthrough.cc:306-319) stay on the scalar unit; the action
+// is never encoded, only its source / target squares are used.
+template <int Policy, class Rng>
+__device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev) {
+  s = make_uniform(s);
+  ev.uniformize();
+  const int c = g.cols;
+  const int last_row0 = (g.rows - 1) * c;  // first square of black's goal row
+  uint64_t b0 = s.pc[0], b1 = s.pc[1];
+  int p = s.to_play;
+  int winner = s.winner;
+  for (;;) {
+    if (winner >= 0 || b0 == 0 || b1 == 0) break;
+    const uint64_t mine = p ? b1 : b0, theirs = p ? b0 : b1;
+    const uint64_t E = g.board64 & ~(b0 | b1);
+    const uint64_t EO = E | theirs;
+    uint64_t L, F, R;
+    if (p == 0) {
+      L = mine & g.notcol0_64 & (EO >> (c - 1));
+      F = mine & (E >> c);
+      R = mine & g.notcollast_64 & (EO >> (c + 1));
+    } else {
+      L = mine & g.notcol0_64 & (EO << (c + 1));
+      F = mine & (E << c);
+      R = mine & g.notcollast_64 & (EO << (c - 1));
+    }
+    const uint32_t n = static_cast<uint32_t>(popc64(L) + popc64(F) + popc64(R));
+    // The topmost piece always has a diagonal move unless cols == 1, where
+    // the reference indexes an empty LegalActions(); end the playout there.
+    if (n == 0) return 0;
+    const uint32_t k = Policy == kPolicyCpp ? AbslUniform(ev, n) : NpChoice(ev, n);
+    // Legal actions from the squares below this lane.
+    uint32_t below = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(L), 0u);
+    below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(L >> 32), below);
+    below = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(F), below);
+    below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(F >> 32), below);
+    below = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(R), below);
+    below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(R >> 32), below);
+    const uint64_t cand = ballot(below <= k) & (L | F | R);
+    const int src = 63 - __builtin_clzll(cand);
+    uint32_t rem = k - rl32(below, src);
+    int o;  // 0 left, 1 forward, 2 right (direction order within a source)
+    if ((L >> src) & 1) {
+      if (rem == 0) {
+        o = 0;
+        goto chosen;
+      }
+      --rem;
+    }
+    o = ((F >> src) & 1) && rem == 0 ? 1 : 2;
+  chosen:
+    const int tgt = src + (p == 0 ? c : -c) + (o - 1);
+    const uint64_t tb = 1ull << tgt;
+    const uint64_t nm = (mine & ~(1ull << src)) | tb;
+    const uint64_t nt = theirs & ~tb;
+    b0 = p ? nt : nm;
+    b1 = p ? nm : nt;
+    if (p == 0 ? tgt >= last_row0 : tgt < c) winner = p;
+    p ^= 1;
+  }
+  if (winner == 0 || b1 == 0) return 1;
+  if (winner == 1 || b0 == 0) return -1;
+  return 0;
+}
+
 template <class G, int Policy, class Rng, class C>
 __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
+  if constexpr (std::is_same<G, Breakthrough>::value) {
+    (void)ctx;
+    return bt_rollout_wave<Policy>(s, g, ev);
+  }
   if constexpr (Policy == kPolicyCpp && SmallAbsl<G>::value) {
     if (ev.use7) return c4_rollout_lanes(s, ctx, ev);
   }
@@ -1116,8 +1194,12 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           rv0 = static_cast<R>(r0);
           rv1 = static_cast<R>(-r0);
         } else {
+          // Every rollout starts from a clone of the leaf (mcts.cc:46-47), so
+          // go's position log is rewound to the leaf before each one.
+          const auto leaf_ctx = ctx;
           double s0 = 0.0, s1 = 0.0;
           for (int k = 0; k < sp.n_rollouts; ++k) {
+            if (k) ctx = leaf_ctx;
             const int r0 = wave_rollout<G, Policy>(s, g, ctx, ev);
             s0 += static_cast<double>(r0);
             s1 += static_cast<double>(-r0);

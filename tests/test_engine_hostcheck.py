@@ -45,7 +45,8 @@ def test_cpp_policy_matches_oracle(gs, R, sims, plies):
   _check(got, ref)
 
 
-@pytest.mark.parametrize("gs", ["tic_tac_toe", "connect_four", "hex(board_size=5)"])
+@pytest.mark.parametrize("gs", ["tic_tac_toe", "connect_four", "hex(board_size=5)",
+                                "go(board_size=5,komi=0.5)"])
 @pytest.mark.parametrize("n_rollouts,solve,uct_c", [(3, True, 1.4142135623730951),
                                                     (1, False, 2.0), (2, False, 0.5)])
 def test_rollout_count_solver_and_uct_variants(gs, n_rollouts, solve, uct_c):

@@ -39,21 +39,29 @@ def _cmp(E, got, ref):
   assert not bad, bad
 
 
+# Both search kernels on every game: k_wsearch (one wave per search) and
+# k_mcts (one lane per search; its workgroup width `block` only matters there).
+LAYOUTS = [("wave", 0), ("lane", 16), ("lane", 64)]
+
+
 @pytest.mark.parametrize("gs,R,sims,plies", CASES)
-@pytest.mark.parametrize("block", [64, 16])
-def test_search_bit_exact(E, gs, R, sims, plies, block):
+@pytest.mark.parametrize("layout,block", LAYOUTS)
+def test_search_bit_exact(E, gs, R, sims, plies, layout, block):
+  from os_amd import _lib
   eng = E.Engine(gs)
   acts, offs = E.make_roots(gs, R, 1000, plies)
   bs = np.arange(R, dtype=np.uint32)
   es = bs + np.uint32(1 << 20)
+  lay = _lib.LAYOUT_WAVE if layout == "wave" else _lib.LAYOUT_LANE
   got = eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
-                       block_size=block)
+                       block_size=block, layout=lay)
   ref = O.Game(gs).mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
                               max_children=eng.max_children, threads=8)
   _cmp(E, got, ref)
 
 
-@pytest.mark.parametrize("gs", ["tic_tac_toe", "connect_four", "hex(board_size=5)"])
+@pytest.mark.parametrize("gs", ["tic_tac_toe", "connect_four", "hex(board_size=5)",
+                                "go(board_size=5,komi=0.5)"])
 @pytest.mark.parametrize("n_rollouts,solve,uct_c", [(3, True, math.sqrt(2)),
                                                     (1, False, 2.0), (2, False, 0.5)])
 def test_search_variants(E, gs, n_rollouts, solve, uct_c):
@@ -179,6 +187,33 @@ def test_full_c2_workload_properties_and_prefix_parity(E):
                               threads=8)
   for k in E.OUTPUT_KEYS:
     assert np.array_equal(o[k][:sub], ref[k]), k
+
+
+def test_full_c3_width_properties_and_prefix_parity(E):
+  """BASELINE configs[2] at full width: 65536 breakthrough(8x8) roots through
+  the automatic layout (the kernel C3 runs in production), sims reduced so the
+  oracle can check a 64-root prefix bit-exactly."""
+  gs, R, sims = "breakthrough(rows=8,columns=8)", 65536, 128
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, R, 1000, 6)
+  bs = np.arange(R, dtype=np.uint32)
+  es = bs + np.uint32(1 << 20)
+  o = eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims)
+  nc = o["nchild"]
+  child_sum = np.array([o["child_n"][r, :nc[r]].sum() for r in range(R)])
+  assert np.array_equal(child_sum, o["root_n"] - 1)
+  assert (o["root_n"] <= sims).all() and (o["root_n"] >= 2).all()
+  early = o["root_n"] < sims
+  assert ((o["root_out"][early] != 2) | (nc[early] == 1)).all()
+  for r in range(0, R, 1021):
+    assert o["best_action"][r] in o["child_action"][r, :nc[r]]
+  for lo in (0, R - 64):  # first and last 64 roots (first and last workgroups)
+    sl = slice(lo, lo + 64)
+    ref = O.Game(gs).mcts_batch(acts[offs[lo]:offs[lo + 64]], offs[lo:lo + 65] - offs[lo],
+                                bs[sl], es[sl], uct_c=2.0, max_simulations=sims,
+                                max_children=eng.max_children, threads=8)
+    for k in E.OUTPUT_KEYS:
+      assert np.array_equal(o[k][sl], ref[k]), (lo, k)
 
 
 def test_python_drop_in_gpu_path(E):
