@@ -112,6 +112,7 @@ struct CtxMaker<Go> {
     c.base = a.root_hashes + gr * a.hash_stride;
     c.n_base = a.root_nhash[gr];
     c.log = log;
+    c.log_stride = 1;
     c.n_log = 0;
     c.cap = kGoLogCap;
     c.init_filters();
@@ -602,7 +603,8 @@ struct RollArgs {
   int32_t n_rollouts;
   const void* root;  // one G::State
   const uint32_t* seeds;
-  uint32_t* mt;      // [n][624]
+  uint32_t* mt;      // [624][n] (k_rollouts, SoA) or [n][624]
+  uint64_t* glog;    // go: [kGoLogCap][n] position logs (k_rollouts, SoA)
   double* out;       // [n][2]
   const uint64_t* zob;
   const uint64_t* root_hashes;
@@ -621,6 +623,7 @@ struct RollCtx<Go> {
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
     c.log = log;
+    c.log_stride = static_cast<int32_t>(a.n);
     c.n_log = 0;
     c.cap = kGoLogCap;
     c.init_filters();
@@ -675,14 +678,16 @@ __global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
   }
 }
 
+// One lane per RandomRolloutEvaluator.  The lanes of a wave start together
+// and draw two words per move in lockstep, so the MT19937 states and go's
+// position logs are batch-SoA in HBM: one contiguous line per word / entry.
 template <class G>
-__global__ void k_rollouts(RollArgs a) {
+__global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
-  MtStream ev{a.mt + i * kMtN, kMtN, 0};
-  mt_seed(ev.s, a.seeds[i]);
-  uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
-  typename G::Ctx ctx = RollCtx<G>::make(a, glog);
+  MtStreamSoA ev{a.mt + i, a.n, 0, 0};
+  ev.seed(a.seeds[i]);
+  typename G::Ctx ctx = RollCtx<G>::make(a, a.glog + i);
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
   for (int k = 0; k < a.n_rollouts; ++k) {
@@ -836,7 +841,7 @@ struct os_engine {
   DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
-      d_sp_obs;
+      d_sp_obs, d_glog;
   std::vector<SearchResult> last_results;
   int64_t last_sims = 0;
   ~os_engine() {
@@ -845,7 +850,7 @@ struct os_engine {
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
-                     &d_az_slots, &d_az_prior};
+                     &d_az_slots, &d_az_prior, &d_glog};
     (void)hipSetDevice(device);
     for (DevBuf* b : all) b->release();
   }
@@ -1519,6 +1524,7 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
   if ((rc = e->d_rollout_out.ensure(std::max<int64_t>(n, 1) * 16))) return rc;
   e->roll_nhash = 0;
   if (e->game.cfg.kind == kGo) {
+    if ((rc = e->d_glog.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 8))) return rc;
     if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
     HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
                       hipMemcpyHostToDevice));
@@ -1546,6 +1552,7 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   a.root = e->d_roots.p;
   a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
   a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.glog = static_cast<uint64_t*>(e->d_glog.p);
   a.out = static_cast<double*>(e->d_rollout_out.p);
   a.zob = static_cast<const uint64_t*>(e->d_zob.p);
   a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);

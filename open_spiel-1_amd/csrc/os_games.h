@@ -444,42 +444,55 @@ struct Filter256 {
   }
 };
 
+// Positional-superko set of one playout / simulation.  Only positions that a
+// capture separates from the current one can repeat it: without a capture in
+// between, every non-pass move adds one stone, so a later position has
+// strictly more stones than an earlier one.  `cand_end` / `cand_filt` cover the
+// log entries logged before the most recent capture (plus every base entry,
+// whose history is unknown); a capturing move widens them to the whole log
+// before its own test.  Same answers as testing the whole set, fewer scans.
 struct GoCtx {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
   const uint64_t* base;    // hashes of positions before this search's root
   int32_t n_base;
   uint64_t* log;           // hashes added since the root (capacity cap)
+  int32_t log_stride;      // element i at log[i * log_stride] (SoA batches)
   int32_t n_log;
+  int32_t cand_end;        // log[0, cand_end): entries a capture separates
   int32_t cap;
-  Filter256 filt;          // all hashes (base + log)
-  Filter256 base_filt;     // base hashes only
+  Filter256 filt;          // base + whole log
+  Filter256 cand_filt;     // base + log[0, cand_end)
 
+  // Empties the log (the base stays).
   OS_HD void reset() {
     n_log = 0;
-    filt = base_filt;
+    cand_end = 0;
+    filt.clear();
+    for (int i = 0; i < n_base; ++i) filt.add(fbit(base[i]));
+    cand_filt = filt;
   }
-  // Builds base_filt from base[0, n_base) and resets.
-  OS_HD void init_filters() {
-    base_filt.clear();
-    for (int i = 0; i < n_base; ++i) base_filt.add(fbit(base[i]));
-    reset();
-  }
+  OS_HD void init_filters() { reset(); }
   OS_HD static int fbit(uint64_t h) { return static_cast<int>(h >> 56); }
-  OS_HD bool filter_has(uint64_t h) const { return filt.has(fbit(h)); }
-  OS_HD void filter_add(uint64_t h) { filt.add(fbit(h)); }
-  OS_HD bool contains(uint64_t h) const {
-    if (!filter_has(h)) return false;
+  OS_HD uint64_t log_at(int i) const { return log[static_cast<int64_t>(i) * log_stride]; }
+  // Whether h is among the candidate positions.
+  OS_HD bool candidate(uint64_t h) const {
+    if (!cand_filt.has(fbit(h))) return false;
     for (int i = 0; i < n_base; ++i)
       if (base[i] == h) return true;
-    for (int i = 0; i < n_log; ++i)
-      if (log[i] == h) return true;
+    for (int i = 0; i < cand_end; ++i)
+      if (log_at(i) == h) return true;
     return false;
   }
-  // Returns false if the position was already present (go.cc:201-205).
-  OS_HD bool insert(uint64_t h) {
-    if (contains(h)) return false;
-    if (n_log < cap) log[n_log++] = h;
-    filter_add(h);
+  // Logs the position after a non-pass move; false if it was already present
+  // (go.cc:201-205).  `captured`: the move removed stones.
+  OS_HD bool insert(uint64_t h, bool captured) {
+    if (captured) {
+      cand_end = n_log;
+      cand_filt = filt;
+    }
+    if (candidate(h)) return false;
+    if (n_log < cap) log[static_cast<int64_t>(n_log++) * log_stride] = h;
+    filt.add(fbit(h));
     return true;
   }
 };
@@ -616,59 +629,97 @@ struct Go {
       s.bw[0] = c ? opp : own;
       s.bw[1] = c ? own : opp;
       s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
-      if (!ctx.insert(s.hash)) s.flags |= kSuperko;
+      if (!ctx.insert(s.hash, captured > 0)) s.flags |= kSuperko;
     }
     s.to_play = static_cast<uint8_t>(1 - c);
     s.moves++;
   }
   // Tromp-Taylor score with the reference's early-abort DFS
-  // (go_board.cc:526-597): neighbour order +row, +col, -col, -row; the
-  // "marked or reached both colours" test happens only on entry.
+  // (go_board.cc:526-597): for every empty point in ascending order that is
+  // not yet marked, a DFS over empty points (neighbour order +row, +col, -col,
+  // -row; "marked or reached both colours" tested only on entry) counts the
+  // points it marks; the count goes to the colour it reached if it reached
+  // only one.  DFSs never cross stones, so each empty region is independent:
+  //   * a region bordering one colour (or none) is explored whole by its first
+  //     DFS -- its size, from a bitboard flood;
+  //   * a region bordering both colours is where the early abort matters: the
+  //     reference's DFS sequence is replayed on it exactly (tt_mixed_region).
   OS_HD static float score(const State& s, const GameCfg& g) {
-    const int n = g.rows;
     const B128 E = g.board & ~(s.bw[0] | s.bw[1]);
     int delta = popc(s.bw[0]) - popc(s.bw[1]);
-    B128 marked = b128(0, 0);
-    uint8_t st_pt[128];
-    uint8_t st_d[128];
     B128 todo = E;
+    while (any(todo)) {
+      const B128 reg = flood(bit128(lowest(todo)), E, g);
+      todo = todo & ~reg;
+      const B128 rim = nbr4(reg, g);
+      const bool rb = any(rim & s.bw[0]), rw = any(rim & s.bw[1]);
+      if (rb && !rw) delta += popc(reg);
+      else if (rw && !rb) delta -= popc(reg);
+      else if (rb && rw && popc(reg) > 1) delta += tt_mixed_region(s, g, reg);
+    }
+    float sc = static_cast<float>(delta) - g.komi;
+    if (g.handicap >= 2) sc -= static_cast<float>(g.handicap);
+    return sc;
+  }
+  // The reference's DFS sequence on one empty region that borders both
+  // colours; returns its contribution to (black - white).  The DFS stack is
+  // held as the 2-bit directions taken from the start point (a point's parent
+  // is one step back along its direction, and an ancestor resumes at the
+  // direction after the one it took), so no per-point stack memory is needed.
+  OS_HD static int tt_mixed_region(const State& s, const GameCfg& g, B128 reg) {
+    const int n = g.rows;
+    int delta = 0;
+    B128 marked = b128(0, 0);
+    B128 todo = reg;
     while (any(todo)) {
       const int p0 = lowest(todo);
       todo = todo & ~bit128(p0);
       if (test(marked, p0)) continue;
       bool rb = false, rw = false;
       int num = 1;
-      int sp = 0;
       marked = marked | bit128(p0);
-      st_pt[0] = static_cast<uint8_t>(p0);
-      st_d[0] = 0;
-      sp = 1;
-      while (sp > 0 && !(rb && rw)) {
-        const int p = st_pt[sp - 1];
-        const int d = st_d[sp - 1];
-        if (d == 4) { --sp; continue; }
-        st_d[sp - 1] = static_cast<uint8_t>(d + 1);
-        const int r = p / n, cc = p % n;
+      uint64_t path0 = 0, path1 = 0, path2 = 0, path3 = 0;  // 2 bits per level
+      int depth = 0;  // stack size - 1
+      int cur = p0, curd = 0;
+      for (;;) {
+        if (rb && rw) break;
+        if (curd == 4) {  // pop
+          if (depth == 0) break;
+          --depth;
+          const int w = depth >> 5, sh = 2 * (depth & 31);
+          const uint64_t pw = w == 0 ? path0 : (w == 1 ? path1 : (w == 2 ? path2 : path3));
+          const int dir = static_cast<int>((pw >> sh) & 3);
+          cur -= dir == 0 ? n : (dir == 1 ? 1 : (dir == 2 ? -1 : -n));
+          curd = dir + 1;
+          continue;
+        }
+        const int d = curd++;
+        const int r = cur / n, cc = cur - r * n;
         int q;
-        if (d == 0) { if (r + 1 >= n) continue; q = p + n; }
-        else if (d == 1) { if (cc + 1 >= n) continue; q = p + 1; }
-        else if (d == 2) { if (cc - 1 < 0) continue; q = p - 1; }
-        else { if (r - 1 < 0) continue; q = p - n; }
+        if (d == 0) { if (r + 1 >= n) continue; q = cur + n; }
+        else if (d == 1) { if (cc + 1 >= n) continue; q = cur + 1; }
+        else if (d == 2) { if (cc - 1 < 0) continue; q = cur - 1; }
+        else { if (r - 1 < 0) continue; q = cur - n; }
         if (test(s.bw[0], q)) { rb = true; continue; }
         if (test(s.bw[1], q)) { rw = true; continue; }
         if (test(marked, q)) continue;
         marked = marked | bit128(q);
         ++num;
-        st_pt[sp] = static_cast<uint8_t>(q);
-        st_d[sp] = 0;
-        ++sp;
+        // Slot `depth` <- d (it may hold a popped sibling's direction).
+        const int w = depth >> 5, sh = 2 * (depth & 31);
+        const uint64_t keep = ~(3ull << sh), m = static_cast<uint64_t>(d) << sh;
+        path0 = w == 0 ? ((path0 & keep) | m) : path0;
+        path1 = w == 1 ? ((path1 & keep) | m) : path1;
+        path2 = w == 2 ? ((path2 & keep) | m) : path2;
+        path3 = w == 3 ? ((path3 & keep) | m) : path3;
+        ++depth;
+        cur = q;
+        curd = 0;
       }
       if (rb && !rw) delta += num;
       else if (!rb && rw) delta -= num;
     }
-    float sc = static_cast<float>(delta) - g.komi;
-    if (g.handicap >= 2) sc -= static_cast<float>(g.handicap);
-    return sc;
+    return delta;
   }
   template <class C>
   OS_HD static int ret0(const State& s, const GameCfg& g, C&) {

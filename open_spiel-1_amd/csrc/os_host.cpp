@@ -255,11 +255,18 @@ GoCtx HostGoCtx(const HostState& s, std::vector<uint64_t>* storage) {
   ctx.base = nullptr;
   ctx.n_base = 0;
   ctx.log = storage->data();
-  ctx.n_log = static_cast<int32_t>(s.hashes.size());
+  ctx.log_stride = 1;
   ctx.cap = cap;
-  ctx.base_filt.clear();
-  ctx.filt.clear();
-  for (size_t i = 0; i < s.hashes.size(); ++i) ctx.filter_add(s.hashes[i]);
+  ctx.reset();
+  // The state's own history is logged with unknown captures in between:
+  // every entry stays a candidate.
+  for (size_t i = 0; i < s.hashes.size(); ++i) {
+    ctx.log[i] = s.hashes[i];
+    ctx.filt.add(GoCtx::fbit(s.hashes[i]));
+  }
+  ctx.n_log = static_cast<int32_t>(s.hashes.size());
+  ctx.cand_end = ctx.n_log;
+  ctx.cand_filt = ctx.filt;
   return ctx;
 }
 

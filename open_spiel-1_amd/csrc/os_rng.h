@@ -74,6 +74,41 @@ struct MtStream {
   }
 };
 
+// The same stream over a structure-of-arrays batch: word i of this stream at
+// s[i * stride] (stride = streams in the batch), so lanes that draw in
+// lockstep read and write one contiguous line per word.  Seeded in place;
+// no numpy import.
+struct MtStreamSoA {
+  uint32_t* s;
+  int64_t stride;
+  int idx;
+  uint32_t words;
+
+  OS_HD uint32_t& at(int i) const { return s[static_cast<int64_t>(i) * stride]; }
+  OS_HD void seed(uint32_t v) {
+    uint32_t x = v;
+    at(0) = x;
+    for (int i = 1; i < kMtN; ++i) {
+      x = 1812433253u * (x ^ (x >> 30)) + static_cast<uint32_t>(i);
+      at(i) = x;
+    }
+    idx = kMtN;
+    words = 0;
+  }
+  OS_HD uint32_t next() {
+    ++words;
+    if (idx >= kMtN) idx = 0;
+    const int i = idx;
+    const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+    const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+    const uint32_t y = (at(i) & 0x80000000u) | (at(i1) & 0x7fffffffu);
+    const uint32_t v = at(im) ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    at(i) = v;
+    idx = i + 1;
+    return MtStream::temper(v);
+  }
+};
+
 OS_HD uint64_t umulhi64(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __umul64hi(a, b);

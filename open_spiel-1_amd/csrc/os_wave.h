@@ -294,41 +294,50 @@ struct WaveMt {
 };
 
 // Go superko context for one search per wave: the per-simulation hash log in
-// LDS, compared 64 entries at a time.
+// LDS, compared 64 entries at a time.  Candidates as in GoCtx (os_games.h):
+// only entries logged before the most recent capture can repeat a position.
 struct GoWaveCtx {
   const uint64_t* zob;
   const uint64_t* base;   // hashes before the root (global)
   int32_t n_base;
   uint64_t* log;          // LDS
   int32_t n_log;
+  int32_t cand_end;
   int32_t cap;
   Filter256 filt;
+  Filter256 cand_filt;
   Filter256 base_filt;
 
   __device__ void reset() {
     n_log = 0;
+    cand_end = 0;
     filt = base_filt;
+    cand_filt = base_filt;
   }
   __device__ void init_filters() {
     base_filt.clear();
     for (int i = 0; i < n_base; ++i) base_filt.add(GoCtx::fbit(base[i]));
     reset();
   }
-  __device__ bool contains(uint64_t h) const {
-    if (!filt.has(GoCtx::fbit(h))) return false;
+  __device__ bool candidate(uint64_t h) const {
+    if (!cand_filt.has(GoCtx::fbit(h))) return false;
     const int l = lane_id();
     for (int i = 0; i < n_base; i += 64) {
       const bool hit = i + l < n_base && base[i + l] == h;
       if (ballot(hit)) return true;
     }
-    for (int i = 0; i < n_log; i += 64) {
-      const bool hit = i + l < n_log && log[i + l] == h;
+    for (int i = 0; i < cand_end; i += 64) {
+      const bool hit = i + l < cand_end && log[i + l] == h;
       if (ballot(hit)) return true;
     }
     return false;
   }
-  __device__ bool insert(uint64_t h) {
-    if (contains(h)) return false;
+  __device__ bool insert(uint64_t h, bool captured) {
+    if (captured) {
+      cand_end = n_log;
+      cand_filt = filt;
+    }
+    if (candidate(h)) return false;
     if (n_log < cap) {
       if (lane_id() == 0) log[n_log] = h;
       __builtin_amdgcn_wave_barrier();

@@ -108,6 +108,12 @@ int oref_game_info(void* g, int32_t* num_actions, int32_t* max_len) {
 
 // Replays `actions` and writes a JSON object describing the reached state.
 // Returns the number of bytes needed (excluding NUL); truncates to buflen-1.
+// go: Tromp-Taylor score of the position after `actions`.
+float oref_go_score(void* g, const int64_t* actions, int64_t n) {
+  auto* og = static_cast<OGame*>(g);
+  return GoScore(*Replay(*og->game, actions, n));
+}
+
 int64_t oref_state_json(void* g, const int64_t* actions, int64_t n, char* buf,
                         int64_t buflen) {
   auto* og = static_cast<OGame*>(g);

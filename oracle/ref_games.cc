@@ -837,6 +837,8 @@ class State : public RState {
            (history_[history_.size() - 1] == board_.pass_action() &&
             history_[history_.size() - 2] == board_.pass_action());
   }
+  // Tromp-Taylor score of the current board (go_board.cc:555-597).
+  float Score() const { return TrompTaylorScore(board_, komi_, handicap_); }
   std::vector<double> Returns() const override {
     if (!IsTerminal()) return {0.0, 0.0};
     if (superko_) return {0.0, 0.0};
@@ -926,6 +928,10 @@ class Game : public RGame {
   int handicap_;
 };
 }  // namespace go
+
+float GoScore(const RState& s) {
+  return dynamic_cast<const go::State&>(s).Score();
+}
 
 std::unique_ptr<RGame> LoadGame(const std::string& gs, std::string* err) {
   std::string name;

@@ -76,6 +76,9 @@ class RGame {
 };
 
 // Returns nullptr (and sets *err) for unknown games / unsupported params.
+// Tromp-Taylor score of a go state's board (go_board.cc:555-597).
+float GoScore(const RState& s);
+
 std::unique_ptr<RGame> LoadGame(const std::string& game_string,
                                 std::string* err);
 

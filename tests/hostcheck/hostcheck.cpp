@@ -40,6 +40,7 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
     ctx.base = root.hashes.data();
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
     ctx.log = logbuf.data();
+    ctx.log_stride = 1;
     ctx.cap = 256;
     ctx.init_filters();
   }
@@ -313,6 +314,18 @@ void hc_mt_roundtrip(uint32_t* key, int32_t* pos, int64_t k, uint32_t* out) {
   *pos = g.idx;
 }
 
+// Product go score (os_games.h Go::score) of the position after `actions`.
+float hc_go_score(const char* game_string, const int64_t* actions, int64_t n) {
+  HostGame game;
+  bool unsup = false;
+  if (!LoadHostGame(game_string, &game, &unsup).empty()) return -1e30f;
+  HostState hs;
+  hs.game = &game;
+  StateInit(&hs);
+  for (int64_t i = 0; i < n; ++i) StateApply(&hs, actions[i]);
+  return Go::score(*reinterpret_cast<const Go::State*>(hs.raw), game.cfg);
+}
+
 // Product rollouts on the host: RandomRolloutEvaluator::Evaluate per seed.
 int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actions,
                 int64_t n, const uint32_t* seeds, double* out) {
@@ -345,6 +358,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
         c.base = hs.hashes.data();
         c.n_base = static_cast<int32_t>(hs.hashes.size());
         c.log = logbuf.data();
+        c.log_stride = 1;
         c.cap = 256;
         c.init_filters();
         r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg, c, ev);

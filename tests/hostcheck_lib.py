@@ -25,6 +25,8 @@ def lib():
                                 vp, vp, ctypes.c_int32] + [vp] * 10
     L.hc_rollouts.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.c_int64,
                               vp, vp]
+    L.hc_go_score.restype = ctypes.c_float
+    L.hc_go_score.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64]
     L.hc_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
     L.hc_absl_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp]
     L.hc_cpp_shuffle.argtypes = [ctypes.c_uint32, ctypes.c_int32, vp]
@@ -76,6 +78,11 @@ def rollouts(game_string, history, seeds):
   if rc:
     raise RuntimeError(lib().hc_last_error().decode())
   return out
+
+
+def go_score(game_string, history):
+  a = np.ascontiguousarray(history, np.int64)
+  return float(lib().hc_go_score(game_string.encode(), a.ctypes.data, len(a)))
 
 
 def mt_words(seed, n):

@@ -46,6 +46,8 @@ def lib():
     L.oref_state_json.restype = ctypes.c_int64
     L.oref_state_json.argtypes = [ctypes.c_void_p, _i64p, ctypes.c_int64,
                                   ctypes.c_char_p, ctypes.c_int64]
+    L.oref_go_score.restype = ctypes.c_float
+    L.oref_go_score.argtypes = [ctypes.c_void_p, _i64p, ctypes.c_int64]
     L.oref_rollouts.argtypes = [ctypes.c_void_p, _i64p, ctypes.c_int64,
                                 ctypes.c_int64, ctypes.c_int32, _u32p, _f64p,
                                 ctypes.c_void_p]
@@ -102,6 +104,10 @@ class Game:
     buf = ctypes.create_string_buffer(int(n) + 1)
     lib().oref_state_json(self._h, a, len(a), buf, n + 1)
     return json.loads(buf.value.decode())
+
+  def go_score(self, history):
+    a = np.ascontiguousarray(history, dtype=np.int64)
+    return float(lib().oref_go_score(self._h, a, len(a)))
 
   def rollouts(self, history, seeds, n_rollouts=1):
     a = np.ascontiguousarray(history, dtype=np.int64)
