@@ -1,50 +1,21 @@
-// libos_mcts.so — gfx950 search / rollout kernels and the C-ABI declared in
-// include/os_mcts.h.
+// libos_mcts.so — host side of the MI355X MCTS engine and the C-ABI declared
+// in include/os_mcts.h.
 //
 // Execution model: every root is one independent search
 // (MCTSBot::MCTSearch, mcts.cc:325-428) with its own flat node arena in HBM.
-//   k_wsearch (OS_LAYOUT_WAVE): one 64-lane wavefront per search; game state
-//     wave-uniform in SGPRs, MT19937 streams + visit path in LDS (os_wave.h).
-//   k_mcts (OS_LAYOUT_LANE): one lane per search; game state in VGPRs, MT
-//     streams in HBM, path / expansion buffers in LDS slices (os_mcts.h).
-// Searches never share memory, so there are no atomics in the search and
-// results are bit-exact regardless of scheduling.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cmath>
-#include <random>
-#include <cstdio>
-#include <cstring>
+// This unit prepares batches (root replay, arena sizing, uploads), launches
+// the per-game kernels through the launcher table (os_kernels.h,
+// os_game_*.hip), fetches results and reports errors.
 #include <memory>
 #include <mutex>
-#include <string>
-#include <vector>
+#include <random>
 
-#include "../../include/os_mcts.h"
-#include "os_host.h"
-#include "os_mcts.h"
-#include "os_wave.h"
-#include "os_az.h"
+#include "os_engine_impl.h"
 
 using namespace osm;
+using namespace osx;
 
-// ---------------------------------------------------------------------------
-// Errors
-namespace {
-thread_local std::string g_err;
-int Fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
-#define HIP_TRY(expr)                                                        \
-  do {                                                                       \
-    hipError_t _e = (expr);                                                  \
-    if (_e != hipSuccess)                                                    \
-      return Fail(OS_ERR_DEVICE, std::string(#expr " failed: ") +            \
-                                     hipGetErrorString(_e));                 \
-  } while (0)
-}  // namespace
+thread_local std::string osx::g_err;
 
 struct os_game {
   HostGame g;
@@ -53,652 +24,8 @@ struct os_state {
   HostState s;
 };
 
-// ---------------------------------------------------------------------------
-// Device code
+namespace osx {
 namespace {
-
-constexpr int kGoLogCap = 248;  // >= 2 * 11 * 11 + 4
-
-#if OS_PHASE_TIMING
-__device__ uint64_t g_phase_cycles[kNumPhases];  // diagnostic build only
-#endif
-
-struct DevArgs {
-  GameCfg cfg;
-  SearchParams sp;
-  int64_t num_roots;      // roots in this launch
-  int64_t root_base;      // global index of the first root of this launch
-  const void* roots;      // [total] G::State
-  const uint32_t* bot_seeds;
-  const uint32_t* eval_seeds;
-  uint32_t* mt;           // [num_roots][2][624]
-  void* arena;            // [num_roots][cap] Node<R>
-  uint32_t cap;
-  int32_t path_cap;       // >= MaxGameLength + 1 (LDS path slice per lane)
-  int32_t child_cap;      // >= max |LegalActions| (LDS expansion slice)
-  int32_t import_state;   // numpy (key, pos) import / export
-  int32_t shared_stream;  // numpy: one RandomState for bot + evaluator
-  int32_t* mt_pos;        // [total][2] in/out when import_state
-  // go
-  const uint64_t* zob;
-  const uint64_t* root_hashes;  // [total][hash_stride]
-  const int32_t* root_nhash;    // [total]
-  int32_t hash_stride;
-  // outputs, indexed by global root
-  SearchResult* results;
-  int32_t max_children;
-  int32_t* child_action;
-  int32_t* child_n;
-  double* child_w;
-  int8_t* child_out;
-  int32_t* nchild;
-  int32_t* root_n;
-  double* root_w;
-  int8_t* root_out;
-  int64_t* best_action;
-};
-
-template <class G>
-struct CtxMaker;
-template <class G>
-struct CtxMaker {
-  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
-};
-template <>
-struct CtxMaker<Go> {
-  __device__ static GoCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
-    GoCtx c;
-    c.zob = a.zob;
-    c.base = a.root_hashes + gr * a.hash_stride;
-    c.n_base = a.root_nhash[gr];
-    c.log = log;
-    c.log_stride = 1;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
-    c.init_filters();
-    return c;
-  }
-};
-
-template <class G, class R, int Policy>
-__global__ void k_mcts(DevArgs a) {
-  const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (lr >= a.num_roots) return;
-  const int64_t gr = a.root_base + lr;
-  // Per-lane LDS slices: [blockDim][2][624] MT19937 words, then
-  // [blockDim][path_cap] u32 visit path, then [blockDim][child_cap] u16
-  // expansion buffer.  Every per-simulation random word and path entry is an
-  // LDS access (~tens of cycles) instead of a dependent HBM/L2 round trip.
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int nb = blockDim.x;
-  const int lane = threadIdx.x;
-  uint32_t* mt0 = reinterpret_cast<uint32_t*>(smem) + lane * 2 * kMtN;
-  PathEnt<R>* path =
-      reinterpret_cast<PathEnt<R>*>(smem + static_cast<size_t>(nb) * 2 * kMtN * 4) +
-      lane * a.path_cap;
-  uint16_t* actbuf =
-      reinterpret_cast<uint16_t*>(
-          smem + static_cast<size_t>(nb) * (2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>))) +
-      lane * a.child_cap;
-  MtStream bot{mt0, kMtN, 0};
-  MtStream ev{mt0 + kMtN, kMtN, 0};
-  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
-  if (a.import_state) {
-    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
-    for (int i = 0; i < 2 * kMtN; ++i) mt0[i] = g0[i];
-    bot.idx = a.mt_pos[2 * gr];
-    bot.pre = 1;
-    ev.idx = a.mt_pos[2 * gr + 1];
-    ev.pre = 1;
-  } else {
-    mt_seed(bot.s, a.bot_seeds[gr]);
-    if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
-  }
-  const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
-  uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
-  typename G::Ctx ctx = CtxMaker<G>::make(a, gr, glog);
-  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
-  SearchResult res;
-  if (Policy == kPolicyNumpy && a.shared_stream)
-    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
-                                    path, actbuf, a.path_cap);
-  else
-    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
-                                    path, actbuf, a.path_cap);
-  res.rng_words = bot.words + ((Policy == kPolicyNumpy && a.shared_stream) ? 0u : ev.words);
-  a.results[gr] = res;
-  const Node<R>& rn = nodes[0];
-  const int P0 = G::to_move(root);
-  const int nc = rn.nchild;
-  a.nchild[gr] = nc;
-  a.root_n[gr] = rn.n;
-  a.root_w[gr] = static_cast<double>(rn.w);
-  a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
-                                       : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
-  const int64_t ob = gr * a.max_children;
-  for (int k = 0; k < nc && k < a.max_children; ++k) {
-    const Node<R>& c = nodes[rn.first + k];
-    a.child_action[ob + k] = c.action;
-    a.child_n[ob + k] = c.n;
-    a.child_w[ob + k] = static_cast<double>(c.w);
-    a.child_out[ob + k] =
-        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
-  }
-  const int b = best_child(nodes, P0);
-  a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
-  if (a.import_state) {
-    bot.finalize();
-    a.mt_pos[2 * gr] = bot.idx;
-    if (!a.shared_stream) {
-      ev.finalize();
-      a.mt_pos[2 * gr + 1] = ev.idx;
-    }
-    uint32_t* g0 = a.mt + lr * 2 * kMtN;
-    for (int i = 0; i < 2 * kMtN; ++i) g0[i] = mt0[i];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Wave-per-search kernel (default layout): one 64-lane workgroup per search.
-template <class G>
-struct WaveCtxMaker {
-  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
-};
-template <>
-struct WaveCtxMaker<Go> {
-  __device__ static GoWaveCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
-    GoWaveCtx c;
-    c.zob = a.zob;
-    c.base = a.root_hashes + gr * a.hash_stride;
-    c.n_base = a.root_nhash[gr];
-    c.log = log;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
-    c.init_filters();
-    return c;
-  }
-};
-
-template <class G, class R>
-__host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
-  return static_cast<size_t>(2 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
-         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
-}
-
-// Minimum waves per SIMD requested from the register allocator (A/B knob).
-#ifndef OS_HEX_OCC
-#define OS_HEX_OCC 1
-#endif
-template <class G>
-struct WaveOcc {
-  static constexpr int value = 1;
-};
-template <>
-struct WaveOcc<Hex> {
-  static constexpr int value = OS_HEX_OCC;
-};
-
-template <class G, class R, int Policy>
-__global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
-  const int64_t lr = blockIdx.x;
-  if (lr >= a.num_roots) return;
-  const int64_t gr = a.root_base + lr;
-  const int l = lane_id();
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
-  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4);
-  uint64_t* glog = reinterpret_cast<uint64_t*>(
-      smem + ((2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
-  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
-  WaveMt bot, ev;
-  bot.s = mt;
-  ev.s = mt + kMtN;
-  bot.use7 = 0;
-  ev.use7 = SmallAbsl<G>::value && Policy == kPolicyCpp && !shared ? 1 : 0;
-  if (a.import_state) {
-    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
-    for (int i = l; i < 2 * kMtN; i += 64) mt[i] = g0[i];
-    __syncthreads();
-    bot.init_import(a.mt_pos[2 * gr]);
-    ev.init_import(a.mt_pos[2 * gr + 1]);
-  } else {
-    if (l == 0) {
-      mt_seed(bot.s, a.bot_seeds[gr]);
-      if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
-    }
-    __syncthreads();
-    bot.init_seeded();
-    ev.init_seeded();
-  }
-  const typename G::State root =
-      make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
-  typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr, glog);
-  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
-  PhaseCycles ph = {};
-  SearchResult res = shared
-      ? wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
-                                  a.path_cap, ph)
-      : wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
-                                  a.path_cap, ph);
-  res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
-#if OS_PHASE_TIMING
-  ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);
-  if (l == 0)
-    for (int i = 0; i < kNumPhases; ++i)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&g_phase_cycles[i]),
-                static_cast<unsigned long long>(ph.c[i]));
-#endif
-  __threadfence_block();
-  const Node<R> rn = nodes[0];
-  const int P0 = G::to_move(root);
-  const int nc = rn.nchild;
-  const int64_t ob = gr * a.max_children;
-  for (int k = l; k < nc && k < a.max_children; k += 64) {
-    const Node<R> c = nodes[rn.first + k];
-    a.child_action[ob + k] = c.action;
-    a.child_n[ob + k] = c.n;
-    a.child_w[ob + k] = static_cast<double>(c.w);
-    a.child_out[ob + k] =
-        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
-  }
-  if (l == 0) {
-    a.results[gr] = res;
-    a.nchild[gr] = nc;
-    a.root_n[gr] = rn.n;
-    a.root_w[gr] = static_cast<double>(rn.w);
-    a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
-                                         : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
-    const int b = best_child(nodes, P0);
-    a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
-  }
-  if (a.import_state) {
-    if (l == 0) {
-      a.mt_pos[2 * gr] = bot.export_pos();
-      if (!shared) a.mt_pos[2 * gr + 1] = ev.export_pos();
-    }
-    __syncthreads();
-    uint32_t* g0 = a.mt + lr * 2 * kMtN;
-    for (int i = l; i < 2 * kMtN; i += 64) g0[i] = mt[i];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Self-play: one wave plays a whole game the way
-// examples/mcts_example.cc:77-136 PlayGame does with two MCTSBots sharing one
-// RandomRolloutEvaluator: every move is bots[CurrentPlayer]->Step(state) =
-// MCTSearch + BestChild (mcts.cc:219-226, 325-428), both bots' rng_ and the
-// shared evaluator's rng persist across moves.
-struct SpArgs {
-  GameCfg cfg;
-  SearchParams sp;
-  int64_t num_games;      // games in this launch
-  int64_t game_base;      // global index of the first game of this launch
-  const void* starts;     // [total] G::State
-  const uint32_t* bot_seeds;   // [total][2]
-  const uint32_t* eval_seeds;  // [total]
-  void* arena;            // [num_games][cap] Node<R>
-  uint32_t cap;
-  int32_t path_cap;
-  int32_t max_len;        // trajectory slots per game
-  int32_t num_actions;
-  // go: per-game position history (grows by one per move)
-  const uint64_t* zob;
-  uint64_t* hist;         // [total][hash_stride]
-  int32_t* hist_n;        // [total]
-  int32_t hash_stride;
-  // outputs
-  int32_t* actions;       // [total][max_len], -1 padded
-  int32_t* length;        // [total]
-  double* returns;        // [total][2]
-  int32_t* visits;        // [total][max_len][num_actions] or null
-  float* obs;             // [total][max_len][obs_size] or null
-  int32_t obs_size;       // C * H * W
-  SearchResult* results;  // [total], summed over the game's searches
-};
-
-template <class G>
-struct SpCtx {  // games without a history context
-  __device__ static NoCtx make(const SpArgs&, int64_t, uint64_t*) { return NoCtx(); }
-  __device__ static void commit(NoCtx&, const SpArgs&, int64_t) {}
-};
-template <>
-struct SpCtx<Go> {
-  __device__ static GoWaveCtx make(const SpArgs& a, int64_t gg, uint64_t* log) {
-    GoWaveCtx c;
-    c.zob = a.zob;
-    c.base = a.hist + gg * a.hash_stride;
-    c.n_base = a.hist_n[gg];
-    c.log = log;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
-    c.init_filters();
-    return c;
-  }
-  // The move just applied logged its position (go.cc:199-208): append it to
-  // the game history that the next searches treat as "before the root".
-  __device__ static void commit(GoWaveCtx& c, const SpArgs& a, int64_t gg) {
-    uint64_t* h = a.hist + gg * a.hash_stride;
-    if (lane_id() == 0)
-      for (int i = 0; i < c.n_log && c.n_base + i < a.hash_stride; ++i) h[c.n_base + i] = c.log[i];
-    __threadfence_block();
-    c.n_base = c.n_base + c.n_log < a.hash_stride ? c.n_base + c.n_log : a.hash_stride;
-    c.init_filters();
-  }
-};
-
-template <class G, class R>
-__host__ __device__ constexpr size_t SelfPlayLdsBytes(int path_cap) {
-  return static_cast<size_t>(3 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
-         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
-}
-
-template <class G, class R>
-__global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
-  const int64_t lg = blockIdx.x;
-  if (lg >= a.num_games) return;
-  const int64_t gg = a.game_base + lg;
-  const int l = lane_id();
-  extern __shared__ __align__(16) unsigned char smem[];
-  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
-  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 3 * kMtN * 4);
-  uint64_t* glog = reinterpret_cast<uint64_t*>(
-      smem + ((3 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
-  WaveMt b0, b1, ev;
-  b0.s = mt;
-  b1.s = mt + kMtN;
-  ev.s = mt + 2 * kMtN;
-  b0.use7 = b1.use7 = 0;
-  ev.use7 = SmallAbsl<G>::value ? 1 : 0;
-  if (l == 0) {
-    mt_seed(b0.s, a.bot_seeds[2 * gg]);
-    mt_seed(b1.s, a.bot_seeds[2 * gg + 1]);
-    mt_seed(ev.s, a.eval_seeds[gg]);
-  }
-  __syncthreads();
-  b0.init_seeded();
-  b1.init_seeded();
-  ev.init_seeded();
-  typename G::State s = make_uniform(static_cast<const typename G::State*>(a.starts)[gg]);
-  typename WaveCtxOf<G>::type ctx = SpCtx<G>::make(a, gg, glog);
-  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lg * static_cast<int64_t>(a.cap);
-  PhaseCycles ph = {};
-  SearchResult tot;
-  tot.status = kOk;
-  tot.sims = tot.nodes = tot.gc_runs = tot.max_depth = 0;
-  tot.used = tot.scanned = tot.backed = tot.expanded = tot.solver_scanned = 0;
-  tot.rng_words = tot.pad = 0;
-  int m = 0;
-  while (!G::terminal(s, a.cfg)) {
-    if (m >= a.max_len) {
-      tot.status = kGameOverflow;
-      break;
-    }
-    const int p = G::to_move(s);
-    WaveMt bot = p == 0 ? b0 : b1;
-    const SearchResult r =
-        wave_search<G, R, kPolicyCpp>(a.cfg, a.sp, s, ctx, nodes, a.cap, bot, ev, path,
-                                      a.path_cap, ph);
-    if (p == 0) b0 = bot;
-    else b1 = bot;
-    tot.sims += r.sims;
-    tot.nodes += r.nodes;
-    tot.used = r.used > tot.used ? r.used : tot.used;
-    tot.gc_runs += r.gc_runs;
-    tot.max_depth = r.max_depth > tot.max_depth ? r.max_depth : tot.max_depth;
-    tot.scanned += r.scanned;
-    tot.backed += r.backed;
-    tot.expanded += r.expanded;
-    tot.solver_scanned += r.solver_scanned;
-    if (r.status != kOk) {
-      tot.status = r.status;
-      break;
-    }
-    __threadfence_block();
-    // MCTSBot::Step: BestChild of the root (mcts.cc:222-225).
-    int bi = 0;
-    if (l == 0) bi = best_child(nodes, p);
-    bi = rli(bi, 0);
-    const uint32_t rfirst = static_cast<uint32_t>(rli(static_cast<int>(nodes[0].first), 0));
-    const int rnc = rli(nodes[0].nchild, 0);
-    const int act = rli(nodes[rfirst + bi].action, 0);
-    if (a.visits) {
-      int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
-      for (int i = l; i < a.num_actions; i += 64) v[i] = 0;
-      __threadfence_block();
-      for (int k = l; k < rnc; k += 64) {
-        const Node<R> c = nodes[rfirst + k];
-        v[c.action] = c.n;
-      }
-    }
-    if (a.obs) {  // ObservationTensor(player to move) of the position searched
-      float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
-      const int cells = a.cfg.rows * a.cfg.cols;
-      for (int i = l; i < a.obs_size; i += 64) o[i] = G::obs(s, a.cfg, p, i / cells, i % cells);
-    }
-    if (l == 0) a.actions[gg * a.max_len + m] = act;
-    ctx.reset();
-    G::apply(s, a.cfg, ctx, act);
-    SpCtx<G>::commit(ctx, a, gg);
-    s = make_uniform(s);
-    ++m;
-  }
-  tot.rng_words = b0.words.get() + b1.words.get() + ev.words.get();
-  for (int k = m + l; k < a.max_len; k += 64) a.actions[gg * a.max_len + k] = -1;
-  if (a.visits) {  // rows after the last move are all-zero policy targets
-    int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
-    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.num_actions;
-    for (int64_t i = l; i < nz; i += 64) v[i] = 0;
-  }
-  if (a.obs) {
-    float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
-    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.obs_size;
-    for (int64_t i = l; i < nz; i += 64) o[i] = 0.0f;
-  }
-  if (l == 0) {
-    const int r0 = G::terminal(s, a.cfg) ? G::ret0(s, a.cfg, ctx) : 0;
-    a.length[gg] = m;
-    a.returns[2 * gg] = static_cast<double>(r0);
-    a.returns[2 * gg + 1] = static_cast<double>(-r0);
-    a.results[gg] = tot;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// External-evaluator MCTS (os_az.h): one lane per search, one step per launch.
-struct AzArgs {
-  GameCfg cfg;
-  SearchParams sp;
-  int32_t puct;
-  int64_t num_roots;
-  const void* roots;        // [R] G::State
-  void* slots;              // [R] AzSlot<G>
-  Node<double>* arena;      // [R][cap]
-  double* priors;           // [R][cap]
-  uint32_t cap;
-  uint32_t* mt;             // [R][624] bot rng
-  const uint32_t* bot_seeds;
-  int32_t obs_size;
-  int32_t num_actions;
-  int32_t* kind;            // [R]
-  float* obs;               // [R][obs_size]
-  uint8_t* legal;           // [R][A]
-  const double* prior_in;   // [R][A]
-  const double* value_in;   // [R]
-  int32_t* pending;         // requests written by this step
-  // outputs (same layout as the search kernels)
-  SearchResult* results;
-  int32_t max_children;
-  int32_t* child_action;
-  int32_t* child_n;
-  double* child_w;
-  int8_t* child_out;
-  int32_t* nchild;
-  int32_t* root_n;
-  double* root_w;
-  int8_t* root_out;
-  int64_t* best_action;
-};
-
-template <class G>
-__global__ void k_az_step(AzArgs a) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r >= a.num_roots) return;
-  AzSlot<G>& sl = static_cast<AzSlot<G>*>(a.slots)[r];
-  const int stage0 = sl.stage;
-  if (stage0 == kAzDone) {
-    a.kind[r] = kAzNone;
-    return;
-  }
-  uint32_t* mt = a.mt + r * kMtN;
-  if (stage0 == kAzStart) {
-    mt_seed(mt, a.bot_seeds[r]);
-    sl.mt_idx = kMtN;
-    sl.mt_pre = 0;
-    sl.depth = 0;
-    sl.s = static_cast<const typename G::State*>(a.roots)[r];
-  }
-  MtStream bot{mt, sl.mt_idx, sl.mt_pre, 0};
-  const typename G::State root = static_cast<const typename G::State*>(a.roots)[r];
-  Node<double>* nodes = a.arena + r * static_cast<int64_t>(a.cap);
-  AzIo io;
-  io.kind = a.kind + r;
-  io.obs = a.obs + r * a.obs_size;
-  io.legal = a.legal + r * a.num_actions;
-  io.prior = a.prior_in + r * a.num_actions;
-  io.value = a.value_in + r;
-  az_step<G>(a.cfg, a.sp, a.puct, root, sl, nodes, a.priors + r * static_cast<int64_t>(a.cap),
-             a.cap, bot, io, a.obs_size, a.num_actions);
-  sl.mt_idx = bot.idx;
-  sl.mt_pre = bot.pre;
-  if (*io.kind != kAzNone) {
-    atomicAdd(a.pending, 1);
-    return;
-  }
-  // Finished in this step: publish the root's children like the search kernels.
-  const int P0 = G::to_move(root);
-  const Node<double> rn = nodes[0];
-  const int nc = rn.nchild;
-  const int64_t ob = r * a.max_children;
-  for (int k = 0; k < nc && k < a.max_children; ++k) {
-    const Node<double> c = nodes[rn.first + k];
-    a.child_action[ob + k] = c.action;
-    a.child_n[ob + k] = c.n;
-    a.child_w[ob + k] = c.w;
-    a.child_out[ob + k] =
-        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
-  }
-  a.results[r] = sl.res;
-  a.nchild[r] = nc;
-  a.root_n[r] = rn.n;
-  a.root_w[r] = rn.w;
-  a.root_out[r] = rn.out == kUnsolved ? kUnsolved
-                                      : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
-  const int b = best_child(nodes, P0);
-  a.best_action[r] = b < 0 ? -1 : nodes[rn.first + b].action;
-}
-
-struct RollArgs {
-  GameCfg cfg;
-  int64_t n;
-  int32_t n_rollouts;
-  const void* root;  // one G::State
-  const uint32_t* seeds;
-  uint32_t* mt;      // [624][n] (k_rollouts, SoA) or [n][624]
-  uint64_t* glog;    // go: [kGoLogCap][n] position logs (k_rollouts, SoA)
-  double* out;       // [n][2]
-  const uint64_t* zob;
-  const uint64_t* root_hashes;
-  int32_t n_root_hashes;
-};
-
-template <class G>
-struct RollCtx {
-  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
-};
-template <>
-struct RollCtx<Go> {
-  __device__ static GoCtx make(const RollArgs& a, uint64_t* log) {
-    GoCtx c;
-    c.zob = a.zob;
-    c.base = a.root_hashes;
-    c.n_base = a.n_root_hashes;
-    c.log = log;
-    c.log_stride = static_cast<int32_t>(a.n);
-    c.n_log = 0;
-    c.cap = kGoLogCap;
-    c.init_filters();
-    return c;
-  }
-};
-
-template <class G>
-struct WaveRollCtx {
-  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
-};
-template <>
-struct WaveRollCtx<Go> {
-  __device__ static GoWaveCtx make(const RollArgs& a, uint64_t* log) {
-    GoWaveCtx c;
-    c.zob = a.zob;
-    c.base = a.root_hashes;
-    c.n_base = a.n_root_hashes;
-    c.log = log;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
-    c.init_filters();
-    return c;
-  }
-};
-
-// One wave per RandomRolloutEvaluator (n_rollouts playouts from the root).
-template <class G>
-__global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
-  const int64_t i = blockIdx.x;
-  if (i >= a.n) return;
-  __shared__ uint32_t mt[kMtN];
-  __shared__ uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
-  WaveMt ev;
-  ev.s = mt;
-  ev.use7 = SmallAbsl<G>::value ? 1 : 0;
-  if (lane_id() == 0) mt_seed(mt, a.seeds[i]);
-  __syncthreads();
-  ev.init_seeded();
-  typename WaveCtxOf<G>::type ctx = WaveRollCtx<G>::make(a, glog);
-  const typename G::State root = make_uniform(*static_cast<const typename G::State*>(a.root));
-  double s0 = 0.0, s1 = 0.0;
-  for (int k = 0; k < a.n_rollouts; ++k) {
-    ctx.reset();
-    const int r0 = wave_rollout<G, kPolicyCpp>(root, a.cfg, ctx, ev);
-    s0 += static_cast<double>(r0);
-    s1 += static_cast<double>(-r0);
-  }
-  if (lane_id() == 0) {
-    a.out[2 * i] = s0 / a.n_rollouts;
-    a.out[2 * i + 1] = s1 / a.n_rollouts;
-  }
-}
-
-// One lane per RandomRolloutEvaluator.  The lanes of a wave start together
-// and draw two words per move in lockstep, so the MT19937 states and go's
-// position logs are batch-SoA in HBM: one contiguous line per word / entry.
-template <class G>
-__global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  MtStreamSoA ev{a.mt + i, a.n, 0, 0};
-  ev.seed(a.seeds[i]);
-  typename G::Ctx ctx = RollCtx<G>::make(a, a.glog + i);
-  const typename G::State root = *static_cast<const typename G::State*>(a.root);
-  double s0 = 0.0, s1 = 0.0;
-  for (int k = 0; k < a.n_rollouts; ++k) {
-    ctx.reset();
-    const int r0 = rollout_ret0<G, kPolicyCpp>(root, a.cfg, ctx, ev);
-    s0 += static_cast<double>(r0);
-    s1 += static_cast<double>(-r0);
-  }
-  a.out[2 * i] = s0 / a.n_rollouts;
-  a.out[2 * i + 1] = s1 / a.n_rollouts;
-}
 
 // Root-parallel reduction: scatter each tree's root
 // children to a dense [R][A] action-indexed image, then sum every action's
@@ -772,94 +99,55 @@ __global__ __launch_bounds__(256) void k_outcome_counts(const double* out, int64
 
 }  // namespace
 
-// ---------------------------------------------------------------------------
-// Host engine
-namespace {
+DevArgs MakeArgs(os_engine* e) {
+  DevArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.sp.uct_c = e->params.uct_c;
+  a.sp.max_simulations = e->params.max_simulations;
+  a.sp.n_rollouts = e->params.n_rollouts;
+  a.sp.solve = e->params.solve;
+  // mcts.cc:201: max_nodes_ = (max_memory_mb << 20) / sizeof(SearchNode) + 1,
+  // with sizeof(SearchNode) == 80 on LP64 libstdc++ (SURVEY.md §8a M1).
+  const int64_t mn = (e->params.max_memory_mb << 20) / 80 + 1;
+  a.sp.max_nodes = static_cast<int32_t>(mn);
+  a.sp.policy = e->params.policy;
+  a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
+  a.roots = e->d_roots.p;
+  a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.eval_seeds = static_cast<const uint32_t*>(e->d_eseed.p);
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.arena = e->d_arena.p;
+  a.cap = e->cap;
+  // Paths hold depth + 1 <= MaxGameLength + 1 nodes; keep slices 4-byte even.
+  a.path_cap = e->game.cfg.max_game_length + 2;
+  a.child_cap = (e->game.cfg.max_children + 1) & ~1;
+  a.import_state = e->import_state ? 1 : 0;
+  a.shared_stream = e->shared_stream ? 1 : 0;
+  a.mt_pos = static_cast<int32_t*>(e->d_pos.p);
+  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+  a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
+  a.root_nhash = static_cast<const int32_t*>(e->d_rnh.p);
+  a.hash_stride = e->hash_stride;
+  a.results = static_cast<SearchResult*>(e->d_res.p);
+  a.max_children = e->max_children;
+  a.child_action = static_cast<int32_t*>(e->d_cact.p);
+  a.child_n = static_cast<int32_t*>(e->d_cn.p);
+  a.child_w = static_cast<double*>(e->d_cw.p);
+  a.child_out = static_cast<int8_t*>(e->d_cout.p);
+  a.nchild = static_cast<int32_t*>(e->d_nch.p);
+  a.root_n = static_cast<int32_t*>(e->d_rn.p);
+  a.root_w = static_cast<double*>(e->d_rw.p);
+  a.root_out = static_cast<int8_t*>(e->d_rout.p);
+  a.best_action = static_cast<int64_t*>(e->d_best.p);
+  return a;
+}
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  int ensure(size_t b) {
-    if (b <= bytes && p) return 0;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-    if (b == 0) return 0;
-    hipError_t e = hipMalloc(&p, b);
-    if (e != hipSuccess) {
-      p = nullptr;
-      return Fail(OS_ERR_DEVICE, std::string("hipMalloc(") + std::to_string(b) +
-                                     ") failed: " + hipGetErrorString(e));
-    }
-    bytes = b;
-    return 0;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-};
-
-}  // namespace
-
-struct os_engine {
-  HostGame game;
-  int device = 0;
-  // prepared run
-  os_mcts_params params{};
-  int64_t num_roots = 0;
-  int64_t chunk_roots = 0;
-  uint32_t cap = 0;
-  int node_bytes = 16;
-  int32_t max_children = 0;
-  int32_t hash_stride = 1;
-  bool import_state = false;
-  bool shared_stream = false;
-  int32_t rollout_layout = OS_LAYOUT_LANE;  // 4-140x faster than WAVE (profiles/r01)
-  // prepared rollout batch
-  int64_t roll_n = 0;
-  int32_t roll_nr = 1;
-  int32_t roll_nhash = 0;
-  bool roll_ready = false;
-  // prepared self-play batch
-  int64_t sp_games = 0;
-  int32_t sp_max_len = 0;
-  bool sp_visits = false;
-  bool sp_obs = false;
-  bool sp_ready = false;
-  // prepared external-evaluator batch (os_az_*): caller-owned device buffers
-  bool az_ready = false;
-  int32_t az_puct = 0;
-  int32_t* az_kind = nullptr;
-  float* az_obs = nullptr;
-  uint8_t* az_legal = nullptr;
-  const double* az_prior = nullptr;
-  const double* az_value = nullptr;
-  int32_t* az_pending = nullptr;
-  DevBuf d_az_slots, d_az_prior;
-  DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
-      d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
-      d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
-      d_sp_obs, d_glog;
-  std::vector<SearchResult> last_results;
-  int64_t last_sims = 0;
-  ~os_engine() {
-    DevBuf* all[] = {&d_roots, &d_bseed, &d_eseed, &d_mt,  &d_arena, &d_lut,
-                     &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
-                     &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
-                     &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
-                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
-                     &d_az_slots, &d_az_prior, &d_glog};
-    (void)hipSetDevice(device);
-    for (DevBuf* b : all) b->release();
-  }
-};
+}  // namespace osx
 
 namespace {
 
-template <class G>
-using StateOf = typename G::State;
+
 
 // Replays a history on the host; returns false if an action is illegal.
 bool ReplayRoot(const HostGame& g, const int64_t* a, int64_t n, HostState* s,
@@ -876,71 +164,10 @@ bool ReplayRoot(const HostGame& g, const int64_t* a, int64_t n, HostState* s,
   return true;
 }
 
-constexpr size_t kLdsBytes = 160 * 1024;  // LDS per CU on gfx950
-constexpr int kDefaultBlock = 16;           // searches (lanes) per workgroup
 
-template <class R>
-size_t LdsPerLane(int path_cap, int child_cap) {
-  return static_cast<size_t>(2 * kMtN * 4) + path_cap * sizeof(PathEnt<R>) +
-         static_cast<size_t>(child_cap) * 2;
-}
 
-template <class G, class R, int Policy>
-int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
-  const size_t lds = WaveLdsBytes<G, R>(a.path_cap);
-  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsearch<G, R, Policy>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds)));
-  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
-    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
-    a.root_base = base;
-    a.num_roots = n;
-    hipLaunchKernelGGL((k_wsearch<G, R, Policy>), dim3(static_cast<unsigned>(n)), dim3(64),
-                       lds, stream, a);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess)
-      return Fail(OS_ERR_DEVICE, std::string("k_wsearch launch failed: ") +
-                                     hipGetErrorString(err));
-  }
-  return OS_OK;
-}
 
-template <class G, class R, int Policy>
-int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
-  if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
-  int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
-  const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
-  if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
-  if (bs < 1) return Fail(OS_ERR_CAPACITY, "per-lane LDS slice exceeds the CU's LDS");
-  const size_t lds = per_lane * bs;
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mcts<G, R, Policy>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds)));
-  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
-    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
-    a.root_base = base;
-    a.num_roots = n;
-    const unsigned grid = static_cast<unsigned>((n + bs - 1) / bs);
-    hipLaunchKernelGGL((k_mcts<G, R, Policy>), dim3(grid), dim3(bs), lds, stream, a);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess)
-      return Fail(OS_ERR_DEVICE, std::string("k_mcts launch failed: ") +
-                                     hipGetErrorString(err));
-  }
-  return OS_OK;
-}
 
-template <class G>
-int LaunchForGame(os_engine* e, const DevArgs& a, hipStream_t stream) {
-  const bool dbl = e->params.n_rollouts != 1;
-  if (e->params.policy == OS_POLICY_NUMPY) {
-    return dbl ? LaunchSearch<G, double, kPolicyNumpy>(e, a, stream)
-               : LaunchSearch<G, int32_t, kPolicyNumpy>(e, a, stream);
-  }
-  return dbl ? LaunchSearch<G, double, kPolicyCpp>(e, a, stream)
-             : LaunchSearch<G, int32_t, kPolicyCpp>(e, a, stream);
-}
 
 int CheckParams(const os_engine* e, const os_mcts_params* p) {
   if (!p) return Fail(OS_ERR_INVALID, "null params");
@@ -1079,62 +306,13 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   return OS_OK;
 }
 
-DevArgs MakeArgs(os_engine* e) {
-  DevArgs a;
-  std::memset(&a, 0, sizeof a);
-  a.cfg = e->game.cfg;
-  a.sp.uct_c = e->params.uct_c;
-  a.sp.max_simulations = e->params.max_simulations;
-  a.sp.n_rollouts = e->params.n_rollouts;
-  a.sp.solve = e->params.solve;
-  // mcts.cc:201: max_nodes_ = (max_memory_mb << 20) / sizeof(SearchNode) + 1,
-  // with sizeof(SearchNode) == 80 on LP64 libstdc++ (SURVEY.md §8a M1).
-  const int64_t mn = (e->params.max_memory_mb << 20) / 80 + 1;
-  a.sp.max_nodes = static_cast<int32_t>(mn);
-  a.sp.policy = e->params.policy;
-  a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
-  a.roots = e->d_roots.p;
-  a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
-  a.eval_seeds = static_cast<const uint32_t*>(e->d_eseed.p);
-  a.mt = static_cast<uint32_t*>(e->d_mt.p);
-  a.arena = e->d_arena.p;
-  a.cap = e->cap;
-  // Paths hold depth + 1 <= MaxGameLength + 1 nodes; keep slices 4-byte even.
-  a.path_cap = e->game.cfg.max_game_length + 2;
-  a.child_cap = (e->game.cfg.max_children + 1) & ~1;
-  a.import_state = e->import_state ? 1 : 0;
-  a.shared_stream = e->shared_stream ? 1 : 0;
-  a.mt_pos = static_cast<int32_t*>(e->d_pos.p);
-  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
-  a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
-  a.root_nhash = static_cast<const int32_t*>(e->d_rnh.p);
-  a.hash_stride = e->hash_stride;
-  a.results = static_cast<SearchResult*>(e->d_res.p);
-  a.max_children = e->max_children;
-  a.child_action = static_cast<int32_t*>(e->d_cact.p);
-  a.child_n = static_cast<int32_t*>(e->d_cn.p);
-  a.child_w = static_cast<double*>(e->d_cw.p);
-  a.child_out = static_cast<int8_t*>(e->d_cout.p);
-  a.nchild = static_cast<int32_t*>(e->d_nch.p);
-  a.root_n = static_cast<int32_t*>(e->d_rn.p);
-  a.root_w = static_cast<double*>(e->d_rw.p);
-  a.root_out = static_cast<int8_t*>(e->d_rout.p);
-  a.best_action = static_cast<int64_t*>(e->d_best.p);
-  return a;
-}
 
 int Run(os_engine* e, hipStream_t stream) {
   HIP_TRY(hipSetDevice(e->device));
   if (e->num_roots == 0) return OS_OK;
-  DevArgs a = MakeArgs(e);
-  switch (e->game.cfg.kind) {
-    case kTicTacToe: return LaunchForGame<TicTacToe>(e, a, stream);
-    case kConnectFour: return LaunchForGame<ConnectFour>(e, a, stream);
-    case kBreakthrough: return LaunchForGame<Breakthrough>(e, a, stream);
-    case kHex: return LaunchForGame<Hex>(e, a, stream);
-    case kGo: return LaunchForGame<Go>(e, a, stream);
-  }
-  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  return L->search(e, MakeArgs(e), stream);
 }
 
 int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
@@ -1299,69 +477,14 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
   return OS_OK;
 }
 
-template <class G, class R>
-int SpLaunch(os_engine* e, hipStream_t stream) {
-  SpArgs a;
-  std::memset(&a, 0, sizeof a);
-  a.cfg = e->game.cfg;
-  a.sp.uct_c = e->params.uct_c;
-  a.sp.max_simulations = e->params.max_simulations;
-  a.sp.n_rollouts = e->params.n_rollouts;
-  a.sp.solve = e->params.solve;
-  a.sp.max_nodes = static_cast<int32_t>((e->params.max_memory_mb << 20) / 80 + 1);
-  a.sp.policy = kPolicyCpp;
-  a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
-  a.starts = e->d_roots.p;
-  a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
-  a.eval_seeds = static_cast<const uint32_t*>(e->d_eseed.p);
-  a.arena = e->d_arena.p;
-  a.cap = e->cap;
-  a.path_cap = e->game.cfg.max_game_length + 2;
-  a.max_len = e->sp_max_len;
-  a.num_actions = e->game.cfg.num_actions;
-  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
-  a.hist = static_cast<uint64_t*>(e->d_rhash.p);
-  a.hist_n = static_cast<int32_t*>(e->d_rnh.p);
-  a.hash_stride = e->hash_stride;
-  a.actions = static_cast<int32_t*>(e->d_sp_act.p);
-  a.length = static_cast<int32_t*>(e->d_sp_len.p);
-  a.returns = static_cast<double*>(e->d_sp_ret.p);
-  a.visits = e->sp_visits ? static_cast<int32_t*>(e->d_sp_vis.p) : nullptr;
-  a.obs = e->sp_obs ? static_cast<float*>(e->d_sp_obs.p) : nullptr;
-  a.obs_size = ObservationShape(e->game, nullptr);
-  a.results = static_cast<SearchResult*>(e->d_res.p);
-  const size_t lds = SelfPlayLdsBytes<G, R>(a.path_cap);
-  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "self-play LDS slice exceeds the CU's LDS");
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay<G, R>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds)));
-  for (int64_t base = 0; base < e->sp_games; base += e->chunk_roots) {
-    const int64_t n = std::min<int64_t>(e->chunk_roots, e->sp_games - base);
-    a.game_base = base;
-    a.num_games = n;
-    hipLaunchKernelGGL((k_wselfplay<G, R>), dim3(static_cast<unsigned>(n)), dim3(64), lds,
-                       stream, a);
-    HIP_TRY(hipGetLastError());
-  }
-  return OS_OK;
-}
 
 int SpRun(os_engine* e, hipStream_t stream) {
   if (!e->sp_ready) return Fail(OS_ERR_INVALID, "os_selfplay_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
   if (e->sp_games == 0) return OS_OK;
-  const bool dbl = e->params.n_rollouts != 1;
-  switch (e->game.cfg.kind) {
-#define OS_SP_CASE(K, G) \
-  case K: return dbl ? SpLaunch<G, double>(e, stream) : SpLaunch<G, int32_t>(e, stream);
-    OS_SP_CASE(kTicTacToe, TicTacToe)
-    OS_SP_CASE(kConnectFour, ConnectFour)
-    OS_SP_CASE(kBreakthrough, Breakthrough)
-    OS_SP_CASE(kHex, Hex)
-    OS_SP_CASE(kGo, Go)
-#undef OS_SP_CASE
-  }
-  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  return L->selfplay(e, stream);
 }
 
 int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
@@ -1407,9 +530,6 @@ int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
   return OS_OK;
 }
 
-// ---- external-evaluator search (os_az_*) ----
-template <class G>
-size_t AzSlotBytes() { return sizeof(AzSlot<G>); }
 
 int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
               const int64_t* root_actions, const int64_t* root_offsets,
@@ -1430,14 +550,9 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   if (rc) return rc;
   if (e->chunk_roots < R)
     return Fail(OS_ERR_CAPACITY, "external-evaluator searches must all fit in HBM at once");
-  size_t slot_bytes = 0;
-  switch (e->game.cfg.kind) {
-    case kTicTacToe: slot_bytes = AzSlotBytes<TicTacToe>(); break;
-    case kConnectFour: slot_bytes = AzSlotBytes<ConnectFour>(); break;
-    case kBreakthrough: slot_bytes = AzSlotBytes<Breakthrough>(); break;
-    case kHex: slot_bytes = AzSlotBytes<Hex>(); break;
-    default: return Fail(OS_ERR_UNSUPPORTED, "game");
-  }
+  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  if (!L || !L->az) return Fail(OS_ERR_UNSUPPORTED, "game");
+  const size_t slot_bytes = L->az_slot_bytes;
   const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
   if ((rc = e->d_az_slots.ensure(Rz * slot_bytes)) ||
       (rc = e->d_az_prior.ensure(Rz * static_cast<size_t>(e->cap) * 8)))
@@ -1454,61 +569,13 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   return OS_OK;
 }
 
-template <class G>
-int AzLaunch(os_engine* e, hipStream_t stream) {
-  AzArgs a;
-  std::memset(&a, 0, sizeof a);
-  const DevArgs d = MakeArgs(e);
-  a.cfg = d.cfg;
-  a.sp = d.sp;
-  a.puct = e->az_puct;
-  a.num_roots = e->num_roots;
-  a.roots = d.roots;
-  a.slots = e->d_az_slots.p;
-  a.arena = static_cast<Node<double>*>(e->d_arena.p);
-  a.priors = static_cast<double*>(e->d_az_prior.p);
-  a.cap = e->cap;
-  a.mt = static_cast<uint32_t*>(e->d_mt.p);
-  a.bot_seeds = d.bot_seeds;
-  a.obs_size = ObservationShape(e->game, nullptr);
-  a.num_actions = e->game.cfg.num_actions;
-  a.kind = e->az_kind;
-  a.obs = e->az_obs;
-  a.legal = e->az_legal;
-  a.prior_in = e->az_prior;
-  a.value_in = e->az_value;
-  a.pending = e->az_pending;
-  a.results = d.results;
-  a.max_children = d.max_children;
-  a.child_action = d.child_action;
-  a.child_n = d.child_n;
-  a.child_w = d.child_w;
-  a.child_out = d.child_out;
-  a.nchild = d.nchild;
-  a.root_n = d.root_n;
-  a.root_w = d.root_w;
-  a.root_out = d.root_out;
-  a.best_action = d.best_action;
-  HIP_TRY(hipMemsetAsync(e->az_pending, 0, sizeof(int32_t), stream));
-  if (e->num_roots == 0) return OS_OK;
-  const int bs = 64;
-  hipLaunchKernelGGL(k_az_step<G>, dim3(static_cast<unsigned>((e->num_roots + bs - 1) / bs)),
-                     dim3(bs), 0, stream, a);
-  HIP_TRY(hipGetLastError());
-  return OS_OK;
-}
 
 int AzStep(os_engine* e, hipStream_t stream) {
   if (!e->az_ready) return Fail(OS_ERR_INVALID, "os_az_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
-  switch (e->game.cfg.kind) {
-    case kTicTacToe: return AzLaunch<TicTacToe>(e, stream);
-    case kConnectFour: return AzLaunch<ConnectFour>(e, stream);
-    case kBreakthrough: return AzLaunch<Breakthrough>(e, stream);
-    case kHex: return AzLaunch<Hex>(e, stream);
-    default: break;
-  }
-  return Fail(OS_ERR_UNSUPPORTED, "game");
+  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  if (!L || !L->az) return Fail(OS_ERR_UNSUPPORTED, "game");
+  return L->az(e, stream);
 }
 
 // Uploads one root + n evaluator seeds for the rollout kernels.
@@ -1542,45 +609,14 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
   return OS_OK;
 }
 
-template <class G>
-int RollLaunch(os_engine* e, hipStream_t stream) {
-  RollArgs a;
-  std::memset(&a, 0, sizeof a);
-  a.cfg = e->game.cfg;
-  a.n = e->roll_n;
-  a.n_rollouts = e->roll_nr;
-  a.root = e->d_roots.p;
-  a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
-  a.mt = static_cast<uint32_t*>(e->d_mt.p);
-  a.glog = static_cast<uint64_t*>(e->d_glog.p);
-  a.out = static_cast<double*>(e->d_rollout_out.p);
-  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
-  a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
-  a.n_root_hashes = e->roll_nhash;
-  const int64_t n = e->roll_n;
-  if (e->rollout_layout == OS_LAYOUT_WAVE) {
-    hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream, a);
-  } else {
-    const int bs = 64;
-    hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                       dim3(bs), 0, stream, a);
-  }
-  HIP_TRY(hipGetLastError());
-  return OS_OK;
-}
 
 int RollRun(os_engine* e, hipStream_t stream) {
   if (!e->roll_ready) return Fail(OS_ERR_INVALID, "os_rollouts_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
   if (e->roll_n == 0) return OS_OK;
-  switch (e->game.cfg.kind) {
-    case kTicTacToe: return RollLaunch<TicTacToe>(e, stream);
-    case kConnectFour: return RollLaunch<ConnectFour>(e, stream);
-    case kBreakthrough: return RollLaunch<Breakthrough>(e, stream);
-    case kHex: return RollLaunch<Hex>(e, stream);
-    case kGo: return RollLaunch<Go>(e, stream);
-  }
-  return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  return L->rollouts(e, stream);
 }
 
 }  // namespace
@@ -1594,11 +630,14 @@ const char* os_last_error(void) { return g_err.c_str(); }
 int os_debug_phase_cycles(uint64_t* out, int32_t n) {
 #if OS_PHASE_TIMING
   if (!out || n < kNumPhases) return Fail(OS_ERR_INVALID, "need kNumPhases slots");
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(uint64_t) * kNumPhases));
-  std::vector<uint64_t> zero(kNumPhases, 0);
-  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero.data(),
-                            sizeof(uint64_t) * kNumPhases));
+  // Each game's kernels live in their own code object: sum the counters.
+  std::vector<uint64_t> acc(kNumPhases, 0), one(kNumPhases, 0);
+  for (int k = kTicTacToe; k <= kGo; ++k) {
+    const int rc = LaunchersFor(k)->phase_cycles(one.data(), true);
+    if (rc) return rc;
+    for (int i = 0; i < kNumPhases; ++i) acc[i] += one[i];
+  }
+  std::memcpy(out, acc.data(), sizeof(uint64_t) * kNumPhases);
   return kNumPhases;
 #else
   (void)out;

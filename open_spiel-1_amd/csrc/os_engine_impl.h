@@ -1,0 +1,276 @@
+// Engine internals shared by the host translation unit (os_engine.hip: the
+// C-ABI, batch preparation, result fetch) and the per-game kernel units
+// (os_game_*.hip, built in parallel): kernel argument blocks, device buffers,
+// the engine object, error reporting and the per-game launcher table.
+#ifndef OS_ENGINE_IMPL_H_
+#define OS_ENGINE_IMPL_H_
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/os_mcts.h"
+#include "os_az.h"
+#include "os_host.h"
+#include "os_mcts.h"
+#include "os_wave.h"
+
+namespace osx {
+using namespace osm;
+
+// Thread-local message of the last failed C-ABI call (os_last_error).
+extern thread_local std::string g_err;
+inline int Fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess)                                                    \
+      return ::osx::Fail(OS_ERR_DEVICE, std::string(#expr " failed: ") +    \
+                                            hipGetErrorString(_e));          \
+  } while (0)
+
+constexpr int kGoLogCap = 248;              // >= 2 * 11 * 11 + 4
+constexpr size_t kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
+constexpr int kDefaultBlock = 16;           // searches (lanes) per workgroup (lane layout)
+
+struct DevArgs {
+  GameCfg cfg;
+  SearchParams sp;
+  int64_t num_roots;      // roots in this launch
+  int64_t root_base;      // global index of the first root of this launch
+  const void* roots;      // [total] G::State
+  const uint32_t* bot_seeds;
+  const uint32_t* eval_seeds;
+  uint32_t* mt;           // [num_roots][2][624]
+  void* arena;            // [num_roots][cap] Node<R>
+  uint32_t cap;
+  int32_t path_cap;       // >= MaxGameLength + 1 (LDS path slice per lane)
+  int32_t child_cap;      // >= max |LegalActions| (LDS expansion slice)
+  int32_t import_state;   // numpy (key, pos) import / export
+  int32_t shared_stream;  // numpy: one RandomState for bot + evaluator
+  int32_t* mt_pos;        // [total][2] in/out when import_state
+  // go
+  const uint64_t* zob;
+  const uint64_t* root_hashes;  // [total][hash_stride]
+  const int32_t* root_nhash;    // [total]
+  int32_t hash_stride;
+  // outputs, indexed by global root
+  SearchResult* results;
+  int32_t max_children;
+  int32_t* child_action;
+  int32_t* child_n;
+  double* child_w;
+  int8_t* child_out;
+  int32_t* nchild;
+  int32_t* root_n;
+  double* root_w;
+  int8_t* root_out;
+  int64_t* best_action;
+};
+
+// ---------------------------------------------------------------------------
+// Self-play: one wave plays a whole game the way
+// examples/mcts_example.cc:77-136 PlayGame does with two MCTSBots sharing one
+// RandomRolloutEvaluator: every move is bots[CurrentPlayer]->Step(state) =
+// MCTSearch + BestChild (mcts.cc:219-226, 325-428), both bots' rng_ and the
+// shared evaluator's rng persist across moves.
+struct SpArgs {
+  GameCfg cfg;
+  SearchParams sp;
+  int64_t num_games;      // games in this launch
+  int64_t game_base;      // global index of the first game of this launch
+  const void* starts;     // [total] G::State
+  const uint32_t* bot_seeds;   // [total][2]
+  const uint32_t* eval_seeds;  // [total]
+  void* arena;            // [num_games][cap] Node<R>
+  uint32_t cap;
+  int32_t path_cap;
+  int32_t max_len;        // trajectory slots per game
+  int32_t num_actions;
+  // go: per-game position history (grows by one per move)
+  const uint64_t* zob;
+  uint64_t* hist;         // [total][hash_stride]
+  int32_t* hist_n;        // [total]
+  int32_t hash_stride;
+  // outputs
+  int32_t* actions;       // [total][max_len], -1 padded
+  int32_t* length;        // [total]
+  double* returns;        // [total][2]
+  int32_t* visits;        // [total][max_len][num_actions] or null
+  float* obs;             // [total][max_len][obs_size] or null
+  int32_t obs_size;       // C * H * W
+  SearchResult* results;  // [total], summed over the game's searches
+};
+
+// ---------------------------------------------------------------------------
+// External-evaluator MCTS (os_az.h): one lane per search, one step per launch.
+struct AzArgs {
+  GameCfg cfg;
+  SearchParams sp;
+  int32_t puct;
+  int64_t num_roots;
+  const void* roots;        // [R] G::State
+  void* slots;              // [R] AzSlot<G>
+  Node<double>* arena;      // [R][cap]
+  double* priors;           // [R][cap]
+  uint32_t cap;
+  uint32_t* mt;             // [R][624] bot rng
+  const uint32_t* bot_seeds;
+  int32_t obs_size;
+  int32_t num_actions;
+  int32_t* kind;            // [R]
+  float* obs;               // [R][obs_size]
+  uint8_t* legal;           // [R][A]
+  const double* prior_in;   // [R][A]
+  const double* value_in;   // [R]
+  int32_t* pending;         // requests written by this step
+  // outputs (same layout as the search kernels)
+  SearchResult* results;
+  int32_t max_children;
+  int32_t* child_action;
+  int32_t* child_n;
+  double* child_w;
+  int8_t* child_out;
+  int32_t* nchild;
+  int32_t* root_n;
+  double* root_w;
+  int8_t* root_out;
+  int64_t* best_action;
+};
+
+struct RollArgs {
+  GameCfg cfg;
+  int64_t n;
+  int32_t n_rollouts;
+  const void* root;  // one G::State
+  const uint32_t* seeds;
+  uint32_t* mt;      // [624][n] (k_rollouts, SoA) or [n][624]
+  uint64_t* glog;    // go: [kGoLogCap][n] position logs (k_rollouts, SoA)
+  double* out;       // [n][2]
+  const uint64_t* zob;
+  const uint64_t* root_hashes;
+  int32_t n_root_hashes;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t b) {
+    if (b <= bytes && p) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (b == 0) return 0;
+    hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return Fail(OS_ERR_DEVICE, std::string("hipMalloc(") + std::to_string(b) +
+                                     ") failed: " + hipGetErrorString(e));
+    }
+    bytes = b;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+}  // namespace osx
+
+struct os_engine {
+  osm::HostGame game;
+  int device = 0;
+  // prepared run
+  os_mcts_params params{};
+  int64_t num_roots = 0;
+  int64_t chunk_roots = 0;
+  uint32_t cap = 0;
+  int node_bytes = 16;
+  int32_t max_children = 0;
+  int32_t hash_stride = 1;
+  bool import_state = false;
+  bool shared_stream = false;
+  int32_t rollout_layout = OS_LAYOUT_LANE;  // 4-140x faster than WAVE (profiles/r01)
+  // prepared rollout batch
+  int64_t roll_n = 0;
+  int32_t roll_nr = 1;
+  int32_t roll_nhash = 0;
+  bool roll_ready = false;
+  // prepared self-play batch
+  int64_t sp_games = 0;
+  int32_t sp_max_len = 0;
+  bool sp_visits = false;
+  bool sp_obs = false;
+  bool sp_ready = false;
+  // prepared external-evaluator batch (os_az_*): caller-owned device buffers
+  bool az_ready = false;
+  int32_t az_puct = 0;
+  int32_t* az_kind = nullptr;
+  float* az_obs = nullptr;
+  uint8_t* az_legal = nullptr;
+  const double* az_prior = nullptr;
+  const double* az_value = nullptr;
+  int32_t* az_pending = nullptr;
+  osx::DevBuf d_az_slots, d_az_prior;
+  osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
+      d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
+      d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
+      d_sp_obs, d_glog;
+  std::vector<osm::SearchResult> last_results;
+  int64_t last_sims = 0;
+  ~os_engine() {
+    osx::DevBuf* all[] = {&d_roots, &d_bseed, &d_eseed, &d_mt,  &d_arena, &d_lut,
+                     &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
+                     &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
+                     &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
+                     &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
+                     &d_az_slots, &d_az_prior, &d_glog};
+    (void)hipSetDevice(device);
+    for (osx::DevBuf* b : all) b->release();
+  }
+};
+
+namespace osx {
+
+// Kernel arguments of the prepared search batch (os_engine.hip).
+DevArgs MakeArgs(os_engine* e);
+
+// Per-game entry points, defined by os_game_<name>.hip.
+struct GameLaunchers {
+  int (*search)(os_engine*, const DevArgs&, hipStream_t);  // k_wsearch / k_mcts
+  int (*selfplay)(os_engine*, hipStream_t);                // k_wselfplay
+  int (*az)(os_engine*, hipStream_t);                      // k_az_step, or null
+  int (*rollouts)(os_engine*, hipStream_t);                // k_rollouts / k_wrollouts
+  int (*phase_cycles)(uint64_t*, bool clear);              // OS_PHASE_TIMING builds
+  size_t az_slot_bytes;
+};
+extern GameLaunchers kTicTacToeLaunchers;
+extern GameLaunchers kConnectFourLaunchers;
+extern GameLaunchers kBreakthroughLaunchers;
+extern GameLaunchers kHexLaunchers;
+extern GameLaunchers kGoLaunchers;
+
+inline const GameLaunchers* LaunchersFor(int32_t kind) {
+  switch (kind) {
+    case kTicTacToe: return &kTicTacToeLaunchers;
+    case kConnectFour: return &kConnectFourLaunchers;
+    case kBreakthrough: return &kBreakthroughLaunchers;
+    case kHex: return &kHexLaunchers;
+    case kGo: return &kGoLaunchers;
+  }
+  return nullptr;
+}
+
+}  // namespace osx
+
+#endif  // OS_ENGINE_IMPL_H_

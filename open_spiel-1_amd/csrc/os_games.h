@@ -575,11 +575,29 @@ struct Go {
     if (s.ko >= 0) cand = cand & ~bit128(s.ko);
     const B128 has_lib = nbr4(E, g);
     B128 mask = cand & has_lib;
-    B128 hard = cand & ~has_lib;
-    while (any(hard)) {
-      const int p = lowest(hard);
-      hard = hard & ~bit128(p);
-      if (surrounded_legal(s, g, p, c, E)) mask = mask | bit128(p);
+    const B128 hard = cand & ~has_lib;
+    if (any(hard)) {
+      // A surrounded point is legal iff a neighbouring own chain keeps >= 2
+      // liberties or a neighbouring opponent chain is in atari (== the
+      // per-point surrounded_legal test).  Every chain next to any
+      // surrounded point is flooded once per move and classified; the legal
+      // points are then the surrounded points next to a qualifying chain.
+      const B128 own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+      const B128 ring = nbr4(hard, g);
+      B128 good = b128(0, 0);
+      B128 todo = ring & own;
+      while (any(todo)) {
+        const B128 ch = flood(bit128(lowest(todo)), own, g);
+        todo = todo & ~ch;
+        if (popc(nbr4(ch, g) & E) >= 2) good = good | ch;  // keeps a liberty
+      }
+      todo = ring & opp;
+      while (any(todo)) {
+        const B128 ch = flood(bit128(lowest(todo)), opp, g);
+        todo = todo & ~ch;
+        if (popc(nbr4(ch, g) & E) == 1) good = good | ch;  // atari
+      }
+      mask = mask | (hard & nbr4(good, g));
     }
     Legal l;
     l.mask = mask;

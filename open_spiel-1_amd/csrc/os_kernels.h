@@ -1,0 +1,778 @@
+// gfx950 kernels of the MCTS engine and their launchers, instantiated once per
+// game by os_game_<name>.hip (OS_DEFINE_LAUNCHERS).
+//
+//   k_wsearch   (OS_LAYOUT_WAVE): one 64-lane wavefront per search; game state
+//               wave-uniform in SGPRs, MT19937 streams + visit path in LDS
+//               (os_wave.h).
+//   k_mcts      (OS_LAYOUT_LANE): one lane per search; game state in VGPRs, MT
+//               streams + path / expansion buffers in LDS slices (os_mcts.h).
+//   k_wselfplay one wave plays a whole self-play game.
+//   k_az_step   external-evaluator search, one resumable step per launch.
+//   k_rollouts / k_wrollouts  RandomRolloutEvaluator batches.
+// Searches never share memory, so the search kernels use no atomics and are
+// bit-exact whatever the scheduling.
+#ifndef OS_KERNELS_H_
+#define OS_KERNELS_H_
+
+#include "os_engine_impl.h"
+
+namespace osx {
+
+
+
+#if OS_PHASE_TIMING
+__device__ uint64_t g_phase_cycles[kNumPhases];  // diagnostic build only (per game TU)
+#endif
+
+
+template <class G>
+struct CtxMaker;
+template <class G>
+struct CtxMaker {
+  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct CtxMaker<Go> {
+  __device__ static GoCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
+    GoCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = log;
+    c.log_stride = 1;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+
+template <class G, class R, int Policy>
+__global__ void k_mcts(DevArgs a) {
+  const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (lr >= a.num_roots) return;
+  const int64_t gr = a.root_base + lr;
+  // Per-lane LDS slices: [blockDim][2][624] MT19937 words, then
+  // [blockDim][path_cap] u32 visit path, then [blockDim][child_cap] u16
+  // expansion buffer.  Every per-simulation random word and path entry is an
+  // LDS access (~tens of cycles) instead of a dependent HBM/L2 round trip.
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int nb = blockDim.x;
+  const int lane = threadIdx.x;
+  uint32_t* mt0 = reinterpret_cast<uint32_t*>(smem) + lane * 2 * kMtN;
+  PathEnt<R>* path =
+      reinterpret_cast<PathEnt<R>*>(smem + static_cast<size_t>(nb) * 2 * kMtN * 4) +
+      lane * a.path_cap;
+  uint16_t* actbuf =
+      reinterpret_cast<uint16_t*>(
+          smem + static_cast<size_t>(nb) * (2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>))) +
+      lane * a.child_cap;
+  MtStream bot{mt0, kMtN, 0};
+  MtStream ev{mt0 + kMtN, kMtN, 0};
+  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
+  if (a.import_state) {
+    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = 0; i < 2 * kMtN; ++i) mt0[i] = g0[i];
+    bot.idx = a.mt_pos[2 * gr];
+    bot.pre = 1;
+    ev.idx = a.mt_pos[2 * gr + 1];
+    ev.pre = 1;
+  } else {
+    mt_seed(bot.s, a.bot_seeds[gr]);
+    if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
+  }
+  const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
+  uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
+  typename G::Ctx ctx = CtxMaker<G>::make(a, gr, glog);
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  SearchResult res;
+  if (Policy == kPolicyNumpy && a.shared_stream)
+    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
+                                    path, actbuf, a.path_cap);
+  else
+    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
+                                    path, actbuf, a.path_cap);
+  res.rng_words = bot.words + ((Policy == kPolicyNumpy && a.shared_stream) ? 0u : ev.words);
+  a.results[gr] = res;
+  const Node<R>& rn = nodes[0];
+  const int P0 = G::to_move(root);
+  const int nc = rn.nchild;
+  a.nchild[gr] = nc;
+  a.root_n[gr] = rn.n;
+  a.root_w[gr] = static_cast<double>(rn.w);
+  a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
+                                       : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+  const int64_t ob = gr * a.max_children;
+  for (int k = 0; k < nc && k < a.max_children; ++k) {
+    const Node<R>& c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = static_cast<double>(c.w);
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  const int b = best_child(nodes, P0);
+  a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+  if (a.import_state) {
+    bot.finalize();
+    a.mt_pos[2 * gr] = bot.idx;
+    if (!a.shared_stream) {
+      ev.finalize();
+      a.mt_pos[2 * gr + 1] = ev.idx;
+    }
+    uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = 0; i < 2 * kMtN; ++i) g0[i] = mt0[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-per-search kernel (default layout): one 64-lane workgroup per search.
+template <class G>
+struct WaveCtxMaker {
+  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct WaveCtxMaker<Go> {
+  __device__ static GoWaveCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+
+template <class G, class R>
+__host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
+  return static_cast<size_t>(2 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
+}
+
+// Minimum waves per SIMD requested from the register allocator (A/B knob).
+#ifndef OS_HEX_OCC
+#define OS_HEX_OCC 1
+#endif
+template <class G>
+struct WaveOcc {
+  static constexpr int value = 1;
+};
+template <>
+struct WaveOcc<Hex> {
+  static constexpr int value = OS_HEX_OCC;
+};
+
+template <class G, class R, int Policy>
+__global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
+  const int64_t lr = blockIdx.x;
+  if (lr >= a.num_roots) return;
+  const int64_t gr = a.root_base + lr;
+  const int l = lane_id();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4);
+  uint64_t* glog = reinterpret_cast<uint64_t*>(
+      smem + ((2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
+  WaveMt bot, ev;
+  bot.s = mt;
+  ev.s = mt + kMtN;
+  bot.use7 = 0;
+  ev.use7 = SmallAbsl<G>::value && Policy == kPolicyCpp && !shared ? 1 : 0;
+  if (a.import_state) {
+    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = l; i < 2 * kMtN; i += 64) mt[i] = g0[i];
+    __syncthreads();
+    bot.init_import(a.mt_pos[2 * gr]);
+    ev.init_import(a.mt_pos[2 * gr + 1]);
+  } else {
+    if (l == 0) {
+      mt_seed(bot.s, a.bot_seeds[gr]);
+      if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
+    }
+    __syncthreads();
+    bot.init_seeded();
+    ev.init_seeded();
+  }
+  const typename G::State root =
+      make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
+  typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr, glog);
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  PhaseCycles ph = {};
+  SearchResult res = shared
+      ? wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
+                                  a.path_cap, ph)
+      : wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                                  a.path_cap, ph);
+  res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
+#if OS_PHASE_TIMING
+  ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);
+  if (l == 0)
+    for (int i = 0; i < kNumPhases; ++i)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&g_phase_cycles[i]),
+                static_cast<unsigned long long>(ph.c[i]));
+#endif
+  __threadfence_block();
+  const Node<R> rn = nodes[0];
+  const int P0 = G::to_move(root);
+  const int nc = rn.nchild;
+  const int64_t ob = gr * a.max_children;
+  for (int k = l; k < nc && k < a.max_children; k += 64) {
+    const Node<R> c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = static_cast<double>(c.w);
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  if (l == 0) {
+    a.results[gr] = res;
+    a.nchild[gr] = nc;
+    a.root_n[gr] = rn.n;
+    a.root_w[gr] = static_cast<double>(rn.w);
+    a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
+                                         : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+    const int b = best_child(nodes, P0);
+    a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+  }
+  if (a.import_state) {
+    if (l == 0) {
+      a.mt_pos[2 * gr] = bot.export_pos();
+      if (!shared) a.mt_pos[2 * gr + 1] = ev.export_pos();
+    }
+    __syncthreads();
+    uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = l; i < 2 * kMtN; i += 64) g0[i] = mt[i];
+  }
+}
+
+
+template <class G>
+struct SpCtx {  // games without a history context
+  __device__ static NoCtx make(const SpArgs&, int64_t, uint64_t*) { return NoCtx(); }
+  __device__ static void commit(NoCtx&, const SpArgs&, int64_t) {}
+};
+template <>
+struct SpCtx<Go> {
+  __device__ static GoWaveCtx make(const SpArgs& a, int64_t gg, uint64_t* log) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.hist + gg * a.hash_stride;
+    c.n_base = a.hist_n[gg];
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+  // The move just applied logged its position (go.cc:199-208): append it to
+  // the game history that the next searches treat as "before the root".
+  __device__ static void commit(GoWaveCtx& c, const SpArgs& a, int64_t gg) {
+    uint64_t* h = a.hist + gg * a.hash_stride;
+    if (lane_id() == 0)
+      for (int i = 0; i < c.n_log && c.n_base + i < a.hash_stride; ++i) h[c.n_base + i] = c.log[i];
+    __threadfence_block();
+    c.n_base = c.n_base + c.n_log < a.hash_stride ? c.n_base + c.n_log : a.hash_stride;
+    c.init_filters();
+  }
+};
+
+template <class G, class R>
+__host__ __device__ constexpr size_t SelfPlayLdsBytes(int path_cap) {
+  return static_cast<size_t>(3 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
+}
+
+template <class G, class R>
+__global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
+  const int64_t lg = blockIdx.x;
+  if (lg >= a.num_games) return;
+  const int64_t gg = a.game_base + lg;
+  const int l = lane_id();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 3 * kMtN * 4);
+  uint64_t* glog = reinterpret_cast<uint64_t*>(
+      smem + ((3 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  WaveMt b0, b1, ev;
+  b0.s = mt;
+  b1.s = mt + kMtN;
+  ev.s = mt + 2 * kMtN;
+  b0.use7 = b1.use7 = 0;
+  ev.use7 = SmallAbsl<G>::value ? 1 : 0;
+  if (l == 0) {
+    mt_seed(b0.s, a.bot_seeds[2 * gg]);
+    mt_seed(b1.s, a.bot_seeds[2 * gg + 1]);
+    mt_seed(ev.s, a.eval_seeds[gg]);
+  }
+  __syncthreads();
+  b0.init_seeded();
+  b1.init_seeded();
+  ev.init_seeded();
+  typename G::State s = make_uniform(static_cast<const typename G::State*>(a.starts)[gg]);
+  typename WaveCtxOf<G>::type ctx = SpCtx<G>::make(a, gg, glog);
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lg * static_cast<int64_t>(a.cap);
+  PhaseCycles ph = {};
+  SearchResult tot;
+  tot.status = kOk;
+  tot.sims = tot.nodes = tot.gc_runs = tot.max_depth = 0;
+  tot.used = tot.scanned = tot.backed = tot.expanded = tot.solver_scanned = 0;
+  tot.rng_words = tot.pad = 0;
+  int m = 0;
+  while (!G::terminal(s, a.cfg)) {
+    if (m >= a.max_len) {
+      tot.status = kGameOverflow;
+      break;
+    }
+    const int p = G::to_move(s);
+    WaveMt bot = p == 0 ? b0 : b1;
+    const SearchResult r =
+        wave_search<G, R, kPolicyCpp>(a.cfg, a.sp, s, ctx, nodes, a.cap, bot, ev, path,
+                                      a.path_cap, ph);
+    if (p == 0) b0 = bot;
+    else b1 = bot;
+    tot.sims += r.sims;
+    tot.nodes += r.nodes;
+    tot.used = r.used > tot.used ? r.used : tot.used;
+    tot.gc_runs += r.gc_runs;
+    tot.max_depth = r.max_depth > tot.max_depth ? r.max_depth : tot.max_depth;
+    tot.scanned += r.scanned;
+    tot.backed += r.backed;
+    tot.expanded += r.expanded;
+    tot.solver_scanned += r.solver_scanned;
+    if (r.status != kOk) {
+      tot.status = r.status;
+      break;
+    }
+    __threadfence_block();
+    // MCTSBot::Step: BestChild of the root (mcts.cc:222-225).
+    int bi = 0;
+    if (l == 0) bi = best_child(nodes, p);
+    bi = rli(bi, 0);
+    const uint32_t rfirst = static_cast<uint32_t>(rli(static_cast<int>(nodes[0].first), 0));
+    const int rnc = rli(nodes[0].nchild, 0);
+    const int act = rli(nodes[rfirst + bi].action, 0);
+    if (a.visits) {
+      int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+      for (int i = l; i < a.num_actions; i += 64) v[i] = 0;
+      __threadfence_block();
+      for (int k = l; k < rnc; k += 64) {
+        const Node<R> c = nodes[rfirst + k];
+        v[c.action] = c.n;
+      }
+    }
+    if (a.obs) {  // ObservationTensor(player to move) of the position searched
+      float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
+      const int cells = a.cfg.rows * a.cfg.cols;
+      for (int i = l; i < a.obs_size; i += 64) o[i] = G::obs(s, a.cfg, p, i / cells, i % cells);
+    }
+    if (l == 0) a.actions[gg * a.max_len + m] = act;
+    ctx.reset();
+    G::apply(s, a.cfg, ctx, act);
+    SpCtx<G>::commit(ctx, a, gg);
+    s = make_uniform(s);
+    ++m;
+  }
+  tot.rng_words = b0.words.get() + b1.words.get() + ev.words.get();
+  for (int k = m + l; k < a.max_len; k += 64) a.actions[gg * a.max_len + k] = -1;
+  if (a.visits) {  // rows after the last move are all-zero policy targets
+    int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.num_actions;
+    for (int64_t i = l; i < nz; i += 64) v[i] = 0;
+  }
+  if (a.obs) {
+    float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
+    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.obs_size;
+    for (int64_t i = l; i < nz; i += 64) o[i] = 0.0f;
+  }
+  if (l == 0) {
+    const int r0 = G::terminal(s, a.cfg) ? G::ret0(s, a.cfg, ctx) : 0;
+    a.length[gg] = m;
+    a.returns[2 * gg] = static_cast<double>(r0);
+    a.returns[2 * gg + 1] = static_cast<double>(-r0);
+    a.results[gg] = tot;
+  }
+}
+
+
+template <class G>
+__global__ void k_az_step(AzArgs a) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= a.num_roots) return;
+  AzSlot<G>& sl = static_cast<AzSlot<G>*>(a.slots)[r];
+  const int stage0 = sl.stage;
+  if (stage0 == kAzDone) {
+    a.kind[r] = kAzNone;
+    return;
+  }
+  uint32_t* mt = a.mt + r * kMtN;
+  if (stage0 == kAzStart) {
+    mt_seed(mt, a.bot_seeds[r]);
+    sl.mt_idx = kMtN;
+    sl.mt_pre = 0;
+    sl.depth = 0;
+    sl.s = static_cast<const typename G::State*>(a.roots)[r];
+  }
+  MtStream bot{mt, sl.mt_idx, sl.mt_pre, 0};
+  const typename G::State root = static_cast<const typename G::State*>(a.roots)[r];
+  Node<double>* nodes = a.arena + r * static_cast<int64_t>(a.cap);
+  AzIo io;
+  io.kind = a.kind + r;
+  io.obs = a.obs + r * a.obs_size;
+  io.legal = a.legal + r * a.num_actions;
+  io.prior = a.prior_in + r * a.num_actions;
+  io.value = a.value_in + r;
+  az_step<G>(a.cfg, a.sp, a.puct, root, sl, nodes, a.priors + r * static_cast<int64_t>(a.cap),
+             a.cap, bot, io, a.obs_size, a.num_actions);
+  sl.mt_idx = bot.idx;
+  sl.mt_pre = bot.pre;
+  if (*io.kind != kAzNone) {
+    atomicAdd(a.pending, 1);
+    return;
+  }
+  // Finished in this step: publish the root's children like the search kernels.
+  const int P0 = G::to_move(root);
+  const Node<double> rn = nodes[0];
+  const int nc = rn.nchild;
+  const int64_t ob = r * a.max_children;
+  for (int k = 0; k < nc && k < a.max_children; ++k) {
+    const Node<double> c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = c.w;
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  a.results[r] = sl.res;
+  a.nchild[r] = nc;
+  a.root_n[r] = rn.n;
+  a.root_w[r] = rn.w;
+  a.root_out[r] = rn.out == kUnsolved ? kUnsolved
+                                      : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+  const int b = best_child(nodes, P0);
+  a.best_action[r] = b < 0 ? -1 : nodes[rn.first + b].action;
+}
+
+
+template <class G>
+struct RollCtx {
+  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct RollCtx<Go> {
+  __device__ static GoCtx make(const RollArgs& a, uint64_t* log) {
+    GoCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes;
+    c.n_base = a.n_root_hashes;
+    c.log = log;
+    c.log_stride = static_cast<int32_t>(a.n);
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+
+template <class G>
+struct WaveRollCtx {
+  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
+};
+template <>
+struct WaveRollCtx<Go> {
+  __device__ static GoWaveCtx make(const RollArgs& a, uint64_t* log) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes;
+    c.n_base = a.n_root_hashes;
+    c.log = log;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+
+// One wave per RandomRolloutEvaluator (n_rollouts playouts from the root).
+template <class G>
+__global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
+  const int64_t i = blockIdx.x;
+  if (i >= a.n) return;
+  __shared__ uint32_t mt[kMtN];
+  __shared__ uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
+  WaveMt ev;
+  ev.s = mt;
+  ev.use7 = SmallAbsl<G>::value ? 1 : 0;
+  if (lane_id() == 0) mt_seed(mt, a.seeds[i]);
+  __syncthreads();
+  ev.init_seeded();
+  typename WaveCtxOf<G>::type ctx = WaveRollCtx<G>::make(a, glog);
+  const typename G::State root = make_uniform(*static_cast<const typename G::State*>(a.root));
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < a.n_rollouts; ++k) {
+    ctx.reset();
+    const int r0 = wave_rollout<G, kPolicyCpp>(root, a.cfg, ctx, ev);
+    s0 += static_cast<double>(r0);
+    s1 += static_cast<double>(-r0);
+  }
+  if (lane_id() == 0) {
+    a.out[2 * i] = s0 / a.n_rollouts;
+    a.out[2 * i + 1] = s1 / a.n_rollouts;
+  }
+}
+
+// One lane per RandomRolloutEvaluator.  The lanes of a wave start together
+// and draw two words per move in lockstep, so the MT19937 states and go's
+// position logs are batch-SoA in HBM: one contiguous line per word / entry.
+template <class G>
+__global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  MtStreamSoA ev{a.mt + i, a.n, 0, 0};
+  ev.seed(a.seeds[i]);
+  typename G::Ctx ctx = RollCtx<G>::make(a, a.glog + i);
+  const typename G::State root = *static_cast<const typename G::State*>(a.root);
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = 0; k < a.n_rollouts; ++k) {
+    ctx.reset();
+    const int r0 = rollout_ret0<G, kPolicyCpp>(root, a.cfg, ctx, ev);
+    s0 += static_cast<double>(r0);
+    s1 += static_cast<double>(-r0);
+  }
+  a.out[2 * i] = s0 / a.n_rollouts;
+  a.out[2 * i + 1] = s1 / a.n_rollouts;
+}
+
+
+
+
+
+// ---------------------------------------------------------------------------
+// Launchers (host side of this game's kernels)
+
+template <class R>
+size_t LdsPerLane(int path_cap, int child_cap) {
+  return static_cast<size_t>(2 * kMtN * 4) + path_cap * sizeof(PathEnt<R>) +
+         static_cast<size_t>(child_cap) * 2;
+}
+
+template <class G, class R, int Policy>
+int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
+  const size_t lds = WaveLdsBytes<G, R>(a.path_cap);
+  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsearch<G, R, Policy>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)));
+  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+    a.root_base = base;
+    a.num_roots = n;
+    hipLaunchKernelGGL((k_wsearch<G, R, Policy>), dim3(static_cast<unsigned>(n)), dim3(64),
+                       lds, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+      return Fail(OS_ERR_DEVICE, std::string("k_wsearch launch failed: ") +
+                                     hipGetErrorString(err));
+  }
+  return OS_OK;
+}
+
+template <class G, class R, int Policy>
+int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
+  if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
+  int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
+  const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
+  if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
+  if (bs < 1) return Fail(OS_ERR_CAPACITY, "per-lane LDS slice exceeds the CU's LDS");
+  const size_t lds = per_lane * bs;
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mcts<G, R, Policy>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)));
+  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+    a.root_base = base;
+    a.num_roots = n;
+    const unsigned grid = static_cast<unsigned>((n + bs - 1) / bs);
+    hipLaunchKernelGGL((k_mcts<G, R, Policy>), dim3(grid), dim3(bs), lds, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+      return Fail(OS_ERR_DEVICE, std::string("k_mcts launch failed: ") +
+                                     hipGetErrorString(err));
+  }
+  return OS_OK;
+}
+
+template <class G>
+int LaunchForGame(os_engine* e, const DevArgs& a, hipStream_t stream) {
+  const bool dbl = e->params.n_rollouts != 1;
+  if (e->params.policy == OS_POLICY_NUMPY) {
+    return dbl ? LaunchSearch<G, double, kPolicyNumpy>(e, a, stream)
+               : LaunchSearch<G, int32_t, kPolicyNumpy>(e, a, stream);
+  }
+  return dbl ? LaunchSearch<G, double, kPolicyCpp>(e, a, stream)
+             : LaunchSearch<G, int32_t, kPolicyCpp>(e, a, stream);
+}
+
+template <class G, class R>
+int SpLaunch(os_engine* e, hipStream_t stream) {
+  SpArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.sp.uct_c = e->params.uct_c;
+  a.sp.max_simulations = e->params.max_simulations;
+  a.sp.n_rollouts = e->params.n_rollouts;
+  a.sp.solve = e->params.solve;
+  a.sp.max_nodes = static_cast<int32_t>((e->params.max_memory_mb << 20) / 80 + 1);
+  a.sp.policy = kPolicyCpp;
+  a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
+  a.starts = e->d_roots.p;
+  a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.eval_seeds = static_cast<const uint32_t*>(e->d_eseed.p);
+  a.arena = e->d_arena.p;
+  a.cap = e->cap;
+  a.path_cap = e->game.cfg.max_game_length + 2;
+  a.max_len = e->sp_max_len;
+  a.num_actions = e->game.cfg.num_actions;
+  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+  a.hist = static_cast<uint64_t*>(e->d_rhash.p);
+  a.hist_n = static_cast<int32_t*>(e->d_rnh.p);
+  a.hash_stride = e->hash_stride;
+  a.actions = static_cast<int32_t*>(e->d_sp_act.p);
+  a.length = static_cast<int32_t*>(e->d_sp_len.p);
+  a.returns = static_cast<double*>(e->d_sp_ret.p);
+  a.visits = e->sp_visits ? static_cast<int32_t*>(e->d_sp_vis.p) : nullptr;
+  a.obs = e->sp_obs ? static_cast<float*>(e->d_sp_obs.p) : nullptr;
+  a.obs_size = ObservationShape(e->game, nullptr);
+  a.results = static_cast<SearchResult*>(e->d_res.p);
+  const size_t lds = SelfPlayLdsBytes<G, R>(a.path_cap);
+  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "self-play LDS slice exceeds the CU's LDS");
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay<G, R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds)));
+  for (int64_t base = 0; base < e->sp_games; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->sp_games - base);
+    a.game_base = base;
+    a.num_games = n;
+    hipLaunchKernelGGL((k_wselfplay<G, R>), dim3(static_cast<unsigned>(n)), dim3(64), lds,
+                       stream, a);
+    HIP_TRY(hipGetLastError());
+  }
+  return OS_OK;
+}
+
+// ---- external-evaluator search (os_az_*) ----
+template <class G>
+size_t AzSlotBytes() { return sizeof(AzSlot<G>); }
+
+template <class G>
+int AzLaunch(os_engine* e, hipStream_t stream) {
+  AzArgs a;
+  std::memset(&a, 0, sizeof a);
+  const DevArgs d = MakeArgs(e);
+  a.cfg = d.cfg;
+  a.sp = d.sp;
+  a.puct = e->az_puct;
+  a.num_roots = e->num_roots;
+  a.roots = d.roots;
+  a.slots = e->d_az_slots.p;
+  a.arena = static_cast<Node<double>*>(e->d_arena.p);
+  a.priors = static_cast<double*>(e->d_az_prior.p);
+  a.cap = e->cap;
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.bot_seeds = d.bot_seeds;
+  a.obs_size = ObservationShape(e->game, nullptr);
+  a.num_actions = e->game.cfg.num_actions;
+  a.kind = e->az_kind;
+  a.obs = e->az_obs;
+  a.legal = e->az_legal;
+  a.prior_in = e->az_prior;
+  a.value_in = e->az_value;
+  a.pending = e->az_pending;
+  a.results = d.results;
+  a.max_children = d.max_children;
+  a.child_action = d.child_action;
+  a.child_n = d.child_n;
+  a.child_w = d.child_w;
+  a.child_out = d.child_out;
+  a.nchild = d.nchild;
+  a.root_n = d.root_n;
+  a.root_w = d.root_w;
+  a.root_out = d.root_out;
+  a.best_action = d.best_action;
+  HIP_TRY(hipMemsetAsync(e->az_pending, 0, sizeof(int32_t), stream));
+  if (e->num_roots == 0) return OS_OK;
+  const int bs = 64;
+  hipLaunchKernelGGL(k_az_step<G>, dim3(static_cast<unsigned>((e->num_roots + bs - 1) / bs)),
+                     dim3(bs), 0, stream, a);
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
+}
+
+template <class G>
+int RollLaunch(os_engine* e, hipStream_t stream) {
+  RollArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.cfg = e->game.cfg;
+  a.n = e->roll_n;
+  a.n_rollouts = e->roll_nr;
+  a.root = e->d_roots.p;
+  a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
+  a.mt = static_cast<uint32_t*>(e->d_mt.p);
+  a.glog = static_cast<uint64_t*>(e->d_glog.p);
+  a.out = static_cast<double*>(e->d_rollout_out.p);
+  a.zob = static_cast<const uint64_t*>(e->d_zob.p);
+  a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
+  a.n_root_hashes = e->roll_nhash;
+  const int64_t n = e->roll_n;
+  if (e->rollout_layout == OS_LAYOUT_WAVE) {
+    hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream, a);
+  } else {
+    const int bs = 64;
+    hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
+                       dim3(bs), 0, stream, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
+}
+
+#if OS_PHASE_TIMING
+inline int PhaseCycles(uint64_t* out, bool clear) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(uint64_t) * kNumPhases));
+  if (clear) {
+    std::vector<uint64_t> zero(kNumPhases, 0);
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero.data(),
+                              sizeof(uint64_t) * kNumPhases));
+  }
+  return OS_OK;
+}
+#else
+inline int PhaseCycles(uint64_t*, bool) {
+  return Fail(OS_ERR_UNSUPPORTED, "built without -DOS_PHASE_TIMING=1");
+}
+#endif
+
+template <class G>
+int SelfPlayEntry(os_engine* e, hipStream_t stream) {
+  return e->params.n_rollouts != 1 ? SpLaunch<G, double>(e, stream)
+                                   : SpLaunch<G, int32_t>(e, stream);
+}
+
+}  // namespace osx
+
+// Defines osx::k<G>Launchers for game G; WITH_AZ = 0 leaves the external-
+// evaluator search unsupported for it.
+// A non-const host variable: the device pass instantiates the launch code
+// (and so every kernel it launches) but does not emit the table itself.
+#define OS_DEFINE_LAUNCHERS(G, WITH_AZ)                                          \
+  namespace osx {                                                                \
+  extern GameLaunchers k##G##Launchers;                                          \
+  GameLaunchers k##G##Launchers = {                                              \
+      &LaunchForGame<G>, &SelfPlayEntry<G>, (WITH_AZ) ? &AzLaunch<G> : nullptr,  \
+      &RollLaunch<G>, &PhaseCycles, (WITH_AZ) ? AzSlotBytes<G>() : 0};           \
+  }
+
+#endif  // OS_KERNELS_H_
