@@ -126,6 +126,102 @@ OS_HD B128 lowmask128(int n) {
   return b128(~0ull, ~0ull);
 }
 
+// 384-bit bitboard (six u64 words) for boards above 11 x 11 (hex, go up to
+// 19 x 19).  Same operations as B128; every loop is unrolled, so the words
+// are only ever indexed by constants.
+struct B384 {
+  uint64_t w[6];
+};
+#define OS_B384_MAP(expr) \
+  B384 r;                  \
+  _Pragma("unroll") for (int i = 0; i < 6; ++i) r.w[i] = (expr); \
+  return r
+OS_HD B384 operator|(B384 a, B384 b) { OS_B384_MAP(a.w[i] | b.w[i]); }
+OS_HD B384 operator&(B384 a, B384 b) { OS_B384_MAP(a.w[i] & b.w[i]); }
+OS_HD B384 operator^(B384 a, B384 b) { OS_B384_MAP(a.w[i] ^ b.w[i]); }
+OS_HD B384 operator~(B384 a) { OS_B384_MAP(~a.w[i]); }
+OS_HD bool operator==(B384 a, B384 b) {
+  uint64_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) d |= a.w[i] ^ b.w[i];
+  return d == 0;
+}
+OS_HD bool operator!=(B384 a, B384 b) { return !(a == b); }
+OS_HD bool any(B384 a) {
+  uint64_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) d |= a.w[i];
+  return d != 0;
+}
+OS_HD int popc(B384 a) {
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c += popc64(a.w[i]);
+  return c;
+}
+OS_HD B384 shl(B384 a, int s) {  // 0 < s < 64
+  OS_B384_MAP((a.w[i] << s) | (i ? a.w[i ? i - 1 : 0] >> (64 - s) : 0ull));
+}
+OS_HD B384 shr(B384 a, int s) {  // 0 < s < 64
+  OS_B384_MAP((a.w[i] >> s) | (i < 5 ? a.w[i < 5 ? i + 1 : 5] << (64 - s) : 0ull));
+}
+OS_HD B384 sel384(bool c, B384 x, B384 y) { OS_B384_MAP(c ? x.w[i] : y.w[i]); }
+OS_HD B384 bit384(int b) { OS_B384_MAP((b >> 6) == i ? (1ull << (b & 63)) : 0ull); }
+OS_HD bool test(B384 a, int b) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v |= (b >> 6) == i ? a.w[i] : 0ull;
+  return (v >> (b & 63)) & 1;
+}
+OS_HD int lowest(B384 a) {  // a != 0
+  int r = -1;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) r = a.w[i] ? 64 * i + ctz64(a.w[i]) : r;
+  return r;
+}
+OS_HD int select384(B384 a, int k) {  // k < popc(a)
+  int r = -1;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int c = popc64(a.w[i]);
+    if (r < 0 && k < c) r = 64 * i + select64(a.w[i], k);
+    k -= c;
+  }
+  return r;
+}
+OS_HD B384 lowmask384(int n) {  // 0 <= n <= 384
+  OS_B384_MAP(n >= 64 * (i + 1) ? ~0ull : (n <= 64 * i ? 0ull : (1ull << (n - 64 * i)) - 1));
+}
+#undef OS_B384_MAP
+OS_HD B384 pick(const B384* a, int i) { return sel384(i != 0, a[1], a[0]); }
+OS_HD void put(B384* a, int i, B384 v) {
+  const B384 v0 = sel384(i != 0, a[0], v), v1 = sel384(i != 0, v, a[1]);
+  a[0] = v0;
+  a[1] = v1;
+}
+
+// Bitboard-width-generic constructors for the game templates (os_games.h).
+template <class B>
+struct BB;
+template <>
+struct BB<B128> {
+  static constexpr int kBits = 128;
+  OS_HD static B128 zero() { return b128(0, 0); }
+  OS_HD static B128 bit(int i) { return bit128(i); }
+  OS_HD static B128 lowmask(int n) { return lowmask128(n); }
+  OS_HD static int select(B128 a, int k) { return select128(a, k); }
+  OS_HD static B128 sel(bool c, B128 x, B128 y) { return sel128(c, x, y); }
+};
+template <>
+struct BB<B384> {
+  static constexpr int kBits = 384;
+  OS_HD static B384 zero() { return lowmask384(0); }
+  OS_HD static B384 bit(int i) { return bit384(i); }
+  OS_HD static B384 lowmask(int n) { return lowmask384(n); }
+  OS_HD static int select(B384 a, int k) { return select384(a, k); }
+  OS_HD static B384 sel(bool c, B384 x, B384 y) { return sel384(c, x, y); }
+};
+
 }  // namespace osm
 
 #endif  // OS_COMMON_H_

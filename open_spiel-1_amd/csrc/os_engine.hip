@@ -764,6 +764,11 @@ int os_engine_create(const char* game_string, int32_t device, os_engine** out) {
   bool unsupported = false;
   std::string err = LoadHostGame(game_string, &e->game, &unsupported);
   if (!err.empty()) return Fail(unsupported ? OS_ERR_UNSUPPORTED : OS_ERR_INVALID, err);
+  const GameCfg& cfg = e->game.cfg;
+  if ((cfg.kind == kHex || cfg.kind == kGo) && cfg.rows > kB128Side)
+    return Fail(OS_ERR_UNSUPPORTED,
+                "the device engine runs hex / go up to 11 x 11 (B128 bitboards); larger "
+                "boards are supported by the State API only");
   int ndev = 0;
   hipError_t he = hipGetDeviceCount(&ndev);
   if (he != hipSuccess || ndev == 0)

@@ -49,6 +49,28 @@ struct GameCfg {
   // where the reference's wrap filter (hex.cc:206-222) also drops the genuine
   // left/right and diagonal neighbours, leaving only up/down.
   B128 hex_a, hex_b;
+  // The same masks for boards above 11 x 11 (B384; host State API only).
+  B384 big_board, big_notcol0, big_notcollast, big_hex_a, big_hex_b;
+};
+
+// Board masks of a GameCfg for the bitboard width B.
+template <class B>
+struct CfgMasks;
+template <>
+struct CfgMasks<B128> {
+  OS_HD static const B128& board(const GameCfg& g) { return g.board; }
+  OS_HD static const B128& notcol0(const GameCfg& g) { return g.notcol0; }
+  OS_HD static const B128& notcollast(const GameCfg& g) { return g.notcollast; }
+  OS_HD static const B128& hex_a(const GameCfg& g) { return g.hex_a; }
+  OS_HD static const B128& hex_b(const GameCfg& g) { return g.hex_b; }
+};
+template <>
+struct CfgMasks<B384> {
+  OS_HD static const B384& board(const GameCfg& g) { return g.big_board; }
+  OS_HD static const B384& notcol0(const GameCfg& g) { return g.big_notcol0; }
+  OS_HD static const B384& notcollast(const GameCfg& g) { return g.big_notcollast; }
+  OS_HD static const B384& hex_a(const GameCfg& g) { return g.big_hex_a; }
+  OS_HD static const B384& hex_b(const GameCfg& g) { return g.big_hex_b; }
 };
 
 struct NoCtx {
@@ -315,11 +337,13 @@ struct Breakthrough {
 // north-south, white west-east.  Per player: stones, and the stones whose
 // group touches edge A (north / west) or edge B (south / east) -- the bitboard
 // form of the reference's per-cell edge labels (hex.cc:55-134, flood :149-184).
-struct Hex {
+template <class B>
+struct HexT {
+  using M = CfgMasks<B>;
   struct State {
-    B128 st[2];
-    B128 ea[2];
-    B128 eb[2];
+    B st[2];
+    B ea[2];
+    B eb[2];
     int16_t win_cell;  // -1 none
     int8_t result;     // +1 black won, -1 white won, 0 running
     uint8_t to_play;
@@ -329,26 +353,26 @@ struct Hex {
   };
   using Ctx = NoCtx;
   struct Legal {
-    B128 mask;
+    B mask;
     int count;
-    OS_HD int kth(int k) const { return select128(mask, k); }
+    OS_HD int kth(int k) const { return BB<B>::select(mask, k); }
   };
-  OS_HD static B128 nbr6(B128 x, const GameCfg& g) {
+  OS_HD static B nbr6(B x, const GameCfg& g) {
     const int n = g.rows;
-    B128 r = shr(x, n) | (shr(x, n - 1) & g.hex_a) | (shr(x, 1) & g.hex_b) |
-             (shl(x, 1) & g.hex_a) | (shl(x, n - 1) & g.hex_b) | shl(x, n);
-    return r & g.board;
+    B r = shr(x, n) | (shr(x, n - 1) & M::hex_a(g)) | (shr(x, 1) & M::hex_b(g)) |
+             (shl(x, 1) & M::hex_a(g)) | (shl(x, n - 1) & M::hex_b(g)) | shl(x, n);
+    return r & M::board(g);
   }
   OS_HD static void init(State& s, const GameCfg&) {
-    s.st[0] = s.ea[0] = s.eb[0] = b128(0, 0);
-    s.st[1] = s.ea[1] = s.eb[1] = b128(0, 0);
+    s.st[0] = s.ea[0] = s.eb[0] = BB<B>::zero();
+    s.st[1] = s.ea[1] = s.eb[1] = BB<B>::zero();
     s.win_cell = -1; s.result = 0; s.to_play = 0; s.moves = 0; s.pad = 0;
   }
   OS_HD static bool terminal(const State& s, const GameCfg&) { return s.result != 0; }
   OS_HD static int to_move(const State& s) { return s.to_play; }
   OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
     Legal l;
-    l.mask = g.board & ~(s.st[0] | s.st[1]);
+    l.mask = M::board(g) & ~(s.st[0] | s.st[1]);
     l.count = popc(l.mask);
     return l;
   }
@@ -364,7 +388,7 @@ struct Hex {
       ea = (m % n) == 0;
       eb = !ea && (m % n) == n - 1;
     }
-    const B128 nb = nbr6(bit128(m), g);
+    const B nb = nbr6(BB<B>::bit(m), g);
     ea |= any(nb & pick(s.ea, p));
     eb |= any(nb & pick(s.eb, p));
     *a = ea;
@@ -374,25 +398,25 @@ struct Hex {
     const int p = s.to_play;
     bool a, b;
     edges_if(s, g, p, m, &a, &b);
-    const B128 mb = bit128(m);
-    const B128 st = pick(s.st, p) | mb;
+    const B mb = BB<B>::bit(m);
+    const B st = pick(s.st, p) | mb;
     put(s.st, p, st);
     if (a && b) {
       s.result = static_cast<int8_t>(p == 0 ? 1 : -1);
       s.win_cell = static_cast<int16_t>(m);
     } else if (a || b) {
-      const B128 ea = pick(s.ea, p), eb = pick(s.eb, p);
-      const B128 plain = st & ~ea & ~eb;
-      B128 comp = mb;
+      const B ea = pick(s.ea, p), eb = pick(s.eb, p);
+      const B plain = st & ~ea & ~eb;
+      B comp = mb;
       for (;;) {
-        B128 nx = comp | (nbr6(comp, g) & plain);
+        B nx = comp | (nbr6(comp, g) & plain);
         if (nx == comp) break;
         comp = nx;
       }
       // Both pairs are written on this path (no store sinking through a
       // pointer phi, which would pin the state in scratch).
-      put(s.ea, p, sel128(a, ea | comp, ea));
-      put(s.eb, p, sel128(a, eb, eb | comp));
+      put(s.ea, p, BB<B>::sel(a, ea | comp, ea));
+      put(s.eb, p, BB<B>::sel(a, eb, eb | comp));
     }
     s.to_play = static_cast<uint8_t>(1 - p);
     s.moves++;
@@ -415,6 +439,8 @@ struct Hex {
     return plane == want ? 1.0f : 0.0f;
   }
 };
+using Hex = HexT<B128>;
+using HexBig = HexT<B384>;  // board_size 12..19 (host State API)
 
 // ----------------------------------------------------------------------------
 // Go: n x n <= 121 cells (board_size <= 11), row-major bit = row * n + col
@@ -497,9 +523,11 @@ struct GoCtx {
   }
 };
 
-struct Go {
+template <class B>
+struct GoT {
+  using M = CfgMasks<B>;
   struct State {
-    B128 bw[2];     // black, white stones
+    B bw[2];     // black, white stones
     uint64_t hash;  // Zobrist hash of the stones
     int16_t ko;     // ko cell or -1
     uint16_t moves; // history length (since the empty board)
@@ -511,15 +539,15 @@ struct Go {
   using Ctx = GoCtx;
   static constexpr uint8_t kSuperko = 1, kLastPass = 2, kPrevPass = 4;
 
-  OS_HD static B128 nbr4(B128 x, const GameCfg& g) {
+  OS_HD static B nbr4(B x, const GameCfg& g) {
     const int n = g.rows;
-    B128 r = shl(x, n) | shr(x, n) | (shl(x, 1) & g.notcol0) | (shr(x, 1) & g.notcollast);
-    return r & g.board;
+    B r = shl(x, n) | shr(x, n) | (shl(x, 1) & M::notcol0(g)) | (shr(x, 1) & M::notcollast(g));
+    return r & M::board(g);
   }
-  OS_HD static B128 flood(B128 seed, B128 within, const GameCfg& g) {
-    B128 c = seed;
+  OS_HD static B flood(B seed, B within, const GameCfg& g) {
+    B c = seed;
     for (;;) {
-      B128 nx = (c | nbr4(c, g)) & within;
+      B nx = (c | nbr4(c, g)) & within;
       if (nx == c) return c;
       c = nx;
     }
@@ -527,38 +555,38 @@ struct Go {
   // Whether empty cell p with no empty neighbour is a legal move for player c
   // (go_board.cc:425-440).
   OS_HD static bool surrounded_legal(const State& s, const GameCfg& g, int p, int c,
-                                     B128 E) {
-    const B128 own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-    B128 nb = nbr4(bit128(p), g);
-    B128 on = nb & own;
+                                     B E) {
+    const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+    B nb = nbr4(BB<B>::bit(p), g);
+    B on = nb & own;
     while (any(on)) {  // joins an own chain that keeps a liberty
       const int q = lowest(on);
-      const B128 ch = flood(bit128(q), own, g);
-      const B128 libs = nbr4(ch, g) & E;
+      const B ch = flood(BB<B>::bit(q), own, g);
+      const B libs = nbr4(ch, g) & E;
       if (popc(libs) >= 2) return true;
       on = on & ~ch;
     }
-    B128 opn = nb & opp;
+    B opn = nb & opp;
     while (any(opn)) {  // captures an opponent chain in atari
       const int q = lowest(opn);
-      const B128 ch = flood(bit128(q), opp, g);
-      const B128 libs = nbr4(ch, g) & E;
+      const B ch = flood(BB<B>::bit(q), opp, g);
+      const B libs = nbr4(ch, g) & E;
       if (popc(libs) == 1) return true;
       opn = opn & ~ch;
     }
     return false;
   }
   struct Legal {
-    B128 mask;  // legal board points (pass excluded)
+    B mask;  // legal board points (pass excluded)
     int count;  // including pass
     int pass_action;
     OS_HD int kth(int k) const {
       const int c = count - 1;
-      return k < c ? select128(mask, k) : pass_action;
+      return k < c ? BB<B>::select(mask, k) : pass_action;
     }
   };
   OS_HD static void init(State& s, const GameCfg&) {
-    s.bw[0] = s.bw[1] = b128(0, 0);
+    s.bw[0] = s.bw[1] = BB<B>::zero();
     s.hash = 0; s.ko = -1; s.moves = 0; s.to_play = 0; s.flags = 0; s.pad = 0;
   }
   OS_HD static bool terminal(const State& s, const GameCfg& g) {
@@ -570,30 +598,30 @@ struct Go {
   template <class C>
   OS_HD static Legal legal(const State& s, const GameCfg& g, C&) {
     const int c = s.to_play;
-    const B128 E = g.board & ~(s.bw[0] | s.bw[1]);
-    B128 cand = E;
-    if (s.ko >= 0) cand = cand & ~bit128(s.ko);
-    const B128 has_lib = nbr4(E, g);
-    B128 mask = cand & has_lib;
-    const B128 hard = cand & ~has_lib;
+    const B E = M::board(g) & ~(s.bw[0] | s.bw[1]);
+    B cand = E;
+    if (s.ko >= 0) cand = cand & ~BB<B>::bit(s.ko);
+    const B has_lib = nbr4(E, g);
+    B mask = cand & has_lib;
+    const B hard = cand & ~has_lib;
     if (any(hard)) {
       // A surrounded point is legal iff a neighbouring own chain keeps >= 2
       // liberties or a neighbouring opponent chain is in atari (== the
       // per-point surrounded_legal test).  Every chain next to any
       // surrounded point is flooded once per move and classified; the legal
       // points are then the surrounded points next to a qualifying chain.
-      const B128 own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-      const B128 ring = nbr4(hard, g);
-      B128 good = b128(0, 0);
-      B128 todo = ring & own;
+      const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+      const B ring = nbr4(hard, g);
+      B good = BB<B>::zero();
+      B todo = ring & own;
       while (any(todo)) {
-        const B128 ch = flood(bit128(lowest(todo)), own, g);
+        const B ch = flood(BB<B>::bit(lowest(todo)), own, g);
         todo = todo & ~ch;
         if (popc(nbr4(ch, g) & E) >= 2) good = good | ch;  // keeps a liberty
       }
       todo = ring & opp;
       while (any(todo)) {
-        const B128 ch = flood(bit128(lowest(todo)), opp, g);
+        const B ch = flood(BB<B>::bit(lowest(todo)), opp, g);
         todo = todo & ~ch;
         if (popc(nbr4(ch, g) & E) == 1) good = good | ch;  // atari
       }
@@ -617,29 +645,29 @@ struct Go {
       s.flags |= kLastPass;
       // Hash unchanged: the repetition insert is a no-op for a pass.
     } else {
-      const B128 pb = bit128(a);
-      const B128 nb = nbr4(pb, g);
-      B128 own = pick(s.bw, c) | pb;
-      B128 opp = pick(s.bw, 1 - c);
+      const B pb = BB<B>::bit(a);
+      const B nb = nbr4(pb, g);
+      B own = pick(s.bw, c) | pb;
+      B opp = pick(s.bw, 1 - c);
       const bool enemy_eye = !any(nb & ~opp);
       s.hash ^= ctx.zob[2 * a + c];
-      B128 E = g.board & ~(own | opp);
+      B E = M::board(g) & ~(own | opp);
       int captured = 0;
       int cap_pt = -1;
-      B128 on = nb & opp;
+      B on = nb & opp;
       while (any(on)) {
         const int q = lowest(on);
-        const B128 ch = flood(bit128(q), opp, g);
+        const B ch = flood(BB<B>::bit(q), opp, g);
         on = on & ~ch;
         if (!any(nbr4(ch, g) & E)) {
           opp = opp & ~ch;
           E = E | ch;
           captured += popc(ch);
           cap_pt = q;
-          B128 rem = ch;
+          B rem = ch;
           while (any(rem)) {
             const int x = lowest(rem);
-            rem = rem & ~bit128(x);
+            rem = rem & ~BB<B>::bit(x);
             s.hash ^= ctx.zob[2 * x + (1 - c)];
           }
         }
@@ -663,13 +691,13 @@ struct Go {
   //   * a region bordering both colours is where the early abort matters: the
   //     reference's DFS sequence is replayed on it exactly (tt_mixed_region).
   OS_HD static float score(const State& s, const GameCfg& g) {
-    const B128 E = g.board & ~(s.bw[0] | s.bw[1]);
+    const B E = M::board(g) & ~(s.bw[0] | s.bw[1]);
     int delta = popc(s.bw[0]) - popc(s.bw[1]);
-    B128 todo = E;
+    B todo = E;
     while (any(todo)) {
-      const B128 reg = flood(bit128(lowest(todo)), E, g);
+      const B reg = flood(BB<B>::bit(lowest(todo)), E, g);
       todo = todo & ~reg;
-      const B128 rim = nbr4(reg, g);
+      const B rim = nbr4(reg, g);
       const bool rb = any(rim & s.bw[0]), rw = any(rim & s.bw[1]);
       if (rb && !rw) delta += popc(reg);
       else if (rw && !rb) delta -= popc(reg);
@@ -684,18 +712,18 @@ struct Go {
   // held as the 2-bit directions taken from the start point (a point's parent
   // is one step back along its direction, and an ancestor resumes at the
   // direction after the one it took), so no per-point stack memory is needed.
-  OS_HD static int tt_mixed_region(const State& s, const GameCfg& g, B128 reg) {
+  OS_HD static int tt_mixed_region(const State& s, const GameCfg& g, B reg) {
     const int n = g.rows;
     int delta = 0;
-    B128 marked = b128(0, 0);
-    B128 todo = reg;
+    B marked = BB<B>::zero();
+    B todo = reg;
     while (any(todo)) {
       const int p0 = lowest(todo);
-      todo = todo & ~bit128(p0);
+      todo = todo & ~BB<B>::bit(p0);
       if (test(marked, p0)) continue;
       bool rb = false, rw = false;
       int num = 1;
-      marked = marked | bit128(p0);
+      marked = marked | BB<B>::bit(p0);
       uint64_t path0 = 0, path1 = 0, path2 = 0, path3 = 0;  // 2 bits per level
       int depth = 0;  // stack size - 1
       int cur = p0, curd = 0;
@@ -721,7 +749,7 @@ struct Go {
         if (test(s.bw[0], q)) { rb = true; continue; }
         if (test(s.bw[1], q)) { rw = true; continue; }
         if (test(marked, q)) continue;
-        marked = marked | bit128(q);
+        marked = marked | BB<B>::bit(q);
         ++num;
         // Slot `depth` <- d (it may hold a popped sibling's direction).
         const int w = depth >> 5, sh = 2 * (depth & 31);
@@ -755,6 +783,8 @@ struct Go {
     return plane == want ? 1.0f : 0.0f;
   }
 };
+using Go = GoT<B128>;
+using GoBig = GoT<B384>;  // board_size 12..19 (host State API)
 
 }  // namespace osm
 

@@ -12,6 +12,7 @@
 #include <map>
 #include <random>
 #include <sstream>
+#include <type_traits>
 
 namespace osm {
 namespace {
@@ -67,18 +68,27 @@ bool GetDouble(const std::map<std::string, std::string>& kv, const char* k,
   return true;
 }
 
-void SquareMasks(int n, GameCfg* c) {
-  c->board = lowmask128(n * n);
-  B128 col0 = b128(0, 0), coll = b128(0, 0);
+template <class B>
+void SquareMasksOf(int n, B* board, B* notcol0, B* notcollast, B* hex_a, B* hex_b) {
+  *board = BB<B>::lowmask(n * n);
+  B col0 = BB<B>::zero(), coll = BB<B>::zero();
   for (int r = 0; r < n; ++r) {
-    col0 = col0 | bit128(r * n);
-    coll = coll | bit128(r * n + n - 1);
+    col0 = col0 | BB<B>::bit(r * n);
+    coll = coll | BB<B>::bit(r * n + n - 1);
   }
-  c->notcol0 = c->board & ~col0;
-  c->notcollast = c->board & ~coll;
+  *notcol0 = *board & ~col0;
+  *notcollast = *board & ~coll;
   const bool n2 = n == 2;
-  c->hex_a = n2 ? b128(0, 0) : c->notcol0;
-  c->hex_b = n2 ? b128(0, 0) : c->notcollast;
+  *hex_a = n2 ? BB<B>::zero() : *notcol0;
+  *hex_b = n2 ? BB<B>::zero() : *notcollast;
+}
+
+void SquareMasks(int n, GameCfg* c) {
+  if (n <= kB128Side)
+    SquareMasksOf(n, &c->board, &c->notcol0, &c->notcollast, &c->hex_a, &c->hex_b);
+  else
+    SquareMasksOf(n, &c->big_board, &c->big_notcol0, &c->big_notcollast, &c->big_hex_a,
+                  &c->big_hex_b);
 }
 
 std::string FormatDouble(double v) {
@@ -95,6 +105,22 @@ template <class G>
 const typename G::State& St(const HostState& s) {
   return *reinterpret_cast<const typename G::State*>(s.raw);
 }
+
+// Calls f(G{}) with G the state machine of the game `g` (hex / go boards above
+// 11 x 11 use the B384 instantiations).
+template <class F>
+auto WithGame(const GameCfg& g, F&& f) {
+  switch (g.kind) {
+    case kTicTacToe: return f(TicTacToe{});
+    case kConnectFour: return f(ConnectFour{});
+    case kBreakthrough: return f(Breakthrough{});
+    case kHex: return g.rows > kB128Side ? f(HexBig{}) : f(Hex{});
+    default: return g.rows > kB128Side ? f(GoBig{}) : f(Go{});
+  }
+}
+
+template <class G>
+constexpr bool kIsGo = std::is_same<typename G::Ctx, GoCtx>::value;
 
 }  // namespace
 
@@ -170,9 +196,9 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
     if (!e.empty()) return e;
     int n;
     if (!GetInt(kv, "board_size", 11, &n)) return "bad hex board_size";
-    if (n < 2 || n > 11) {
+    if (n < 2 || n > kMaxSide) {
       *unsupported = true;
-      return "hex board_size must be in [2, 11] for this engine";
+      return "hex board_size must be in [2, 19] for this engine";
     }
     c.kind = kHex;
     c.rows = c.cols = n;
@@ -181,7 +207,7 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
     c.max_game_length = n * n;
     SquareMasks(n, &c);
     g->canonical = kv.empty() ? "hex()" : "hex(board_size=" + std::to_string(n) + ")";
-    g->state_bytes = sizeof(Hex::State);
+    g->state_bytes = n > kB128Side ? sizeof(HexBig::State) : sizeof(Hex::State);
   } else if (name == "go") {
     std::string e = reject_unknown({"board_size", "komi", "handicap"});
     if (!e.empty()) return e;
@@ -190,9 +216,9 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
     if (!GetInt(kv, "board_size", 19, &n) || !GetInt(kv, "handicap", 0, &handicap) ||
         !GetDouble(kv, "komi", 7.5, &komi))
       return "bad go parameter";
-    if (n < 2 || n > 11) {
+    if (n < 2 || n > kMaxSide) {
       *unsupported = true;
-      return "go board_size must be in [2, 11] for this engine";
+      return "go board_size must be in [2, 19] for this engine";
     }
     if (handicap >= 2) {
       *unsupported = true;
@@ -234,7 +260,7 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
       else if (it.first == "handicap") add("handicap", std::to_string(handicap));
     }
     g->canonical = canon + ")";
-    g->state_bytes = sizeof(Go::State);
+    g->state_bytes = n > kB128Side ? sizeof(GoBig::State) : sizeof(Go::State);
   } else {
     *unsupported = true;
     return "game '" + name + "' is not supported by this engine (supported: "
@@ -275,40 +301,27 @@ void StateInit(HostState* s) {
   s->history.clear();
   s->hashes.clear();
   const GameCfg& g = s->game->cfg;
-  switch (g.kind) {
-    case kTicTacToe: TicTacToe::init(St<TicTacToe>(*s), g); break;
-    case kConnectFour: ConnectFour::init(St<ConnectFour>(*s), g); break;
-    case kBreakthrough: Breakthrough::init(St<Breakthrough>(*s), g); break;
-    case kHex: Hex::init(St<Hex>(*s), g); break;
-    case kGo:
-      Go::init(St<Go>(*s), g);
-      s->hashes.push_back(St<Go>(*s).hash);  // go.cc:218-224 ResetBoard
-      break;
-  }
+  WithGame(g, [&](auto tag) {
+    using G = decltype(tag);
+    G::init(St<G>(*s), g);
+    if constexpr (kIsGo<G>) s->hashes.push_back(St<G>(*s).hash);  // go.cc:218-224
+  });
 }
 
 bool StateTerminal(const HostState& s) {
   const GameCfg& g = s.game->cfg;
-  switch (g.kind) {
-    case kTicTacToe: return TicTacToe::terminal(St<TicTacToe>(s), g);
-    case kConnectFour: return ConnectFour::terminal(St<ConnectFour>(s), g);
-    case kBreakthrough: return Breakthrough::terminal(St<Breakthrough>(s), g);
-    case kHex: return Hex::terminal(St<Hex>(s), g);
-    case kGo: return Go::terminal(St<Go>(s), g);
-  }
-  return true;
+  return WithGame(g, [&](auto tag) {
+    using G = decltype(tag);
+    return G::terminal(St<G>(s), g);
+  });
 }
 
 int StateCurrentPlayer(const HostState& s) {
   if (StateTerminal(s)) return -4;
-  switch (s.game->cfg.kind) {
-    case kTicTacToe: return TicTacToe::to_move(St<TicTacToe>(s));
-    case kConnectFour: return ConnectFour::to_move(St<ConnectFour>(s));
-    case kBreakthrough: return Breakthrough::to_move(St<Breakthrough>(s));
-    case kHex: return Hex::to_move(St<Hex>(s));
-    case kGo: return Go::to_move(St<Go>(s));
-  }
-  return -4;
+  return WithGame(s.game->cfg, [&](auto tag) {
+    using G = decltype(tag);
+    return G::to_move(St<G>(s));
+  });
 }
 
 namespace {
@@ -322,19 +335,17 @@ void LegalOf(const HostState& s, typename G::Ctx& ctx, std::vector<int64_t>* out
 void StateLegal(const HostState& s, std::vector<int64_t>* out) {
   out->clear();
   if (StateTerminal(s)) return;
-  NoCtx nc;
-  switch (s.game->cfg.kind) {
-    case kTicTacToe: LegalOf<TicTacToe>(s, nc, out); break;
-    case kConnectFour: LegalOf<ConnectFour>(s, nc, out); break;
-    case kBreakthrough: LegalOf<Breakthrough>(s, nc, out); break;
-    case kHex: LegalOf<Hex>(s, nc, out); break;
-    case kGo: {
+  WithGame(s.game->cfg, [&](auto tag) {
+    using G = decltype(tag);
+    if constexpr (kIsGo<G>) {
       std::vector<uint64_t> storage;
       GoCtx ctx = HostGoCtx(s, &storage);
-      LegalOf<Go>(s, ctx, out);
-      break;
+      LegalOf<G>(s, ctx, out);
+    } else {
+      NoCtx nc;
+      LegalOf<G>(s, nc, out);
     }
-  }
+  });
 }
 
 bool StateApply(HostState* s, int64_t a) {
@@ -344,21 +355,19 @@ bool StateApply(HostState* s, int64_t a) {
   for (int64_t x : legal) ok |= x == a;
   if (!ok) return false;
   const GameCfg& g = s->game->cfg;
-  NoCtx nc;
   const int ai = static_cast<int>(a);
-  switch (g.kind) {
-    case kTicTacToe: TicTacToe::apply(St<TicTacToe>(*s), g, nc, ai); break;
-    case kConnectFour: ConnectFour::apply(St<ConnectFour>(*s), g, nc, ai); break;
-    case kBreakthrough: Breakthrough::apply(St<Breakthrough>(*s), g, nc, ai); break;
-    case kHex: Hex::apply(St<Hex>(*s), g, nc, ai); break;
-    case kGo: {
+  WithGame(g, [&](auto tag) {
+    using G = decltype(tag);
+    if constexpr (kIsGo<G>) {
       std::vector<uint64_t> storage;
       GoCtx ctx = HostGoCtx(*s, &storage);
-      Go::apply(St<Go>(*s), g, ctx, ai);
+      G::apply(St<G>(*s), g, ctx, ai);
       s->hashes.assign(storage.begin(), storage.begin() + ctx.n_log);
-      break;
+    } else {
+      NoCtx nc;
+      G::apply(St<G>(*s), g, nc, ai);
     }
-  }
+  });
   s->history.push_back(a);
   return true;
 }
@@ -367,20 +376,17 @@ void StateReturns(const HostState& s, double* r) {
   r[0] = r[1] = 0.0;
   if (!StateTerminal(s)) return;
   const GameCfg& g = s.game->cfg;
-  NoCtx nc;
-  int r0 = 0;
-  switch (g.kind) {
-    case kTicTacToe: r0 = TicTacToe::ret0(St<TicTacToe>(s), g, nc); break;
-    case kConnectFour: r0 = ConnectFour::ret0(St<ConnectFour>(s), g, nc); break;
-    case kBreakthrough: r0 = Breakthrough::ret0(St<Breakthrough>(s), g, nc); break;
-    case kHex: r0 = Hex::ret0(St<Hex>(s), g, nc); break;
-    case kGo: {
+  const int r0 = WithGame(g, [&](auto tag) {
+    using G = decltype(tag);
+    if constexpr (kIsGo<G>) {
       std::vector<uint64_t> storage;
       GoCtx ctx = HostGoCtx(s, &storage);
-      r0 = Go::ret0(St<Go>(s), g, ctx);
-      break;
+      return G::ret0(St<G>(s), g, ctx);
+    } else {
+      NoCtx nc;
+      return G::ret0(St<G>(s), g, nc);
     }
-  }
+  });
   r[0] = static_cast<double>(r0);
   r[1] = static_cast<double>(-r0);
 }
@@ -398,14 +404,7 @@ void ObsFill(const HostState& s, int player, float* out) {
 }  // namespace
 
 int ObservationShape(const HostGame& g, int32_t* shape3) {
-  int c = 0;
-  switch (g.cfg.kind) {
-    case kTicTacToe: c = ObsPlanes<TicTacToe>(); break;
-    case kConnectFour: c = ObsPlanes<ConnectFour>(); break;
-    case kBreakthrough: c = ObsPlanes<Breakthrough>(); break;
-    case kHex: c = ObsPlanes<Hex>(); break;
-    case kGo: c = ObsPlanes<Go>(); break;
-  }
+  const int c = WithGame(g.cfg, [&](auto tag) { return ObsPlanes<decltype(tag)>(); });
   if (shape3) {
     shape3[0] = c;
     shape3[1] = g.cfg.rows;
@@ -415,13 +414,7 @@ int ObservationShape(const HostGame& g, int32_t* shape3) {
 }
 
 void StateObservation(const HostState& s, int player, float* out) {
-  switch (s.game->cfg.kind) {
-    case kTicTacToe: ObsFill<TicTacToe>(s, player, out); break;
-    case kConnectFour: ObsFill<ConnectFour>(s, player, out); break;
-    case kBreakthrough: ObsFill<Breakthrough>(s, player, out); break;
-    case kHex: ObsFill<Hex>(s, player, out); break;
-    case kGo: ObsFill<Go>(s, player, out); break;
-  }
+  WithGame(s.game->cfg, [&](auto tag) { ObsFill<decltype(tag)>(s, player, out); });
 }
 
 namespace {
@@ -466,7 +459,8 @@ std::string BtString(const Breakthrough::State& s, const GameCfg& g) {
   return out;
 }
 
-char HexCellChar(const Hex::State& s, int i) {
+template <class HS>
+char HexCellChar(const HS& s, int i) {
   if (test(s.st[0], i)) {
     if (s.win_cell == i) return 'X';
     if (test(s.ea[0], i)) return 'y';
@@ -482,7 +476,8 @@ char HexCellChar(const Hex::State& s, int i) {
   return '.';
 }
 
-std::string HexString(const Hex::State& s, const GameCfg& g) {
+template <class HS>
+std::string HexString(const HS& s, const GameCfg& g) {
   const int n = g.rows;
   std::string out;
   int line = 0;
@@ -498,7 +493,8 @@ std::string HexString(const Hex::State& s, const GameCfg& g) {
   return out;
 }
 
-std::string GoString(const Go::State& s, const GameCfg& g, size_t hist) {
+template <class GS>
+std::string GoString(const GS& s, const GameCfg& g, size_t hist) {
   std::ostringstream ss;
   ss << "GoState(komi=" << g.komi << ", to_play=" << (s.to_play == 0 ? "B" : "W")
      << ", history.size()=" << hist << ")\n";
@@ -527,8 +523,11 @@ std::string StateToString(const HostState& s) {
     case kTicTacToe: return TttString(St<TicTacToe>(s));
     case kConnectFour: return C4String(St<ConnectFour>(s));
     case kBreakthrough: return BtString(St<Breakthrough>(s), g);
-    case kHex: return HexString(St<Hex>(s), g);
-    case kGo: return GoString(St<Go>(s), g, s.history.size());
+    case kHex:
+      return g.rows > kB128Side ? HexString(St<HexBig>(s), g) : HexString(St<Hex>(s), g);
+    case kGo:
+      return g.rows > kB128Side ? GoString(St<GoBig>(s), g, s.history.size())
+                                : GoString(St<Go>(s), g, s.history.size());
   }
   return "";
 }
@@ -556,9 +555,11 @@ std::string StateActionToString(const HostState& s, int player, int64_t a) {
       return out;
     }
     case kHex: {
-      const Hex::State& hs = St<Hex>(s);
       bool ea, eb;
-      Hex::edges_if(hs, g, player, static_cast<int>(a), &ea, &eb);
+      if (g.rows > kB128Side)
+        HexBig::edges_if(St<HexBig>(s), g, player, static_cast<int>(a), &ea, &eb);
+      else
+        Hex::edges_if(St<Hex>(s), g, player, static_cast<int>(a), &ea, &eb);
       char ch;
       if (player == 0) ch = ea && eb ? 'X' : (ea ? 'y' : (eb ? 'z' : 'x'));
       else ch = ea && eb ? 'O' : (ea ? 'p' : (eb ? 'q' : 'o'));

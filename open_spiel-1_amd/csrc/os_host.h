@@ -11,8 +11,10 @@
 
 namespace osm {
 
-// Largest device state record (Hex: 6 x B128 + scalars).
-constexpr int kStateBytes = 112;
+// Host state record: any G::State, big-board hex / go included.
+constexpr int kStateBytes = 320;  // >= every G::State (HexBig: 296 B)
+constexpr int kB128Side = 11;     // hex / go sides on B128 bitboards (device kernels)
+constexpr int kMaxSide = 19;      // hex / go sides on B384 bitboards (host State API)
 
 struct HostGame {
   GameCfg cfg;

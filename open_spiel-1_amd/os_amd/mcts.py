@@ -9,8 +9,9 @@ Dirichlet noise, one of the five supported games — continuing the bot's and
 the evaluator's `np.random.RandomState` streams in place, bit-exact with the
 reference module (one shared RandomState, as in mcts_test.py:41-54, or two).
 Searches the engine does not implement (user evaluators, custom
-`child_selection_fn`, Dirichlet noise) run the generic host loop below; pass
-`backend="hip"` to forbid that and fail loudly instead.
+`child_selection_fn`, Dirichlet noise, hex / go boards above 11 x 11) run the
+generic host loop below; pass `backend="hip"` to forbid that and fail loudly
+instead.
 """
 import math
 import time
@@ -190,7 +191,7 @@ class MCTSBot(pyspiel.Bot):
     return (type(self.evaluator) is RandomRolloutEvaluator and
             self._child_selection_fn is SearchNode.uct_value and
             not self._dirichlet_noise and
-            isinstance(self._game, pyspiel.Game))
+            isinstance(self._game, pyspiel.Game) and self._game.on_device())
 
   def restart_at(self, state):
     pass

@@ -169,6 +169,14 @@ class Game:
   def get_type(self):
     return _TYPES[self._info.kind]
 
+  # hex / go sides the device engine runs (B128 bitboards); larger boards
+  # (up to 19 x 19) have the State API only.
+  DEVICE_MAX_SIDE = 11
+
+  def on_device(self):
+    """Whether the GPU engine can search this game (else: host State API)."""
+    return self._info.kind not in (3, 4) or self._info.rows <= Game.DEVICE_MAX_SIDE
+
   def get_parameters(self):
     k = self._info.kind
     if k == 2:
@@ -260,8 +268,9 @@ class State:
   def legal_actions(self, player=None):
     if player is not None and player != self.current_player():
       return []
-    buf = np.zeros(256, np.int64)
-    n = lib.os_state_legal_actions(self._h, buf.ctypes.data, 256)
+    cap = self._game._info.num_distinct_actions
+    buf = np.zeros(cap, np.int64)
+    n = lib.os_state_legal_actions(self._h, buf.ctypes.data, cap)
     return [int(a) for a in buf[:n]]
 
   def legal_actions_mask(self, player=None):
