@@ -121,7 +121,9 @@ def test_unsupported_games_raise_value_error():
   with pytest.raises(ValueError):
     pyspiel.load_game("chess")
   with pytest.raises(ValueError):
-    pyspiel.load_game("go(board_size=19)")
+    pyspiel.load_game("go(board_size=21)")  # go_board.h kMaxBoardSize = 19
+  with pytest.raises(ValueError):
+    pyspiel.load_game("hex(board_size=20)")  # beyond this engine's B384 boards
   with pytest.raises(RuntimeError):
     pyspiel.load_game("hex(bogus=1)")
 
