@@ -18,7 +18,8 @@ PLAYTHROUGHS = [("tic_tac_toe", "tic_tac_toe"), ("connect_four", "connect_four")
 GAMES = ["tic_tac_toe", "connect_four", "breakthrough",
          "breakthrough(rows=6,columns=5)", "breakthrough(rows=4,columns=3)",
          "hex(board_size=5)", "hex", "hex(board_size=2)", "go(board_size=9)",
-         "go(board_size=7,komi=4.5)", "go(board_size=5)", "go(board_size=11)"]
+         "go(board_size=7,komi=4.5)", "go(board_size=5)", "go(board_size=11)",
+         "go(board_size=13)", "hex(board_size=13)"]  # B384 boards (host only)
 
 
 def info(s):
