@@ -436,6 +436,8 @@ def bench_playouts(args, ctx, layout):
   for _ in range(args.warmup):
     c = step()
   returns = be.eng.rollouts_fetch()
+  alg_bytes = None if ctx.rehearse else be.eng.rollouts_algorithmic_bytes(count)
+  rstats = None if ctx.rehearse else be.eng.rollouts_stats()
   ret0 = returns[:, 0]
   local = np.array([(ret0 > 0).sum(), (ret0 < 0).sum(), (ret0 == 0).sum()], np.int64)
   lc = ctx.torch.from_numpy(local).to(ctx.dev)
@@ -459,8 +461,11 @@ def bench_playouts(args, ctx, layout):
                                     % (game, N, ctx.world),
                         "game": game, "playouts_total": N,
                         "parallelism": "sharded x%d (RCCL all_reduce int64[3] per step)"
-                                       % ctx.world, "layout": "lane"})
-  line["roofline"] = None
+                                       % ctx.world, "layout": "lane",
+                        "playouts_per_step_per_gpu": count})
+  line["roofline"] = (None if alg_bytes is None else
+                      _roofline("k_rollouts", game, alg_bytes, kernel_ms, count, "playout"))
+  line["playout_stats"] = rstats
   line["kernel_ms_per_launch"] = kernel_ms
   line["cpu_baseline"] = cpu
   line["parity"] = parity

@@ -248,6 +248,11 @@ int os_rollouts_fetch(os_engine* e, double* out_returns);
  * mean player-0 return), on hip_stream; overwrites dev_counts.  Lets ranks
  * all-reduce the totals without a host round trip. */
 int os_rollouts_outcomes_async(os_engine* e, int64_t* dev_counts, void* hip_stream);
+/* Instrumentation of the last lane-layout rollout run (k_rollouts), for the
+ * algorithmic-bytes model of bench.py: out[0] = MT19937 words drawn, out[1] =
+ * moves played (both summed over the batch), out[2] = root state bytes.  No
+ * reference counterpart (the reference has no device). */
+int os_rollouts_stats(os_engine* e, int64_t* out);
 
 /* Root-parallel MCTS (the reference has no root-parallel
  * driver — each tree is one MCTSBot::MCTSearch, mcts.cc:325-428): action-indexed

@@ -589,6 +589,8 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
   if (n > 0) HIP_TRY(hipMemcpy(e->d_bseed.p, seeds, n * 4, hipMemcpyHostToDevice));
   if ((rc = e->d_mt.ensure(std::max<int64_t>(n, 1) * kMtN * 4))) return rc;
   if ((rc = e->d_rollout_out.ensure(std::max<int64_t>(n, 1) * 16))) return rc;
+  if ((rc = e->d_roll_cnt.ensure(std::max<int64_t>(n, 1) * 8))) return rc;
+  HIP_TRY(hipMemset(e->d_roll_cnt.p, 0, std::max<int64_t>(n, 1) * 8));
   e->roll_nhash = 0;
   if (e->game.cfg.kind == kGo) {
     if ((rc = e->d_glog.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 8))) return rc;
@@ -1018,6 +1020,23 @@ int os_rollouts_fetch(os_engine* e, double* out_returns) {
   HIP_TRY(hipDeviceSynchronize());
   if (e->roll_n > 0)
     HIP_TRY(hipMemcpy(out_returns, e->d_rollout_out.p, e->roll_n * 16, hipMemcpyDeviceToHost));
+  return OS_OK;
+}
+
+int os_rollouts_stats(os_engine* e, int64_t* out) {
+  if (!e || !out) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->roll_ready) return Fail(OS_ERR_INVALID, "os_rollouts_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<uint32_t> c(static_cast<size_t>(e->roll_n) * 2);
+  if (e->roll_n > 0)
+    HIP_TRY(hipMemcpy(c.data(), e->d_roll_cnt.p, c.size() * 4, hipMemcpyDeviceToHost));
+  out[0] = out[1] = 0;
+  for (size_t i = 0; i < c.size(); i += 2) {
+    out[0] += c[i];
+    out[1] += c[i + 1];
+  }
+  out[2] = e->game.state_bytes;
   return OS_OK;
 }
 

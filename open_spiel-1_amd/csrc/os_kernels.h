@@ -536,14 +536,23 @@ __global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   typename G::Ctx ctx = RollCtx<G>::make(a, a.glog + i);
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
+  uint32_t moves = 0;
   for (int k = 0; k < a.n_rollouts; ++k) {
     ctx.reset();
-    const int r0 = rollout_ret0<G, kPolicyCpp>(root, a.cfg, ctx, ev);
+    // rollout_ret0 (mcts.cc:46-55), counting the moves for the byte model.
+    typename G::State s = root;
+    while (!G::terminal(s, a.cfg)) {
+      const typename G::Legal l = G::legal(s, a.cfg, ctx);
+      G::apply(s, a.cfg, ctx, l.kth(static_cast<int>(AbslUniform(ev, static_cast<uint32_t>(l.count)))));
+      ++moves;
+    }
+    const int r0 = G::ret0(s, a.cfg, ctx);
     s0 += static_cast<double>(r0);
     s1 += static_cast<double>(-r0);
   }
   a.out[2 * i] = s0 / a.n_rollouts;
   a.out[2 * i + 1] = s1 / a.n_rollouts;
+  a.counters[i] = make_uint2(ev.words, moves);  // (MT words drawn, moves played)
 }
 
 
@@ -722,6 +731,7 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   a.seeds = static_cast<const uint32_t*>(e->d_bseed.p);
   a.mt = static_cast<uint32_t*>(e->d_mt.p);
   a.glog = static_cast<uint64_t*>(e->d_glog.p);
+  a.counters = static_cast<uint2*>(e->d_roll_cnt.p);
   a.out = static_cast<double*>(e->d_rollout_out.p);
   a.zob = static_cast<const uint64_t*>(e->d_zob.p);
   a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);

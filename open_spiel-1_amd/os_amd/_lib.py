@@ -131,6 +131,7 @@ _sig("os_rollouts_prepare", ctypes.c_int, [_vp, _P, _i64, _i64, _i32, _P])
 _sig("os_rollouts_run_async", ctypes.c_int, [_vp, _vp])
 _sig("os_rollouts_fetch", ctypes.c_int, [_vp, _P])
 _sig("os_rollouts_outcomes_async", ctypes.c_int, [_vp, _vp, _vp])
+_sig("os_rollouts_stats", ctypes.c_int, [_vp, _vp])
 _sig("os_engine_root_sums_async", ctypes.c_int, [_vp, _i32, _vp, _vp, _vp])
 _sig("os_selfplay", ctypes.c_int,
      [_vp, ctypes.POINTER(MctsParams), _i64, _P, _P, _P, _P, _i32, _P, _P, _P, _P, _P])

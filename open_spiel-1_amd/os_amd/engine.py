@@ -180,6 +180,19 @@ class Engine:
     check(lib.os_rollouts_fetch(self._h, ptr(out)))
     return out
 
+  def rollouts_stats(self):
+    """Counters of the last lane-layout rollout run (os_rollouts_stats)."""
+    out = np.zeros(3, np.int64)
+    check(lib.os_rollouts_stats(self._h, ptr(out)))
+    return {"rng_words": int(out[0]), "moves": int(out[1]), "state_bytes": int(out[2])}
+
+  def rollouts_algorithmic_bytes(self, n):
+    """HBM bytes n playouts must move: one MT19937 state
+    word read + written per word drawn, one position-hash log write + probe
+    (16 B) per move, one root state read per playout."""
+    s = self.rollouts_stats()
+    return s["rng_words"] * 8 + s["moves"] * 16 + n * s["state_bytes"]
+
   def rollouts_outcomes_async(self, dev_counts_ptr, stream=None):
     """Writes int64[3] (p0 wins, p1 wins, draws) to a device address."""
     check(lib.os_rollouts_outcomes_async(self._h, dev_counts_ptr, stream))

@@ -47,7 +47,8 @@ def main():
     if os.path.exists(log):
       for line in open(log):
         if line.startswith("{"):
-          sims = json.loads(line)["config"]["sims_per_step_per_gpu"]
+          cfg = json.loads(line)["config"]
+          sims = cfg.get("sims_per_step_per_gpu", cfg.get("playouts_per_step_per_gpu"))
   sys.path.insert(0, ROOT)
   import bench
   rec = {"kernel": kernel, "game": game, "sims_per_launch": sims,
