@@ -528,6 +528,7 @@ struct GoT {
   using M = CfgMasks<B>;
   struct State {
     B bw[2];     // black, white stones
+    B atari;     // stones (both colours) whose chain has exactly one liberty
     uint64_t hash;  // Zobrist hash of the stones
     int16_t ko;     // ko cell or -1
     uint16_t moves; // history length (since the empty board)
@@ -552,30 +553,6 @@ struct GoT {
       c = nx;
     }
   }
-  // Whether empty cell p with no empty neighbour is a legal move for player c
-  // (go_board.cc:425-440).
-  OS_HD static bool surrounded_legal(const State& s, const GameCfg& g, int p, int c,
-                                     B E) {
-    const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-    B nb = nbr4(BB<B>::bit(p), g);
-    B on = nb & own;
-    while (any(on)) {  // joins an own chain that keeps a liberty
-      const int q = lowest(on);
-      const B ch = flood(BB<B>::bit(q), own, g);
-      const B libs = nbr4(ch, g) & E;
-      if (popc(libs) >= 2) return true;
-      on = on & ~ch;
-    }
-    B opn = nb & opp;
-    while (any(opn)) {  // captures an opponent chain in atari
-      const int q = lowest(opn);
-      const B ch = flood(BB<B>::bit(q), opp, g);
-      const B libs = nbr4(ch, g) & E;
-      if (popc(libs) == 1) return true;
-      opn = opn & ~ch;
-    }
-    return false;
-  }
   struct Legal {
     B mask;  // legal board points (pass excluded)
     int count;  // including pass
@@ -586,7 +563,7 @@ struct GoT {
     }
   };
   OS_HD static void init(State& s, const GameCfg&) {
-    s.bw[0] = s.bw[1] = BB<B>::zero();
+    s.bw[0] = s.bw[1] = s.atari = BB<B>::zero();
     s.hash = 0; s.ko = -1; s.moves = 0; s.to_play = 0; s.flags = 0; s.pad = 0;
   }
   OS_HD static bool terminal(const State& s, const GameCfg& g) {
@@ -605,26 +582,12 @@ struct GoT {
     B mask = cand & has_lib;
     const B hard = cand & ~has_lib;
     if (any(hard)) {
-      // A surrounded point is legal iff a neighbouring own chain keeps >= 2
-      // liberties or a neighbouring opponent chain is in atari (== the
-      // per-point surrounded_legal test).  Every chain next to any
-      // surrounded point is flooded once per move and classified; the legal
-      // points are then the surrounded points next to a qualifying chain.
+      // A surrounded point is legal iff it joins an own chain that keeps a
+      // liberty (>= 2 now) or captures an opponent chain in atari
+      // (go_board.cc:425-440).  Every stone's chain has >= 1 liberty, so with
+      // the atari set both are masks: no chain is flooded here.
       const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-      const B ring = nbr4(hard, g);
-      B good = BB<B>::zero();
-      B todo = ring & own;
-      while (any(todo)) {
-        const B ch = flood(BB<B>::bit(lowest(todo)), own, g);
-        todo = todo & ~ch;
-        if (popc(nbr4(ch, g) & E) >= 2) good = good | ch;  // keeps a liberty
-      }
-      todo = ring & opp;
-      while (any(todo)) {
-        const B ch = flood(BB<B>::bit(lowest(todo)), opp, g);
-        todo = todo & ~ch;
-        if (popc(nbr4(ch, g) & E) == 1) good = good | ch;  // atari
-      }
+      const B good = (own & ~s.atari) | (opp & s.atari);
       mask = mask | (hard & nbr4(good, g));
     }
     Legal l;
@@ -654,14 +617,22 @@ struct GoT {
       B E = M::board(g) & ~(own | opp);
       int captured = 0;
       int cap_pt = -1;
+      // The atari set changes only for chains the move touches: adjacent
+      // opponent chains lose liberty a (captured at zero), the mover's chain
+      // through a is new, and own chains next to captured stones gain
+      // liberties.  Every other chain keeps its liberties.
+      B atari = s.atari;
+      B capd = BB<B>::zero();
       B on = nb & opp;
       while (any(on)) {
         const int q = lowest(on);
         const B ch = flood(BB<B>::bit(q), opp, g);
         on = on & ~ch;
-        if (!any(nbr4(ch, g) & E)) {
+        const B libs = nbr4(ch, g) & E;
+        if (!any(libs)) {
           opp = opp & ~ch;
           E = E | ch;
+          capd = capd | ch;
           captured += popc(ch);
           cap_pt = q;
           B rem = ch;
@@ -671,7 +642,15 @@ struct GoT {
             s.hash ^= ctx.zob[2 * x + (1 - c)];
           }
         }
+        atari = (atari & ~ch) | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
       }
+      B todo = pb | (nbr4(capd, g) & own);
+      while (any(todo)) {
+        const B ch = flood(BB<B>::bit(lowest(todo)), own, g);
+        todo = todo & ~ch;
+        atari = (atari & ~ch) | BB<B>::sel(popc(nbr4(ch, g) & E) == 1, ch, BB<B>::zero());
+      }
+      s.atari = atari;
       s.bw[0] = c ? opp : own;
       s.bw[1] = c ? own : opp;
       s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
