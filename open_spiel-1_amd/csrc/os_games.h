@@ -75,6 +75,8 @@ struct CfgMasks<B384> {
 
 struct NoCtx {
   OS_HD void reset() {}
+  OS_HD int mark() const { return 0; }
+  OS_HD void rewind(int) {}
 };
 
 // ----------------------------------------------------------------------------
@@ -470,55 +472,73 @@ struct Filter256 {
   }
 };
 
-// Positional-superko set of one playout / simulation.  Only positions that a
-// capture separates from the current one can repeat it: without a capture in
-// between, every non-pass move adds one stone, so a later position has
-// strictly more stones than an earlier one.  `cand_end` / `cand_filt` cover the
-// log entries logged before the most recent capture (plus every base entry,
-// whose history is unknown); a capturing move widens them to the whole log
-// before its own test.  Same answers as testing the whole set, fewer scans.
+// Positional-superko set of one playout / simulation (go.cc:199-208).
+// Two positions can only be equal if they have the same number of stones, so
+// the log is bucketed by stone count: head[k] is the last entry with k stones
+// (+ 1, 0 = none) and link[e] holds entry e's stone count (high half) and the
+// previous entry + 1 with the same count (low half).  A new position is compared only with its own bucket -- in random
+// playouts under one entry on average, against ~50 candidates for a linear
+// scan -- and the buckets give the same answers as testing the whole set.
+// Positions before the root (`base`, counts unknown) are scanned behind a
+// 256-bit pre-filter.  Arrays may be batch-SoA: element i at [i * stride].
 struct GoCtx {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
   const uint64_t* base;    // hashes of positions before this search's root
   int32_t n_base;
   uint64_t* log;           // hashes added since the root (capacity cap)
-  int32_t log_stride;      // element i at log[i * log_stride] (SoA batches)
+  uint32_t* link;          // [cap] stone count << 16 | previous same-count entry + 1
+  uint16_t* head;          // [n_heads] last entry + 1 with k stones
+  int32_t stride;          // SoA stride of log / next / head (1: contiguous)
   int32_t n_log;
-  int32_t cand_end;        // log[0, cand_end): entries a capture separates
   int32_t cap;
-  Filter256 filt;          // base + whole log
-  Filter256 cand_filt;     // base + log[0, cand_end)
+  int32_t n_heads;         // cells + 1
+  Filter256 base_filt;     // base hashes
 
   // Empties the log (the base stays).
   OS_HD void reset() {
     n_log = 0;
-    cand_end = 0;
-    filt.clear();
-    for (int i = 0; i < n_base; ++i) filt.add(fbit(base[i]));
-    cand_filt = filt;
+    for (int k = 0; k < n_heads; ++k) head[static_cast<int64_t>(k) * stride] = 0;
   }
-  OS_HD void init_filters() { reset(); }
+  // Builds base_filt from base[0, n_base) and resets.
+  OS_HD void init_filters() {
+    base_filt.clear();
+    for (int i = 0; i < n_base; ++i) base_filt.add(fbit(base[i]));
+    reset();
+  }
   OS_HD static int fbit(uint64_t h) { return static_cast<int>(h >> 56); }
-  OS_HD uint64_t log_at(int i) const { return log[static_cast<int64_t>(i) * log_stride]; }
-  // Whether h is among the candidate positions.
-  OS_HD bool candidate(uint64_t h) const {
-    if (!cand_filt.has(fbit(h))) return false;
-    for (int i = 0; i < n_base; ++i)
-      if (base[i] == h) return true;
-    for (int i = 0; i < cand_end; ++i)
-      if (log_at(i) == h) return true;
+  OS_HD bool contains(uint64_t h, int stones) const {
+    if (base_filt.has(fbit(h)))
+      for (int i = 0; i < n_base; ++i)
+        if (base[i] == h) return true;
+    for (int e = head[static_cast<int64_t>(stones) * stride]; e;
+         e = static_cast<int>(link[static_cast<int64_t>(e - 1) * stride] & 0xFFFFu))
+      if (log[static_cast<int64_t>(e - 1) * stride] == h) return true;
     return false;
   }
-  // Logs the position after a non-pass move; false if it was already present
-  // (go.cc:201-205).  `captured`: the move removed stones.
-  OS_HD bool insert(uint64_t h, bool captured) {
-    if (captured) {
-      cand_end = n_log;
-      cand_filt = filt;
+  // Log position count, and dropping back to it (each rollout of a leaf
+  // starts from the leaf's log, mcts.cc:46-47): the buckets are unlinked in
+  // reverse order of insertion.
+  OS_HD int mark() const { return n_log; }
+  OS_HD void rewind(int m) {
+    while (n_log > m) {
+      --n_log;
+      const uint32_t lk = link[static_cast<int64_t>(n_log) * stride];
+      head[static_cast<int64_t>(lk >> 16) * stride] = static_cast<uint16_t>(lk & 0xFFFFu);
     }
-    if (candidate(h)) return false;
-    if (n_log < cap) log[static_cast<int64_t>(n_log++) * log_stride] = h;
-    filt.add(fbit(h));
+  }
+  // Logs the position after a non-pass move; false if it was already present
+  // (go.cc:201-205).
+  OS_HD bool insert(uint64_t h, bool captured, int stones) {
+    (void)captured;
+    if (contains(h, stones)) return false;
+    if (n_log < cap) {
+      const int64_t e = static_cast<int64_t>(n_log) * stride;
+      int64_t hk = static_cast<int64_t>(stones) * stride;
+      log[e] = h;
+      link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
+      head[hk] = static_cast<uint16_t>(n_log + 1);
+      ++n_log;
+    }
     return true;
   }
 };
@@ -654,7 +674,7 @@ struct GoT {
       s.bw[0] = c ? opp : own;
       s.bw[1] = c ? own : opp;
       s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
-      if (!ctx.insert(s.hash, captured > 0)) s.flags |= kSuperko;
+      if (!ctx.insert(s.hash, captured > 0, popc(own) + popc(opp))) s.flags |= kSuperko;
     }
     s.to_play = static_cast<uint8_t>(1 - c);
     s.moves++;

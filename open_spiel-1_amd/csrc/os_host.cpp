@@ -271,28 +271,15 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
   return "";
 }
 
-GoCtx HostGoCtx(const HostState& s, std::vector<uint64_t>* storage) {
+GoCtx HostGoCtx(const HostState& s, HostGoLog* buf) {
   GoCtx ctx;
   std::memset(&ctx, 0, sizeof ctx);
-  const int cap = s.game->cfg.max_game_length + 4;
-  storage->assign(s.hashes.begin(), s.hashes.end());
-  storage->resize(cap);
+  const GameCfg& g = s.game->cfg;
   ctx.zob = s.game->zob.data();
-  ctx.base = nullptr;
-  ctx.n_base = 0;
-  ctx.log = storage->data();
-  ctx.log_stride = 1;
-  ctx.cap = cap;
-  ctx.reset();
-  // The state's own history is logged with unknown captures in between:
-  // every entry stays a candidate.
-  for (size_t i = 0; i < s.hashes.size(); ++i) {
-    ctx.log[i] = s.hashes[i];
-    ctx.filt.add(GoCtx::fbit(s.hashes[i]));
-  }
-  ctx.n_log = static_cast<int32_t>(s.hashes.size());
-  ctx.cand_end = ctx.n_log;
-  ctx.cand_filt = ctx.filt;
+  ctx.base = s.hashes.data();
+  ctx.n_base = static_cast<int32_t>(s.hashes.size());
+  buf->bind(&ctx, 4, g.rows * g.cols);  // one apply logs at most one position
+  ctx.init_filters();
   return ctx;
 }
 
@@ -338,8 +325,8 @@ void StateLegal(const HostState& s, std::vector<int64_t>* out) {
   WithGame(s.game->cfg, [&](auto tag) {
     using G = decltype(tag);
     if constexpr (kIsGo<G>) {
-      std::vector<uint64_t> storage;
-      GoCtx ctx = HostGoCtx(s, &storage);
+      HostGoLog buf;
+      GoCtx ctx = HostGoCtx(s, &buf);
       LegalOf<G>(s, ctx, out);
     } else {
       NoCtx nc;
@@ -359,10 +346,10 @@ bool StateApply(HostState* s, int64_t a) {
   WithGame(g, [&](auto tag) {
     using G = decltype(tag);
     if constexpr (kIsGo<G>) {
-      std::vector<uint64_t> storage;
-      GoCtx ctx = HostGoCtx(*s, &storage);
+      HostGoLog buf;
+      GoCtx ctx = HostGoCtx(*s, &buf);
       G::apply(St<G>(*s), g, ctx, ai);
-      s->hashes.assign(storage.begin(), storage.begin() + ctx.n_log);
+      for (int i = 0; i < ctx.n_log; ++i) s->hashes.push_back(buf.log[i]);
     } else {
       NoCtx nc;
       G::apply(St<G>(*s), g, nc, ai);
@@ -379,8 +366,8 @@ void StateReturns(const HostState& s, double* r) {
   const int r0 = WithGame(g, [&](auto tag) {
     using G = decltype(tag);
     if constexpr (kIsGo<G>) {
-      std::vector<uint64_t> storage;
-      GoCtx ctx = HostGoCtx(s, &storage);
+      HostGoLog buf;
+      GoCtx ctx = HostGoCtx(s, &buf);
       return G::ret0(St<G>(s), g, ctx);
     } else {
       NoCtx nc;

@@ -24,12 +24,34 @@ struct HostGame {
   int state_bytes = 0;
 };
 
+// Contiguous storage of one GoCtx's position log on the host.
+struct HostGoLog {
+  std::vector<uint64_t> log;
+  std::vector<uint32_t> link;
+  std::vector<uint16_t> head;
+  void bind(GoCtx* c, int cap, int cells) {
+    log.assign(cap, 0);
+    link.assign(cap, 0);
+    head.assign(cells + 1, 0);
+    c->log = log.data();
+    c->link = link.data();
+    c->head = head.data();
+    c->stride = 1;
+    c->cap = cap;
+    c->n_heads = cells + 1;
+  }
+};
+
 struct HostState {
   const HostGame* game;
   alignas(16) unsigned char raw[kStateBytes];
   std::vector<int64_t> history;
   std::vector<uint64_t> hashes;  // go: positions seen, incl. the initial one
 };
+
+// A GoCtx whose base is the state's whole position history (the reference's
+// repetitions_ set, go.h:105-120) and whose log is empty, in `buf`.
+GoCtx HostGoCtx(const HostState& s, HostGoLog* buf);
 
 // Parses and validates a game string; returns "" on success, else a message.
 // `unsupported` is set when the game/parameters are valid OpenSpiel but not

@@ -325,10 +325,10 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         } else {
           // Every rollout starts from a clone of the leaf (mcts.cc:46-47), so
           // go's position log is rewound to the leaf before each one.
-          const auto leaf_ctx = ctx;
+          const int leaf_mark = ctx.mark();
           double s0 = 0.0, s1 = 0.0;
           for (int k = 0; k < sp.n_rollouts; ++k) {
-            if (k) ctx = leaf_ctx;
+            if (k) ctx.rewind(leaf_mark);
             const int r0 = rollout_ret0<G, Policy>(s, g, ctx, ev);
             s0 += static_cast<double>(r0);
             s1 += static_cast<double>(-r0);

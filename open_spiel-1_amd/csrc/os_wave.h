@@ -332,7 +332,8 @@ struct GoWaveCtx {
     }
     return false;
   }
-  __device__ bool insert(uint64_t h, bool captured) {
+  __device__ bool insert(uint64_t h, bool captured, int stones) {
+    (void)stones;
     if (captured) {
       cand_end = n_log;
       cand_filt = filt;

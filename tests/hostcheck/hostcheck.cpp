@@ -32,16 +32,13 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
   PathEnt<R> path[kMaxPath];
   uint16_t actbuf[kMaxChildren];
   typename G::Ctx ctx;
-  std::vector<uint64_t> storage;
-  std::vector<uint64_t> logbuf(256);
+  HostGoLog logbuf;
   if constexpr (G::State::kNeedsLog) {
     std::memset(&ctx, 0, sizeof ctx);
     ctx.zob = game.zob.data();
     ctx.base = root.hashes.data();
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
-    ctx.log = logbuf.data();
-    ctx.log_stride = 1;
-    ctx.cap = 256;
+    logbuf.bind(&ctx, 256, game.cfg.rows * game.cfg.cols);
     ctx.init_filters();
   }
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
@@ -341,7 +338,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
   StateInit(&hs);
   for (int64_t i = 0; i < n_actions; ++i) StateApply(&hs, actions[i]);
   std::vector<uint32_t> mt(kMtN);
-  std::vector<uint64_t> logbuf(256);
+  HostGoLog logbuf;
   for (int64_t i = 0; i < n; ++i) {
     MtStream ev{mt.data(), kMtN, 0};
     mt_seed(ev.s, seeds[i]);
@@ -357,9 +354,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
         c.zob = game.zob.data();
         c.base = hs.hashes.data();
         c.n_base = static_cast<int32_t>(hs.hashes.size());
-        c.log = logbuf.data();
-        c.log_stride = 1;
-        c.cap = 256;
+        logbuf.bind(&c, 256, game.cfg.rows * game.cfg.cols);
         c.init_filters();
         r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg, c, ev);
         break;
