@@ -594,8 +594,7 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
   e->roll_nhash = 0;
   if (e->game.cfg.kind == kGo) {
     if ((rc = e->d_glog.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 8)) ||
-        (rc = e->d_glink.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 4)) ||
-        (rc = e->d_ghead.ensure(std::max<int64_t>(n, 1) * kGoHeads * 2)))
+        (rc = e->d_glink.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 4)))
       return rc;
     if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
     HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,

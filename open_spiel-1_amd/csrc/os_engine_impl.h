@@ -156,7 +156,6 @@ struct RollArgs {
   uint32_t* mt;      // [624][n] (k_rollouts, SoA) or [n][624]
   uint64_t* glog;    // go: [kGoLogCap][n] position logs (k_rollouts, SoA)
   uint32_t* glink;   //     [kGoLogCap][n] stone count + same-count links
-  uint16_t* ghead;   //     [kGoHeads][n] bucket heads
   uint2* counters;   // [n] (MT words drawn, moves played) (k_rollouts)
   double* out;       // [n][2]
   const uint64_t* zob;
@@ -229,7 +228,7 @@ struct os_engine {
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
-      d_sp_obs, d_glog, d_glink, d_ghead, d_roll_cnt;
+      d_sp_obs, d_glog, d_glink, d_roll_cnt;
   std::vector<osm::SearchResult> last_results;
   int64_t last_sims = 0;
   ~os_engine() {
@@ -238,7 +237,7 @@ struct os_engine {
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
-                     &d_az_slots, &d_az_prior, &d_glog, &d_glink, &d_ghead,
+                     &d_az_slots, &d_az_prior, &d_glog, &d_glink,
                      &d_roll_cnt};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();

@@ -487,8 +487,9 @@ struct GoCtx {
   int32_t n_base;
   uint64_t* log;           // hashes added since the root (capacity cap)
   uint32_t* link;          // [cap] stone count << 16 | previous same-count entry + 1
-  uint16_t* head;          // [n_heads] last entry + 1 with k stones
-  int32_t stride;          // SoA stride of log / next / head (1: contiguous)
+  uint8_t* head;           // [n_heads] last entry + 1 with k stones (cap <= 255)
+  int32_t stride;          // SoA stride of log / link (1: contiguous)
+  int32_t head_stride;     // stride of head (k_rollouts: LDS, 64 lanes)
   int32_t n_log;
   int32_t cap;
   int32_t n_heads;         // cells + 1
@@ -497,7 +498,7 @@ struct GoCtx {
   // Empties the log (the base stays).
   OS_HD void reset() {
     n_log = 0;
-    for (int k = 0; k < n_heads; ++k) head[static_cast<int64_t>(k) * stride] = 0;
+    for (int k = 0; k < n_heads; ++k) head[k * head_stride] = 0;
   }
   // Builds base_filt from base[0, n_base) and resets.
   OS_HD void init_filters() {
@@ -510,7 +511,7 @@ struct GoCtx {
     if (base_filt.has(fbit(h)))
       for (int i = 0; i < n_base; ++i)
         if (base[i] == h) return true;
-    for (int e = head[static_cast<int64_t>(stones) * stride]; e;
+    for (int e = head[stones * head_stride]; e;
          e = static_cast<int>(link[static_cast<int64_t>(e - 1) * stride] & 0xFFFFu))
       if (log[static_cast<int64_t>(e - 1) * stride] == h) return true;
     return false;
@@ -523,7 +524,7 @@ struct GoCtx {
     while (n_log > m) {
       --n_log;
       const uint32_t lk = link[static_cast<int64_t>(n_log) * stride];
-      head[static_cast<int64_t>(lk >> 16) * stride] = static_cast<uint16_t>(lk & 0xFFFFu);
+      head[static_cast<int>(lk >> 16) * head_stride] = static_cast<uint8_t>(lk & 0xFFFFu);
     }
   }
   // Logs the position after a non-pass move; false if it was already present
@@ -533,10 +534,10 @@ struct GoCtx {
     if (contains(h, stones)) return false;
     if (n_log < cap) {
       const int64_t e = static_cast<int64_t>(n_log) * stride;
-      int64_t hk = static_cast<int64_t>(stones) * stride;
+      const int hk = stones * head_stride;
       log[e] = h;
       link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
-      head[hk] = static_cast<uint16_t>(n_log + 1);
+      head[hk] = static_cast<uint8_t>(n_log + 1);
       ++n_log;
     }
     return true;

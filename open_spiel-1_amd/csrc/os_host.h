@@ -28,8 +28,8 @@ struct HostGame {
 struct HostGoLog {
   std::vector<uint64_t> log;
   std::vector<uint32_t> link;
-  std::vector<uint16_t> head;
-  void bind(GoCtx* c, int cap, int cells) {
+  std::vector<uint8_t> head;
+  void bind(GoCtx* c, int cap, int cells) {  // cap <= 255
     log.assign(cap, 0);
     link.assign(cap, 0);
     head.assign(cells + 1, 0);
@@ -37,6 +37,7 @@ struct HostGoLog {
     c->link = link.data();
     c->head = head.data();
     c->stride = 1;
+    c->head_stride = 1;
     c->cap = cap;
     c->n_heads = cells + 1;
   }

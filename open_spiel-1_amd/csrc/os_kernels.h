@@ -29,14 +29,14 @@ template <class G>
 struct CtxMaker;
 template <class G>
 struct CtxMaker {
-  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*, uint32_t*, uint16_t*) {
+  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*, uint32_t*, uint8_t*) {
     return NoCtx();
   }
 };
 template <>
 struct CtxMaker<Go> {
   __device__ static GoCtx make(const DevArgs& a, int64_t gr, uint64_t* log, uint32_t* link,
-                               uint16_t* head) {
+                               uint8_t* head) {
     GoCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
@@ -45,6 +45,7 @@ struct CtxMaker<Go> {
     c.link = link;
     c.head = head;
     c.stride = 1;
+    c.head_stride = 1;
     c.n_log = 0;
     c.cap = kGoLogCap;
     c.n_heads = a.cfg.rows * a.cfg.cols + 1;
@@ -90,7 +91,7 @@ __global__ void k_mcts(DevArgs a) {
   const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
   uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
   uint32_t glink[G::State::kNeedsLog ? kGoLogCap : 1];
-  uint16_t ghead[G::State::kNeedsLog ? kGoHeads : 1];
+  uint8_t ghead[G::State::kNeedsLog ? kGoHeads : 1];
   typename G::Ctx ctx = CtxMaker<G>::make(a, gr, glog, glink, ghead);
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   SearchResult res;
@@ -467,18 +468,22 @@ __global__ void k_az_step(AzArgs a) {
 
 template <class G>
 struct RollCtx {
-  __device__ static NoCtx make(const RollArgs&, int64_t) { return NoCtx(); }
+  __device__ static NoCtx make(const RollArgs&, int64_t, uint8_t*) { return NoCtx(); }
 };
 template <>
 struct RollCtx<Go> {
-  __device__ static GoCtx make(const RollArgs& a, int64_t i) {
+  // The bucket heads are the only per-move accesses that differ across the
+  // lanes (each lane is at its own stone count): they live in LDS, lane-
+  // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
+  __device__ static GoCtx make(const RollArgs& a, int64_t i, uint8_t* lds_heads) {
     GoCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
     c.log = a.glog + i;
     c.link = a.glink + i;
-    c.head = a.ghead + i;
+    c.head = lds_heads + (threadIdx.x & 63);
+    c.head_stride = 64;
     c.stride = static_cast<int32_t>(a.n);
     c.n_log = 0;
     c.cap = kGoLogCap;
@@ -544,7 +549,8 @@ __global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   if (i >= a.n) return;
   MtStreamSoA ev{a.mt + i, a.n, 0, 0};
   ev.seed(a.seeds[i]);
-  typename G::Ctx ctx = RollCtx<G>::make(a, i);
+  __shared__ uint8_t heads[G::State::kNeedsLog ? kGoHeads * 64 : 1];
+  typename G::Ctx ctx = RollCtx<G>::make(a, i, heads);
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
   uint32_t moves = 0;
@@ -743,7 +749,6 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   a.mt = static_cast<uint32_t*>(e->d_mt.p);
   a.glog = static_cast<uint64_t*>(e->d_glog.p);
   a.glink = static_cast<uint32_t*>(e->d_glink.p);
-  a.ghead = static_cast<uint16_t*>(e->d_ghead.p);
   a.counters = static_cast<uint2*>(e->d_roll_cnt.p);
   a.out = static_cast<double*>(e->d_rollout_out.p);
   a.zob = static_cast<const uint64_t*>(e->d_zob.p);

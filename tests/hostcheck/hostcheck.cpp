@@ -38,7 +38,7 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
     ctx.zob = game.zob.data();
     ctx.base = root.hashes.data();
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
-    logbuf.bind(&ctx, 256, game.cfg.rows * game.cfg.cols);
+    logbuf.bind(&ctx, 248, game.cfg.rows * game.cfg.cols);
     ctx.init_filters();
   }
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
@@ -354,7 +354,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
         c.zob = game.zob.data();
         c.base = hs.hashes.data();
         c.n_base = static_cast<int32_t>(hs.hashes.size());
-        logbuf.bind(&c, 256, game.cfg.rows * game.cfg.cols);
+        logbuf.bind(&c, 248, game.cfg.rows * game.cfg.cols);
         c.init_filters();
         r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg, c, ev);
         break;
