@@ -56,6 +56,9 @@ CONFIGS = {
     # SURVEY §8f rank 1 (not a BASELINE config): full self-play games, two
     # MCTSBots + one shared evaluator per game, one wave per game.
     "sp": ("selfplay", "connect_four", 4096, 256, 4),
+    # SURVEY §8f rank 2 (not a BASELINE config): PUCT search with an external
+    # (network) evaluator, batched across searches; AlphaZero root noise.
+    "az": ("az", "connect_four", 16384, 128, 4),
 }
 KERNEL = {"wave": "k_wsearch", "lane": "k_mcts"}
 
@@ -200,7 +203,7 @@ def main():
   layouts = {"auto": _lib.LAYOUT_AUTO, "wave": _lib.LAYOUT_WAVE, "lane": _lib.LAYOUT_LANE}
   mode = CONFIGS[args.config][0]
   fn = {"search": bench_search, "root_parallel": bench_root_parallel,
-        "playouts": bench_playouts, "selfplay": bench_selfplay}[mode]
+        "playouts": bench_playouts, "selfplay": bench_selfplay, "az": bench_az}[mode]
   line = fn(args, ctx, layouts[args.layout])
   if ctx.rank == 0:
     if ctx.rehearse:
@@ -524,6 +527,123 @@ def bench_selfplay(args, ctx, layout):
   line["outcomes"] = {"p0_wins": int((out["returns"][:, 0] > 0).sum()),
                       "p1_wins": int((out["returns"][:, 0] < 0).sum()),
                       "draws": int((out["returns"][:, 0] == 0).sum())}
+  return line
+
+
+# ---------------------------------------------------------------------------
+# az: external-evaluator PUCT search
+def _az_network(obs_size, A, torch, dev, hidden=256):
+  """A random-init policy/value MLP standing in for the AlphaZero network
+  (bf16 matmuls, f64 priors/values at the boundary)."""
+  g = torch.Generator().manual_seed(0)
+  w1 = (torch.randn(obs_size, hidden, generator=g) / obs_size ** 0.5).to(dev, torch.bfloat16)
+  wp = (torch.randn(hidden, A, generator=g) / hidden ** 0.5).to(dev, torch.bfloat16)
+  wv = (torch.randn(hidden, 1, generator=g) / hidden ** 0.5).to(dev, torch.bfloat16)
+
+  def evaluator(obs, legal, kind):
+    x = obs.reshape(obs.shape[0], -1).to(torch.bfloat16)
+    h = torch.relu(x @ w1)
+    logits = (h @ wp).double().masked_fill(~legal, float("-inf"))
+    prior = torch.softmax(logits, dim=-1).nan_to_num(0.0)
+    value = torch.tanh((h @ wv).double()).squeeze(-1)
+    return prior, value
+  return evaluator
+
+
+def _az_toy_evaluator(A, torch):
+  sys.path.insert(0, os.path.join(ROOT, "tests"))
+  from test_az import toy_eval
+
+  def evaluator(obs, legal, kind):
+    ob = obs.cpu().numpy().reshape(obs.shape[0], -1)
+    lg, kd = legal.cpu().numpy(), kind.cpu().numpy()
+    pr = np.zeros((ob.shape[0], A), np.float64)
+    v = np.zeros(ob.shape[0], np.float64)
+    for i in np.nonzero(kd)[0]:
+      pr[i], v[i] = toy_eval(ob[i], lg[i], int(kd[i]))
+    return torch.from_numpy(pr).to(obs.device), torch.from_numpy(v).to(obs.device)
+  return evaluator
+
+
+def bench_az(args, ctx, layout):
+  """One step = every search of the rank's batch run to completion: k_az_step
+  launches alternating with one batched network call per launch."""
+  from os_amd import engine as E
+  from os_amd.az import ExternalEvaluatorSearch
+  torch = ctx.torch
+  _, game, R, sims, plies = CONFIGS[args.config]
+  R = args.roots or R
+  sims = args.sims or sims
+  alpha, eps, c = 1.0, 0.25, 1.25
+  base = ctx.rank * R
+  acts, offs = E.make_roots(game, R, seed_base=1000 + base, max_plies=plies)
+  seeds = np.arange(base, base + R, dtype=np.uint32)
+  search = ExternalEvaluatorSearch(game, device=ctx.local)
+  A = search.num_actions
+  obs_size = int(np.prod(search.obs_shape))
+  net = _az_network(obs_size, A, torch, ctx.dev)
+  kw = dict(puct=True, max_simulations=sims, uct_c=c, dirichlet_alpha=alpha,
+            dirichlet_epsilon=eps, stream=ctx.stream)
+  parity = None
+  if ctx.rank == 0:  # exact toy evaluator on a prefix vs the oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_az
+    pr = min(args.parity_roots, R)
+    got = search.run(acts[:offs[pr]], offs[:pr + 1], seeds[:pr], _az_toy_evaluator(A, torch),
+                     **kw)
+    ref = _oracle(game).mcts_external(
+        acts[:offs[pr]], offs[:pr + 1], seeds[:pr], test_az._oracle_eval_fn(game), puct=True,
+        uct_c=c, max_simulations=sims, max_children=search.eng.max_children,
+        dirichlet_alpha=alpha, dirichlet_epsilon=eps)
+    bad = [k for k in E.OUTPUT_KEYS if not np.array_equal(got[k], ref[k])]
+    parity = {"roots_checked": pr, "evaluator": "exact toy (tests/test_az.py)",
+              "bit_exact": not bad, "mismatch_fields": bad}
+
+  def step():
+    search.run(acts, offs, seeds, net, **kw)
+
+  for _ in range(args.warmup):
+    step()
+  elapsed, _ = ctx.timed(step, args.steps)
+  # One more instrumented run: per-launch k_az_step time and the tree stats.
+  search.run(acts, offs, seeds, net, time_steps=True, **kw)
+  step_ms = search.step_ms()
+  launches = search.steps
+  requests = search.requests
+  st = search.eng.stats()  # of the run's final os_az_fetch
+  sims_step = st["sims"]
+  total_sims = ctx.total(sims_step * args.steps)
+  if ctx.rank != 0:
+    return None
+  # Algorithmic bytes of the k_az_step launches of one search batch
+  # (DESIGN.md §7): tree traffic as in the search kernels with 24-B f64 nodes
+  # plus an 8-B prior per child read by PUCT; per request, the observation,
+  # legal mask and kind written and the response read; per launch per live
+  # search, its continuation header + working state read and written.
+  sb = st["state_bytes"]
+  nb = 24
+  tree = (st["scanned"] * (nb + 8) + st["backed"] * 2 * nb + st["expanded"] * (nb + 8) +
+          st["solver_scanned"] * nb + st["rng_words"] * 8)
+  io = requests * (obs_size * 4 + A + 4 + A * 8 + 8)
+  cont = requests * 2 * (sb + 64)
+  alg = tree + io + cont
+  kernel_ms = step_ms / max(launches, 1)
+  line = _base_line(args, ctx, "PUCT MCTS simulations/sec with a batched network evaluator "
+                    "on %s" % game, total_sims / elapsed, "sims/s", elapsed, {
+                        "workload": "%s, %d searches x %d sims per GPU, PUCT c=%g, Dirichlet "
+                                    "alpha=%g eps=%g, random-init MLP evaluator (bf16, %d "
+                                    "hidden) on the same GPU" % (game, R, sims, c, alpha, eps, 256),
+                        "game": game, "searches_per_gpu": R, "sims_per_search": sims,
+                        "parallelism": "dp%d (independent searches)" % ctx.world,
+                        "layout": "lane (continuation in HBM)"})
+  line["az"] = {"launches_per_step": launches, "requests_per_step": requests,
+                "k_az_step_ms_total": step_ms,
+                "k_az_step_share_of_step": step_ms / (elapsed / max(args.steps, 1) * 1e3)}
+  line["roofline"] = _roofline("k_az_step", game, alg / max(launches, 1), kernel_ms,
+                               requests / max(launches, 1), "request")
+  line["cpu_baseline"] = None
+  line["parity"] = parity
+  line["tree_stats"] = st
   return line
 
 

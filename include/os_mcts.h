@@ -184,14 +184,24 @@ int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
  *   dev_value[r]         f64 player-0 value
  * *dev_pending = number of requests written by the last step (0 = all done).
  * os_az_fetch then returns the root statistics (os_mcts_batch layout).
- * Supported: tic_tac_toe, connect_four, breakthrough, hex (go needs its
- * superko history context: OS_ERR_UNSUPPORTED); C++ policy; no Dirichlet
- * noise (mcts.cc:177-192, alpha = 0). */
+ * dirichlet_alpha > 0 mixes Dirichlet noise into the root's priors,
+ * (1 - dirichlet_epsilon) * prior + dirichlet_epsilon * noise, drawn from the
+ * bot rng_ before the root's shuffle (MCTSBot ctor dirichlet_alpha /
+ * dirichlet_epsilon, mcts.h:152-159; dirichlet_noise mcts.cc:177-192, used at
+ * :265-273); alpha = 0 disables it.  Noise with a memory budget small enough
+ * for GC to fire (the root could be re-expanded) is OS_ERR_UNSUPPORTED.
+ * All five games (go's superko set travels in the continuation); C++ policy. */
 int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
                   const int64_t* root_actions, const int64_t* root_offsets,
-                  const uint32_t* bot_seeds, int32_t* dev_kind, float* dev_obs,
+                  const uint32_t* bot_seeds, double dirichlet_alpha,
+                  double dirichlet_epsilon, int32_t* dev_kind, float* dev_obs,
                   uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
                   int32_t* dev_pending);
+/* The Dirichlet noise os_az_prepare draws for one fresh MCTSBot(seed) at a
+ * root with `count` legal actions: out[count] (normalised, legal-action
+ * order); returns the MT19937 words consumed (< 0 on error).  Exposed so the
+ * noise can be checked against libstdc++ directly. */
+int64_t os_dirichlet_noise(uint32_t seed, int32_t count, double alpha, double* out);
 int os_az_step_async(os_engine* e, void* hip_stream);
 int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32_t* child_n,
                 double* child_w, int8_t* child_out, int32_t* nchild, int32_t* root_n,

@@ -13,6 +13,18 @@
 // PUCT (mcts.cc:102-111); backup, MCTS-Solver, early stop and GC are those of
 // mcts.cc:325-428 (same code shape as os_mcts.h::mcts_search).  Results are
 // bit-exact with the reference MCTSBot driving the same evaluator.
+//
+// Dirichlet root noise (mcts.cc:177-192, applied at :265-273): the reference
+// draws std::gamma_distribution<double>(alpha, 1) from the bot rng_ at the
+// root's expansion, before the shuffle.  The gamma sampler is libstdc++'s
+// (Marsaglia-Tsang over a polar-method normal, with libm log / sqrt / pow), so
+// its bits are only reproducible with that library: the host runtime draws it
+// at prepare time with the real std::gamma_distribution over the same
+// mt19937(seed) stream (a fresh bot's rng_ is untouched until the root
+// expands) and hands the kernel the normalised noise and the number of words
+// it consumed; the kernel mixes the priors and advances its stream by that
+// count.  go's positional-superko set of the pending simulation lives in the
+// continuation (AzLog), so searches resume mid-descent with it intact.
 #ifndef OS_AZ_H_
 #define OS_AZ_H_
 
@@ -22,6 +34,46 @@ namespace osm {
 
 enum AzStage : int32_t { kAzStart = 0, kAzWaitPrior = 1, kAzWaitValue = 2, kAzDone = 3 };
 enum AzRequest : int32_t { kAzNone = 0, kAzPrior = 1, kAzValue = 2 };
+
+constexpr int kAzLogCap = 248;  // go: positions after the root on one tree path (<= 2 * 11 * 11)
+constexpr int kAzHeads = 122;   // go: stone-count buckets, 0 .. 11 * 11
+
+// go's position log of the pending simulation (GoCtx arrays + fill count);
+// empty for games without a history context.
+template <bool kLog>
+struct AzLog {};
+template <>
+struct AzLog<true> {
+  uint64_t log[kAzLogCap];
+  uint32_t link[kAzLogCap];
+  uint8_t head[kAzHeads];
+  int32_t n_log;
+};
+
+OS_HD void az_bind_log(NoCtx&, AzLog<false>&, bool) {}
+OS_HD void az_save_log(const NoCtx&, AzLog<false>&) {}
+// Points the context at the continuation's log; `resume` restores the count
+// (a fresh search resets it at its first simulation).
+OS_HD void az_bind_log(GoCtx& c, AzLog<true>& m, bool resume) {
+  c.log = m.log;
+  c.link = m.link;
+  c.head = m.head;
+  c.stride = 1;
+  c.head_stride = 1;
+  c.cap = kAzLogCap;
+  c.n_log = resume ? m.n_log : 0;
+  c.init_base_filter();
+}
+OS_HD void az_save_log(const GoCtx& c, AzLog<true>& m) { m.n_log = c.n_log; }
+
+// Dirichlet root noise of one search, drawn by the host (see above):
+// noise[j] pairs with the j-th legal action in ascending order; `skip` = MT
+// words the draws consumed.  noise == nullptr: alpha = 0 (no noise).
+struct AzNoise {
+  const double* noise;
+  int32_t skip;
+  double eps;
+};
 
 // Per-search continuation, resident in HBM between steps.
 template <class G>
@@ -37,6 +89,7 @@ struct AzSlot {
   uint32_t used;
   SearchResult res;
   uint32_t path[kMaxPath];
+  AzLog<G::State::kNeedsLog> glog;
 };
 
 // One search's request / response views (caller-owned buffers).
@@ -50,8 +103,7 @@ struct AzIo {
 
 template <class G>
 OS_HD void az_request(const GameCfg& g, const typename G::State& s, int kind, const AzIo& io,
-                      int obs_size, int num_actions) {
-  typename G::Ctx ctx;
+                      int obs_size, int num_actions, typename G::Ctx& ctx) {
   *io.kind = kind;
   const int cells = g.rows * g.cols;
   const int p = G::to_move(s);
@@ -62,14 +114,15 @@ OS_HD void az_request(const GameCfg& g, const typename G::State& s, int kind, co
 }
 
 // Advances one search until it needs the evaluator (request written, returns)
-// or finishes (kind = kAzNone, stage = kAzDone).  Games with a history
-// context (go superko) are not supported on this path.
+// or finishes (kind = kAzNone, stage = kAzDone).  `ctx` is the game's
+// history context with its root fields set (go: Zobrist table, the positions
+// before the root, n_heads); its log is bound to the continuation here.
 template <class G>
 OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
                    const typename G::State& root, AzSlot<G>& sl, Node<double>* nodes,
                    double* prior, uint32_t cap, MtStream& bot, const AzIo& io, int obs_size,
-                   int num_actions) {
-  typename G::Ctx ctx;
+                   int num_actions, typename G::Ctx& ctx, const AzNoise& nz) {
+  az_bind_log(ctx, sl.glog, sl.stage != kAzStart);
   const int P0 = G::to_move(root);
   const double inf = __builtin_huge_val();
   typename G::State s = sl.s;
@@ -109,6 +162,7 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
     if (phase == 0) {
       if (sl.sim >= sp.max_simulations) break;
       s = root;
+      ctx.reset();
       depth = 0;
       sl.path[0] = 0;
       phase = 1;
@@ -123,12 +177,16 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         sl.res.status = kArenaOverflow;
         break;
       }
+      const bool noisy = x == 0 && nz.noise != nullptr;
+      if (noisy)  // dirichlet_noise consumed these words of rng_ (mcts.cc:265-267)
+        for (int i = 0; i < nz.skip; ++i) bot.next();
       uint8_t perm[kMaxChildren];
       for (int k = 0; k < nc; ++k) perm[k] = static_cast<uint8_t>(k);
       CppShuffle(perm, nc, bot);
       const uint32_t first = sl.used;
       for (int k = 0; k < nc; ++k) {
-        const int a = l.kth(perm[k]);
+        const int j = perm[k];
+        const int a = l.kth(j);
         Node<double>& c = nodes[first + k];
         c.first = 0;
         c.n = 0;
@@ -136,7 +194,9 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         c.action = static_cast<uint16_t>(a);
         c.nchild = 0;
         c.out = kUnsolved;
-        prior[first + k] = io.prior[a];
+        // (1 - eps) * p + eps * noise, separately rounded (mcts.cc:269-271)
+        prior[first + k] = noisy ? (1.0 - nz.eps) * io.prior[a] + nz.eps * nz.noise[j]
+                                 : io.prior[a];
       }
       nodes[x].first = first;
       nodes[x].nchild = static_cast<uint8_t>(nc);
@@ -153,8 +213,9 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         if (nx.nchild == 0) {
           sl.s = s;
           sl.depth = depth;
+          az_save_log(ctx, sl.glog);
           sl.stage = kAzWaitPrior;
-          az_request<G>(g, s, kAzPrior, io, obs_size, num_actions);
+          az_request<G>(g, s, kAzPrior, io, obs_size, num_actions, ctx);
           return;
         }
         const int cp = P0 ^ (depth & 1);
@@ -203,8 +264,9 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
       } else {
         sl.s = s;
         sl.depth = depth;
+        az_save_log(ctx, sl.glog);
         sl.stage = kAzWaitValue;
-        az_request<G>(g, s, kAzValue, io, obs_size, num_actions);
+        az_request<G>(g, s, kAzValue, io, obs_size, num_actions, ctx);
         return;
       }
     }

@@ -533,12 +533,11 @@ int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
 
 int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
               const int64_t* root_actions, const int64_t* root_offsets,
-              const uint32_t* bot_seeds, int32_t* kind, float* obs, uint8_t* legal,
-              const double* prior, const double* value, int32_t* pending) {
+              const uint32_t* bot_seeds, double alpha, double eps, int32_t* kind, float* obs,
+              uint8_t* legal, const double* prior, const double* value, int32_t* pending) {
   if (!p) return Fail(OS_ERR_INVALID, "null params");
-  if (e->game.cfg.kind == kGo)
-    return Fail(OS_ERR_UNSUPPORTED,
-                "external-evaluator search does not support go (superko history context)");
+  if (!(alpha >= 0.0) || !(eps >= 0.0) || eps > 1.0)
+    return Fail(OS_ERR_INVALID, "dirichlet_alpha must be >= 0 and epsilon in [0, 1]");
   if (p->policy != OS_POLICY_CPP)
     return Fail(OS_ERR_UNSUPPORTED, "external-evaluator search implements the C++ MCTSBot");
   if (R > 0 && (!kind || !obs || !legal || !prior || !value || !pending || !bot_seeds))
@@ -558,6 +557,36 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
       (rc = e->d_az_prior.ensure(Rz * static_cast<size_t>(e->cap) * 8)))
     return rc;
   HIP_TRY(hipMemset(e->d_az_slots.p, 0, Rz * slot_bytes));  // stage kAzStart
+  e->az_noise = alpha > 0.0;
+  e->az_eps = eps;
+  if (e->az_noise) {
+    // The root expands once unless GC clears its children (mcts.cc:430-443);
+    // the noise is drawn ahead for that one expansion.
+    const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+    const int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * e->game.cfg.max_children;
+    if (max_nodes > 1 && worst >= max_nodes)
+      return Fail(OS_ERR_UNSUPPORTED,
+                  "Dirichlet noise with a max_memory_mb small enough for GC to fire");
+    const int mc = e->game.cfg.max_children;
+    std::vector<double> noise(Rz * mc, 0.0);
+    std::vector<int32_t> skip(Rz, 0);
+    std::vector<int64_t> acts;
+    for (int64_t r = 0; r < R; ++r) {
+      HostState hs;
+      std::string err;
+      ReplayRoot(e->game, root_actions + root_offsets[r], root_offsets[r + 1] - root_offsets[r],
+                 &hs, &err);
+      StateLegal(hs, &acts);
+      const int64_t w = DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
+                                       noise.data() + r * mc);
+      if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
+      skip[r] = static_cast<int32_t>(w);
+    }
+    if ((rc = e->d_az_noise.ensure(noise.size() * 8)) || (rc = e->d_az_skip.ensure(Rz * 4)))
+      return rc;
+    HIP_TRY(hipMemcpy(e->d_az_noise.p, noise.data(), noise.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_az_skip.p, skip.data(), Rz * 4, hipMemcpyHostToDevice));
+  }
   e->az_puct = puct ? 1 : 0;
   e->az_kind = kind;
   e->az_obs = obs;
@@ -933,12 +962,20 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
 
 int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
                   const int64_t* root_actions, const int64_t* root_offsets,
-                  const uint32_t* bot_seeds, int32_t* dev_kind, float* dev_obs,
+                  const uint32_t* bot_seeds, double dirichlet_alpha,
+                  double dirichlet_epsilon, int32_t* dev_kind, float* dev_obs,
                   uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
                   int32_t* dev_pending) {
   if (!e) return Fail(OS_ERR_INVALID, "null engine");
-  return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, bot_seeds, dev_kind,
-                   dev_obs, dev_legal, dev_prior, dev_value, dev_pending);
+  return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, bot_seeds,
+                   dirichlet_alpha, dirichlet_epsilon, dev_kind, dev_obs, dev_legal, dev_prior,
+                   dev_value, dev_pending);
+}
+
+int64_t os_dirichlet_noise(uint32_t seed, int32_t count, double alpha, double* out) {
+  if (count < 0 || (count > 0 && !out)) return Fail(OS_ERR_INVALID, "null argument");
+  if (!(alpha > 0.0)) return Fail(OS_ERR_INVALID, "alpha must be > 0");
+  return DirichletNoise(seed, count, alpha, out);
 }
 
 int os_az_step_async(os_engine* e, void* hip_stream) {

@@ -133,6 +133,17 @@ struct AzArgs {
   const double* prior_in;   // [R][A]
   const double* value_in;   // [R]
   int32_t* pending;         // requests written by this step
+  // Dirichlet root noise (alpha > 0): [R][noise_stride] normalised draws in
+  // legal-action order + MT words they consumed (host-drawn, os_az.h)
+  const double* noise;      // null: no noise
+  const int32_t* noise_skip;
+  int32_t noise_stride;
+  double noise_eps;
+  // go: superko context of each root
+  const uint64_t* zob;
+  const uint64_t* root_hashes;  // [R][hash_stride]
+  const int32_t* root_nhash;    // [R]
+  int32_t hash_stride;
   // outputs (same layout as the search kernels)
   SearchResult* results;
   int32_t max_children;
@@ -224,7 +235,9 @@ struct os_engine {
   const double* az_prior = nullptr;
   const double* az_value = nullptr;
   int32_t* az_pending = nullptr;
-  osx::DevBuf d_az_slots, d_az_prior;
+  double az_eps = 0.0;
+  bool az_noise = false;
+  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip;
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -237,7 +250,7 @@ struct os_engine {
                      &d_cn,    &d_cw,    &d_cout,  &d_nch, &d_rn,    &d_rw,
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
-                     &d_az_slots, &d_az_prior, &d_glog, &d_glink,
+                     &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();

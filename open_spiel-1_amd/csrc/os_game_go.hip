@@ -3,4 +3,4 @@
 // No external-evaluator search for go (superko history; os_az.h).
 #include "os_kernels.h"
 
-OS_DEFINE_LAUNCHERS(Go, 0)
+OS_DEFINE_LAUNCHERS(Go, 1)

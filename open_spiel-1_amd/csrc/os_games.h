@@ -502,9 +502,13 @@ struct GoCtx {
   }
   // Builds base_filt from base[0, n_base) and resets.
   OS_HD void init_filters() {
+    init_base_filter();
+    reset();
+  }
+  // Builds base_filt only: a resumed search keeps its log (os_az.h).
+  OS_HD void init_base_filter() {
     base_filt.clear();
     for (int i = 0; i < n_base; ++i) base_filt.add(fbit(base[i]));
-    reset();
   }
   OS_HD static int fbit(uint64_t h) { return static_cast<int>(h >> 56); }
   OS_HD bool contains(uint64_t h, int stones) const {

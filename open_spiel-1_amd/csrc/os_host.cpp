@@ -15,6 +15,34 @@
 #include <type_traits>
 
 namespace osm {
+
+namespace {
+// A std::mt19937 that counts the words drawn from it (same URBG range, so
+// generate_canonical consumes it exactly as it consumes the engine itself).
+struct CountingMt {
+  using result_type = uint32_t;
+  std::mt19937 g;
+  int64_t words = 0;
+  explicit CountingMt(uint32_t seed) : g(seed) {}
+  static constexpr result_type min() { return std::mt19937::min(); }
+  static constexpr result_type max() { return std::mt19937::max(); }
+  result_type operator()() {
+    ++words;
+    return static_cast<result_type>(g());
+  }
+};
+}  // namespace
+
+int64_t DirichletNoise(uint32_t seed, int count, double alpha, double* out) {
+  CountingMt rng(seed);
+  std::gamma_distribution<double> gamma(alpha, 1.0);
+  for (int i = 0; i < count; ++i) out[i] = gamma(rng);
+  double sum = 0.0;
+  for (int i = 0; i < count; ++i) sum += out[i];  // absl::c_accumulate(noise, 0.0)
+  for (int i = 0; i < count; ++i) out[i] /= sum;
+  return rng.words;
+}
+
 namespace {
 
 bool ParseGameString(const std::string& s, std::string* name,

@@ -54,6 +54,12 @@ struct HostState {
 // repetitions_ set, go.h:105-120) and whose log is empty, in `buf`.
 GoCtx HostGoCtx(const HostState& s, HostGoLog* buf);
 
+// dirichlet_noise(count, alpha, &rng_) of mcts.cc:177-192 drawn from a fresh
+// std::mt19937(seed) with libstdc++'s own std::gamma_distribution<double>
+// (its Marsaglia-Tsang sampler and libm calls make the bits), normalised by
+// the left-fold sum; writes out[count] and returns the MT words consumed.
+int64_t DirichletNoise(uint32_t seed, int count, double alpha, double* out);
+
 // Parses and validates a game string; returns "" on success, else a message.
 // `unsupported` is set when the game/parameters are valid OpenSpiel but not
 // supported by this engine.

@@ -407,6 +407,24 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
 }
 
 
+// The root fields of the history context; az_step binds the log to the
+// search's continuation.
+template <class G>
+struct AzCtx {
+  __device__ static NoCtx make(const AzArgs&, int64_t) { return NoCtx(); }
+};
+template <>
+struct AzCtx<Go> {
+  __device__ static GoCtx make(const AzArgs& a, int64_t r) {
+    GoCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + r * a.hash_stride;
+    c.n_base = a.root_nhash[r];
+    c.n_heads = a.cfg.rows * a.cfg.cols + 1;
+    return c;
+  }
+};
+
 template <class G>
 __global__ void k_az_step(AzArgs a) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -434,10 +452,16 @@ __global__ void k_az_step(AzArgs a) {
   io.legal = a.legal + r * a.num_actions;
   io.prior = a.prior_in + r * a.num_actions;
   io.value = a.value_in + r;
+  AzNoise nz;
+  nz.noise = a.noise ? a.noise + r * a.noise_stride : nullptr;
+  nz.skip = a.noise ? a.noise_skip[r] : 0;
+  nz.eps = a.noise_eps;
+  typename G::Ctx ctx = AzCtx<G>::make(a, r);
   az_step<G>(a.cfg, a.sp, a.puct, root, sl, nodes, a.priors + r * static_cast<int64_t>(a.cap),
-             a.cap, bot, io, a.obs_size, a.num_actions);
+             a.cap, bot, io, a.obs_size, a.num_actions, ctx, nz);
   sl.mt_idx = bot.idx;
   sl.mt_pre = bot.pre;
+  sl.res.rng_words += bot.words;
   if (*io.kind != kAzNone) {
     atomicAdd(a.pending, 1);
     return;
@@ -717,6 +741,16 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.prior_in = e->az_prior;
   a.value_in = e->az_value;
   a.pending = e->az_pending;
+  if (e->az_noise) {
+    a.noise = static_cast<const double*>(e->d_az_noise.p);
+    a.noise_skip = static_cast<const int32_t*>(e->d_az_skip.p);
+    a.noise_stride = e->game.cfg.max_children;
+    a.noise_eps = e->az_eps;
+  }
+  a.zob = d.zob;
+  a.root_hashes = d.root_hashes;
+  a.root_nhash = d.root_nhash;
+  a.hash_stride = d.hash_stride;
   a.results = d.results;
   a.max_children = d.max_children;
   a.child_action = d.child_action;

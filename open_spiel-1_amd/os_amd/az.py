@@ -47,7 +47,15 @@ class ExternalEvaluatorSearch:
 
   def run(self, root_actions, root_offsets, bot_seeds, evaluator, puct=True,
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
-          stream=None):
+          dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False):
+    """Runs every search to completion; returns the os_mcts_batch outputs.
+
+    dirichlet_alpha / dirichlet_epsilon are the MCTSBot constructor's
+    (mcts.h:152-159): root priors become (1 - eps) * p + eps * Dir(alpha)
+    noise drawn from the bot's rng before the root's shuffle (mcts.cc:265-273).
+    time_steps: record a HIP event pair around every k_az_step launch on the
+    launch stream (`step_ms()` then sums them).
+    """
     torch = self.torch
     offs = _lib.i64(root_offsets)
     R = len(offs) - 1
@@ -64,14 +72,22 @@ class ExternalEvaluatorSearch:
     acts = _lib.i64(root_actions)
     bs = _lib.u32(bot_seeds)
     check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
-                            ptr(offs), ptr(bs), kind.data_ptr(), obs.data_ptr(),
+                            ptr(offs), ptr(bs), float(dirichlet_alpha),
+                            float(dirichlet_epsilon), kind.data_ptr(), obs.data_ptr(),
                             legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
                             pending.data_ptr()))
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     self.steps = 0
     self.requests = 0
+    self.events = []
     while True:
+      if time_steps:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
       check(lib.os_az_step_async(self.eng._h, st.cuda_stream))
+      if time_steps:
+        e1.record(st)
+        self.events.append((e0, e1))
       self.steps += 1
       n = int(pending.item())  # synchronises the stream
       if n == 0:
@@ -84,3 +100,7 @@ class ExternalEvaluatorSearch:
     o = E._alloc_outputs(R, self.eng.max_children)
     check(lib.os_az_fetch(self.eng._h, self.eng.max_children, *E._out_ptrs(o)))
     return o
+
+  def step_ms(self):
+    """Summed k_az_step time of the last run(time_steps=True), ms."""
+    return sum(a.elapsed_time(b) for a, b in self.events)

@@ -328,11 +328,13 @@ class CallbackEvaluator : public oref::Evaluator {
 };
 
 // MCTSBot::MCTSearch with an external evaluator and UCT (puct = 0) or PUCT
-// (puct = 1) child selection (mcts.cc:297-304), one bot seed per root; same
-// output layout as oref_mcts_batch.
+// (puct = 1) child selection (mcts.cc:297-304) and Dirichlet root noise when
+// dirichlet_alpha > 0 (mcts.cc:265-273), one bot seed per root; same output
+// layout as oref_mcts_batch.
 int oref_mcts_external(void* g, int64_t num_roots, const int64_t* root_actions,
                        const int64_t* root_offsets, double uct_c, int32_t max_simulations,
                        int64_t max_memory_mb, int32_t solve, int32_t puct,
+                       double dirichlet_alpha, double dirichlet_epsilon,
                        const uint32_t* bot_seeds, oref_eval_cb cb, int32_t max_children,
                        int32_t* child_action, int32_t* child_n, double* child_w,
                        int8_t* child_out, int32_t* nchild, int32_t* root_n, double* root_w,
@@ -345,7 +347,7 @@ int oref_mcts_external(void* g, int64_t num_roots, const int64_t* root_actions,
     auto state = Replay(*og->game, root_actions + root_offsets[r],
                         root_offsets[r + 1] - root_offsets[r]);
     MCTSBot bot(*og->game, &ev, uct_c, max_simulations, max_memory_mb, solve != 0,
-                bot_seeds[r], puct != 0);
+                bot_seeds[r], puct != 0, dirichlet_alpha, dirichlet_epsilon);
     SearchStats st;
     auto root = bot.MCTSearch(*state, &st);
     FillOut(*root, max_children, r, st, o);

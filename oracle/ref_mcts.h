@@ -13,6 +13,7 @@
 #include <cmath>
 #include <limits>
 #include <memory>
+#include <numeric>
 #include <random>
 #include <vector>
 
@@ -116,13 +117,27 @@ struct SearchStats {
   int sims_run = 0;
 };
 
-// mcts.cc:194-443, UCT policy, no Dirichlet noise (alpha = 0).
+// mcts.cc:177-192: gamma(alpha, 1) draws from the bot rng, normalised by
+// their left-fold sum (absl::c_accumulate).
+inline std::vector<double> DirichletNoise(int count, double alpha, std::mt19937* rng) {
+  std::vector<double> noise;
+  noise.reserve(count);
+  std::gamma_distribution<double> gamma(alpha, 1.0);
+  for (int i = 0; i < count; ++i) noise.emplace_back(gamma(*rng));
+  double sum = std::accumulate(noise.begin(), noise.end(), 0.0);
+  for (double& v : noise) v /= sum;
+  return noise;
+}
+
+// mcts.cc:194-443: UCT or PUCT child selection, optional Dirichlet root noise.
 class MCTSBot {
  public:
   MCTSBot(const RGame& game, Evaluator* evaluator, double uct_c,
           int max_simulations, int64_t max_memory_mb, bool solve, uint32_t seed,
-          bool puct = false)
-      : puct_(puct),
+          bool puct = false, double dirichlet_alpha = 0.0, double dirichlet_epsilon = 0.0)
+      : dirichlet_alpha_(dirichlet_alpha),
+        dirichlet_epsilon_(dirichlet_epsilon),
+        puct_(puct),
         uct_c_(uct_c),
         max_simulations_(max_simulations),
         max_nodes_(static_cast<int>((max_memory_mb << 20) / kNodeBytes + 1)),
@@ -209,6 +224,12 @@ class MCTSBot {
     while (!ws->IsTerminal() && cur->explore_count > 0) {
       if (cur->children.empty()) {
         auto legal = evaluator_->Prior(*ws);
+        if (cur == root && dirichlet_alpha_ > 0) {  // mcts.cc:265-273
+          std::vector<double> noise = DirichletNoise(legal.size(), dirichlet_alpha_, &rng_);
+          for (size_t i = 0; i < legal.size(); ++i)
+            legal[i].second =
+                (1 - dirichlet_epsilon_) * legal[i].second + dirichlet_epsilon_ * noise[i];
+        }
         std::shuffle(legal.begin(), legal.end(), rng_);
         Player player = ws->CurrentPlayer();
         cur->children.reserve(legal.size());
@@ -243,6 +264,8 @@ class MCTSBot {
     }
   }
 
+  double dirichlet_alpha_;
+  double dirichlet_epsilon_;
   bool puct_;
   double uct_c_;
   int max_simulations_;

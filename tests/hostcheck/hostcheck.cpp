@@ -164,9 +164,9 @@ typedef int (*hc_az_cb)(const float* obs, int32_t obs_size, const uint8_t* legal
 namespace {
 template <class G>
 int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp, int puct,
-             uint32_t seed, uint32_t cap, hc_az_cb cb, int32_t mc, int32_t* ca, int32_t* cn,
-             double* cw, int8_t* co, int32_t* nch, int32_t* rn, double* rw, int8_t* ro,
-             int64_t* ba, int32_t* nd) {
+             uint32_t seed, double alpha, double eps, uint32_t cap, hc_az_cb cb, int32_t mc,
+             int32_t* ca, int32_t* cn, double* cw, int8_t* co, int32_t* nch, int32_t* rn,
+             double* rw, int8_t* ro, int64_t* ba, int32_t* nd) {
   const int A = game.cfg.num_actions;
   const int obs_size = ObservationShape(game, nullptr);
   std::vector<Node<double>> nodes(cap);
@@ -184,9 +184,26 @@ int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp
   std::memset(sl.get(), 0, sizeof(AzSlot<G>));
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
   sl->s = rs;
+  typename G::Ctx ctx;
+  if constexpr (G::State::kNeedsLog) {
+    std::memset(&ctx, 0, sizeof ctx);
+    ctx.zob = game.zob.data();
+    ctx.base = root.hashes.data();
+    ctx.n_base = static_cast<int32_t>(root.hashes.size());
+    ctx.n_heads = game.cfg.rows * game.cfg.cols + 1;
+  }
+  std::vector<double> noise(game.cfg.max_children, 0.0);
+  AzNoise nz{nullptr, 0, eps};
+  if (alpha > 0) {
+    std::vector<int64_t> acts;
+    StateLegal(root, &acts);
+    nz.skip = static_cast<int32_t>(
+        DirichletNoise(seed, static_cast<int>(acts.size()), alpha, noise.data()));
+    nz.noise = noise.data();
+  }
   for (;;) {
     az_step<G>(game.cfg, sp, puct, rs, *sl, nodes.data(), prior.data(), cap, bot, io, obs_size,
-               A);
+               A, ctx, nz);
     if (kind == kAzNone) break;
     std::fill(pri.begin(), pri.end(), 0.0);
     cb(obs.data(), obs_size, legal.data(), A, kind, pri.data(), &value);
@@ -219,7 +236,7 @@ extern "C" {
 
 int hc_az_batch(const char* game_string, int64_t num_roots, const int64_t* root_actions,
                 const int64_t* root_offsets, double uct_c, int32_t max_simulations,
-                int64_t max_memory_mb, int32_t solve, int32_t puct,
+                int64_t max_memory_mb, int32_t solve, int32_t puct, double alpha, double eps,
                 const uint32_t* bot_seeds, hc_az_cb cb, int32_t max_children,
                 int32_t* child_action, int32_t* child_n, double* child_w, int8_t* child_out,
                 int32_t* nchild, int32_t* root_n, double* root_w, int8_t* root_out,
@@ -252,7 +269,7 @@ int hc_az_batch(const char* game_string, int64_t num_roots, const int64_t* root_
     const int64_t o = r * max_children;
     int rc = 0;
 #define HC_AZ(G)                                                                          \
-  rc = AzRunOne<G>(game, hs, sp, puct, bot_seeds[r], cap, cb, max_children,               \
+  rc = AzRunOne<G>(game, hs, sp, puct, bot_seeds[r], alpha, eps, cap, cb, max_children,  \
                    child_action + o, child_n + o, child_w + o, child_out + o, nchild + r, \
                    root_n + r, root_w + r, root_out + r, best_action + r, nodes + r)
     switch (game.cfg.kind) {
@@ -260,12 +277,18 @@ int hc_az_batch(const char* game_string, int64_t num_roots, const int64_t* root_
       case kConnectFour: HC_AZ(ConnectFour); break;
       case kBreakthrough: HC_AZ(Breakthrough); break;
       case kHex: HC_AZ(Hex); break;
+      case kGo: HC_AZ(Go); break;
       default: g_err = "unsupported"; return -2;
     }
 #undef HC_AZ
     if (rc) return rc;
   }
   return 0;
+}
+
+// The product's host-drawn Dirichlet noise (os_host.cpp), for known answers.
+int64_t hc_dirichlet_noise(uint32_t seed, int32_t count, double alpha, double* out) {
+  return DirichletNoise(seed, count, alpha, out);
 }
 
 // Product RNG primitives (csrc/os_rng.h) on the host, for known-answer tests.

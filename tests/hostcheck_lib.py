@@ -127,13 +127,15 @@ AZ_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_
 
 
 def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=True,
-             uct_c=2.0, max_simulations=100, max_memory_mb=1000, solve=True):
+             uct_c=2.0, max_simulations=100, max_memory_mb=1000, solve=True,
+             dirichlet_alpha=0.0, dirichlet_epsilon=0.0):
   """csrc/os_az.h stepped on the host; eval_fn(obs float32[obs_size], legal
   bool[A], kind) -> (prior [A], value)."""
   L = lib()
   vp = ctypes.c_void_p
   L.hc_az_batch.argtypes = [ctypes.c_char_p, ctypes.c_int64, vp, vp, ctypes.c_double,
                             ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                            ctypes.c_double, ctypes.c_double,
                             vp, AZ_CB, ctypes.c_int32] + [vp] * 10
   R = len(offs) - 1
   mc = max_children
@@ -159,7 +161,8 @@ def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=Tru
   offs = np.ascontiguousarray(offs, np.int64)
   bs = np.ascontiguousarray(bot_seeds, np.uint32)
   rc = L.hc_az_batch(game_string.encode(), R, acts.ctypes.data, offs.ctypes.data, uct_c,
-                     max_simulations, max_memory_mb, int(solve), int(puct), bs.ctypes.data,
+                     max_simulations, max_memory_mb, int(solve), int(puct),
+                     float(dirichlet_alpha), float(dirichlet_epsilon), bs.ctypes.data,
                      fn, mc, *[o[k].ctypes.data for k in KEYS])
   if rc:
     raise RuntimeError(L.hc_last_error().decode())

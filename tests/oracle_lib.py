@@ -72,7 +72,8 @@ def lib():
         _u32p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
     L.oref_mcts_external.argtypes = [
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double, ctypes.c_int32,
-        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _u32p, EVAL_CB, ctypes.c_int32,
+        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+        _u32p, EVAL_CB, ctypes.c_int32,
         _i32p, _i32p, _f64p, _i8p, _i32p, _i32p, _f64p, _i8p, _i64p, _i32p]
     L.oref_selfplay.argtypes = [
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
@@ -180,7 +181,7 @@ class Game:
 
   def mcts_external(self, root_actions, root_offsets, bot_seeds, eval_fn, puct=True,
                     uct_c=2.0, max_simulations=100, max_memory_mb=1000, solve=True,
-                    max_children=None):
+                    max_children=None, dirichlet_alpha=0.0, dirichlet_epsilon=0.0):
     """MCTSBot with an external evaluator: eval_fn(history, kind) -> (prior
     [A] action-indexed, value for player 0); kind 1 = Prior, 2 = Evaluate."""
     R = len(root_offsets) - 1
@@ -207,7 +208,7 @@ class Game:
     lib().oref_mcts_external(
         self._h, R, np.ascontiguousarray(root_actions, dtype=np.int64),
         np.ascontiguousarray(root_offsets, dtype=np.int64), uct_c, max_simulations,
-        max_memory_mb, int(solve), int(puct),
+        max_memory_mb, int(solve), int(puct), float(dirichlet_alpha), float(dirichlet_epsilon),
         np.ascontiguousarray(bot_seeds, dtype=np.uint32), fn, mc, out["child_action"],
         out["child_n"], out["child_w"], out["child_out"], out["nchild"], out["root_n"],
         out["root_w"], out["root_out"], out["best_action"], out["nodes"])

@@ -6,7 +6,10 @@ representable arithmetic stands in for VPNetEvaluator.  The oracle MCTSBot
 Evaluate call f on the state's observation) is compared bit-exact with:
   * the product state machine stepped on the host (tests/hostcheck, CPU), and
   * the GPU kernel stepped by os_amd.az.ExternalEvaluatorSearch (gpu).
-Both UCT and PUCT child selection are covered.
+Both UCT and PUCT child selection are covered, on all five games (go's
+positional-superko set travels in the continuation), and Dirichlet root noise
+(mcts.cc:177-192, :265-273) with alpha below and above 1 (the two branches of
+libstdc++'s gamma sampler).
 """
 import numpy as np
 import pytest
@@ -21,7 +24,11 @@ CASES = {
     "connect_four": ([[], [3], [3, 3, 2]], 60),
     "breakthrough(rows=6,columns=6)": ([[], [86]], 40),
     "hex(board_size=5)": ([[], [12]], 48),
+    "go(board_size=5)": ([[], [12], [6, 12, 7]], 48),
 }
+# (alpha, epsilon): the AlphaZero defaults (alpha_zero.py: 1 / 0.25) and a
+# sub-1 alpha (pow(u, 1 / alpha) branch of gamma_distribution).
+NOISE = [(1.0, 0.25), (0.3, 0.25)]
 
 
 def toy_eval(obs, legal, kind=0):
@@ -73,6 +80,31 @@ def test_host_state_machine_matches_oracle(game, puct):
     np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
 
+@pytest.mark.parametrize("noise", NOISE)
+@pytest.mark.parametrize("game", sorted(CASES))
+def test_host_state_machine_dirichlet_matches_oracle(game, noise):
+  acts, offs, seeds, sims = _roots(game)
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  alpha, eps = noise
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), puct=True, uct_c=1.5,
+                         max_simulations=sims, max_children=A, dirichlet_alpha=alpha,
+                         dirichlet_epsilon=eps)
+  got = hc.az_batch(game, acts, offs, seeds, A, toy_eval, puct=True, uct_c=1.5,
+                    max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps)
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_dirichlet_noise_changes_the_search():
+  game = "connect_four"
+  acts, offs, seeds, sims = _roots(game)
+  a = hc.az_batch(game, acts, offs, seeds, 7, toy_eval, max_simulations=sims)
+  b = hc.az_batch(game, acts, offs, seeds, 7, toy_eval, max_simulations=sims,
+                  dirichlet_alpha=0.3, dirichlet_epsilon=0.25)
+  assert not all(np.array_equal(a[k], b[k]) for k in ("child_action", "child_n"))
+
+
 def test_puct_changes_the_search():
   game = "connect_four"
   acts, offs, seeds, sims = _roots(game)
@@ -82,17 +114,8 @@ def test_puct_changes_the_search():
   assert not np.array_equal(a["child_n"], b["child_n"])
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("puct", [True, False])
-@pytest.mark.parametrize("game", sorted(CASES))
-def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct):
+def _gpu_toy_evaluator(A):
   import torch
-  from os_amd.az import ExternalEvaluatorSearch
-  acts, offs, seeds, sims = _roots(game)
-  og = oracle_lib.Game(game)
-  A = og.num_distinct_actions
-  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), puct=puct, uct_c=1.5,
-                         max_simulations=sims, max_children=A)
 
   def evaluator(obs, legal, kind):
     ob = obs.cpu().numpy().reshape(obs.shape[0], -1)
@@ -104,10 +127,20 @@ def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct):
       if kd[i]:
         pr[i], v[i] = toy_eval(ob[i], lg[i], int(kd[i]))
     return torch.from_numpy(pr).to(obs.device), torch.from_numpy(v).to(obs.device)
+  return evaluator
 
+
+def _check_gpu(game, puct, alpha=0.0, eps=0.0):
+  from os_amd.az import ExternalEvaluatorSearch
+  acts, offs, seeds, sims = _roots(game)
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), puct=puct, uct_c=1.5,
+                         max_simulations=sims, max_children=A, dirichlet_alpha=alpha,
+                         dirichlet_epsilon=eps)
   search = ExternalEvaluatorSearch(game)
-  got = search.run(acts, offs, seeds, evaluator, puct=puct, uct_c=1.5,
-                   max_simulations=sims)
+  got = search.run(acts, offs, seeds, _gpu_toy_evaluator(A), puct=puct, uct_c=1.5,
+                   max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps)
   mc = search.eng.max_children
   for k in E.OUTPUT_KEYS:
     r = ref[k][:, :mc] if ref[k].ndim == 2 else ref[k]
@@ -116,9 +149,24 @@ def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct):
 
 
 @pytest.mark.gpu
-def test_gpu_external_evaluator_rejects_go(require_gpu):
+@pytest.mark.parametrize("puct", [True, False])
+@pytest.mark.parametrize("game", sorted(CASES))
+def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct):
+  _check_gpu(game, puct)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("noise", NOISE)
+@pytest.mark.parametrize("game", sorted(CASES))
+def test_gpu_external_evaluator_dirichlet_matches_oracle(require_gpu, game, noise):
+  _check_gpu(game, True, *noise)
+
+
+@pytest.mark.gpu
+def test_gpu_dirichlet_with_gc_budget_is_refused(require_gpu):
   from os_amd.az import ExternalEvaluatorSearch
-  search = ExternalEvaluatorSearch("go(board_size=5)")
+  search = ExternalEvaluatorSearch("tic_tac_toe")
   acts, offs = E.roots_from_histories([[]])
   with pytest.raises(ValueError):
-    search.run(acts, offs, [1], lambda *a: None, max_simulations=4)
+    search.run(acts, offs, [1], lambda *a: None, max_simulations=100000, max_memory_mb=1,
+               dirichlet_alpha=0.3, dirichlet_epsilon=0.25)
