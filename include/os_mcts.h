@@ -274,6 +274,24 @@ int os_rollouts_stats(os_engine* e, int64_t* out);
 int os_engine_root_sums_async(os_engine* e, int32_t num_actions, int64_t* dev_visits,
                               double* dev_rewards, void* hip_stream);
 
+/* Root-parallel MCTS over several devices of ONE process (SURVEY.md §8b B3
+ * os_root_parallel, §8e C4; the reference's counterpart is one MCTSBot::
+ * MCTSearch per tree, mcts.cc:325-428, e.g. driven by mcts_example.cc):
+ * engines[g] (g < ndev; one per device, or several on one device) each grow
+ * trees_per_device trees on the same root, the history root_actions[0 ..
+ * n_actions); tree t of engine g uses bot seed seed_base + g * T + t and
+ * evaluator seed that + 2^20 (T = trees_per_device).  Every engine's search
+ * is launched before any wait; each device sums its trees' root children by
+ * action (os_engine_root_sums_async), the per-device sums cross to engines[0]'s
+ * device peer-to-peer (xGMI) and are added there in engine order, so the
+ * result is deterministic.  Writes out_visits[num_actions] (int64, summed
+ * explore_count) and out_rewards[num_actions] (f64, summed total_reward) on
+ * the host and, if out_sims != NULL, the simulations run.  Synchronous. */
+int os_root_parallel(os_engine* const* engines, int32_t ndev, const os_mcts_params* p,
+                     const int64_t* root_actions, int64_t n_actions,
+                     int64_t trees_per_device, uint32_t seed_base, int32_t num_actions,
+                     int64_t* out_visits, double* out_rewards, int64_t* out_sims);
+
 /* ---- Device-resident pipeline (inputs already in HBM; for benchmarks) ---
  * prepare: upload roots + seeds and size the arena; run: launch the search
  * kernel on `hip_stream` (a hipStream_t, or NULL for the null stream) with no

@@ -73,6 +73,21 @@ __global__ __launch_bounds__(256) void k_root_reduce(const int32_t* dn, const do
   }
 }
 
+// Per-device root sums [ndev][A] (visits, then rewards) added in device order.
+__global__ void k_sum_devices(const int64_t* n, const double* w, int32_t ndev, int64_t A,
+                              int64_t* visits, double* rewards) {
+  const int64_t a = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (a >= A) return;
+  int64_t sn = 0;
+  double sw = 0.0;
+  for (int g = 0; g < ndev; ++g) {
+    sn += n[g * A + a];
+    sw += w[g * A + a];
+  }
+  visits[a] = sn;
+  rewards[a] = sw;
+}
+
 // Outcome counts of a rollout batch: [0] player 0 ahead, [1] player 1 ahead,
 // [2] draws (sign of the mean player-0 return of each evaluator).
 __global__ __launch_bounds__(256) void k_outcome_counts(const double* out, int64_t n,
@@ -1134,6 +1149,84 @@ int os_engine_root_sums_async(os_engine* e, int32_t num_actions, int64_t* dev_vi
                      static_cast<const double*>(e->d_dense_w.p), R, A, dev_visits,
                      dev_rewards);
   HIP_TRY(hipGetLastError());
+  return OS_OK;
+}
+
+int os_root_parallel(os_engine* const* engines, int32_t ndev, const os_mcts_params* p,
+                     const int64_t* root_actions, int64_t n_actions,
+                     int64_t trees_per_device, uint32_t seed_base, int32_t num_actions,
+                     int64_t* out_visits, double* out_rewards, int64_t* out_sims) {
+  if (!engines || ndev < 1 || !p || !out_visits || !out_rewards || trees_per_device < 1 ||
+      (n_actions > 0 && !root_actions))
+    return Fail(OS_ERR_INVALID, "bad argument");
+  for (int g = 0; g < ndev; ++g) {
+    if (!engines[g]) return Fail(OS_ERR_INVALID, "null engine");
+    for (int h = 0; h < g; ++h)
+      if (engines[h] == engines[g]) return Fail(OS_ERR_INVALID, "an engine is listed twice");
+    if (engines[g]->game.cfg.kind != engines[0]->game.cfg.kind ||
+        engines[g]->game.cfg.num_actions != engines[0]->game.cfg.num_actions)
+      return Fail(OS_ERR_INVALID, "engines of different games");
+  }
+  if (num_actions < engines[0]->game.cfg.num_actions)
+    return Fail(OS_ERR_INVALID, "num_actions smaller than NumDistinctActions");
+  const int64_t T = trees_per_device;
+  const int64_t A = num_actions;
+  std::vector<int64_t> acts(static_cast<size_t>(T * n_actions));
+  std::vector<int64_t> offs(static_cast<size_t>(T + 1));
+  for (int64_t t = 0; t < T; ++t) {
+    offs[t] = t * n_actions;
+    for (int64_t i = 0; i < n_actions; ++i) acts[t * n_actions + i] = root_actions[i];
+  }
+  offs[T] = T * n_actions;
+  std::vector<uint32_t> bs(T), es(T);
+  int rc;
+  // Launch every engine's trees and its on-device root sums before any wait.
+  for (int g = 0; g < ndev; ++g) {
+    os_engine* e = engines[g];
+    for (int64_t t = 0; t < T; ++t) {
+      bs[t] = seed_base + static_cast<uint32_t>(g * T + t);
+      es[t] = bs[t] + (1u << 20);
+    }
+    if ((rc = Prepare(e, p, T, acts.data(), offs.data(), bs.data(), es.data()))) return rc;
+    if ((rc = Run(e, nullptr))) return rc;
+    if ((rc = e->d_rp_sum.ensure(static_cast<size_t>(A) * 16))) return rc;
+    int64_t* dn = static_cast<int64_t*>(e->d_rp_sum.p);
+    if ((rc = os_engine_root_sums_async(e, num_actions, dn, reinterpret_cast<double*>(dn + A),
+                                        nullptr)))
+      return rc;
+  }
+  // Validate every search, then gather the per-device sums on engines[0].
+  os_engine* e0 = engines[0];
+  if ((rc = e0->d_rp_all.ensure(static_cast<size_t>(ndev) * A * 16))) return rc;
+  int64_t* all_n = static_cast<int64_t*>(e0->d_rp_all.p);
+  double* all_w = reinterpret_cast<double*>(all_n + ndev * A);
+  int64_t sims = 0;
+  for (int g = 0; g < ndev; ++g) {
+    os_engine* e = engines[g];
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<SearchResult> res(T);
+    HIP_TRY(hipMemcpy(res.data(), e->d_res.p, T * sizeof(SearchResult), hipMemcpyDeviceToHost));
+    for (int64_t t = 0; t < T; ++t) {
+      if (res[t].status != kOk)
+        return Fail(OS_ERR_CAPACITY, "engine " + std::to_string(g) + " tree " +
+                                         std::to_string(t) + ": search status " +
+                                         std::to_string(res[t].status));
+      sims += res[t].sims;
+    }
+    const int64_t* dn = static_cast<const int64_t*>(e->d_rp_sum.p);
+    HIP_TRY(hipMemcpyPeer(all_n + g * A, e0->device, dn, e->device, A * 8));
+    HIP_TRY(hipMemcpyPeer(all_w + g * A, e0->device, dn + A, e->device, A * 8));
+  }
+  HIP_TRY(hipSetDevice(e0->device));
+  int64_t* out_n = static_cast<int64_t*>(e0->d_rp_sum.p);  // reused as the result
+  double* out_w = reinterpret_cast<double*>(out_n + A);
+  hipLaunchKernelGGL(k_sum_devices, dim3(static_cast<unsigned>((A + 127) / 128)), dim3(128), 0,
+                     nullptr, all_n, all_w, ndev, A, out_n, out_w);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(out_visits, out_n, A * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out_rewards, out_w, A * 8, hipMemcpyDeviceToHost));
+  if (out_sims) *out_sims = sims;
   return OS_OK;
 }
 

@@ -241,7 +241,7 @@ struct os_engine {
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
-      d_sp_obs, d_glog, d_glink, d_roll_cnt;
+      d_sp_obs, d_glog, d_glink, d_roll_cnt, d_rp_sum, d_rp_all;
   std::vector<osm::SearchResult> last_results;
   int64_t last_sims = 0;
   ~os_engine() {
@@ -251,7 +251,7 @@ struct os_engine {
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
-                     &d_roll_cnt};
+                     &d_roll_cnt, &d_rp_sum, &d_rp_all};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

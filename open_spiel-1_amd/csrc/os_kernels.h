@@ -21,7 +21,7 @@ namespace osx {
 
 
 #if OS_PHASE_TIMING
-__device__ uint64_t g_phase_cycles[kNumPhases];  // diagnostic build only (per game TU)
+static __device__ uint64_t g_phase_cycles[kNumPhases];  // diagnostic build only; internal linkage: one per game TU
 #endif
 
 
@@ -801,7 +801,7 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
 }
 
 #if OS_PHASE_TIMING
-inline int PhaseCycles(uint64_t* out, bool clear) {
+static int PhaseCycles(uint64_t* out, bool clear) {  // static: per game TU
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(uint64_t) * kNumPhases));
   if (clear) {
@@ -812,7 +812,7 @@ inline int PhaseCycles(uint64_t* out, bool clear) {
   return OS_OK;
 }
 #else
-inline int PhaseCycles(uint64_t*, bool) {
+static int PhaseCycles(uint64_t*, bool) {
   return Fail(OS_ERR_UNSUPPORTED, "built without -DOS_PHASE_TIMING=1");
 }
 #endif

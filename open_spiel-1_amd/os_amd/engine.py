@@ -300,6 +300,24 @@ class Engine:
             num_roots * s["state_bytes"])
 
 
+def root_parallel(engines, root_actions, trees_per_device, seed_base=0, **params):
+  """Root-parallel search over the engines' devices in one process (C-ABI
+  os_root_parallel): returns (visits int64[A], rewards f64[A], sims), the
+  action-indexed sums of every tree's root children.  Tree t of engine g is
+  seeded seed_base + g * trees_per_device + t (evaluator: + 2^20)."""
+  p = make_params(**params)
+  A = engines[0].num_distinct_actions
+  hs = (ctypes.c_void_p * len(engines))(*[e._h for e in engines])
+  acts = _lib.i64(root_actions)
+  visits = np.zeros(A, np.int64)
+  rewards = np.zeros(A, np.float64)
+  sims = np.zeros(1, np.int64)
+  check(lib.os_root_parallel(ctypes.cast(hs, ctypes.c_void_p), len(engines), ctypes.byref(p),
+                             ptr(acts), len(acts), int(trees_per_device), int(seed_base), A,
+                             ptr(visits), ptr(rewards), ptr(sims)))
+  return visits, rewards, int(sims[0])
+
+
 def make_roots(game_string, num_roots, seed_base=1000, max_plies=8):
   """Benchmark roots: see os_make_roots in include/os_mcts.h."""
   g = ctypes.c_void_p()

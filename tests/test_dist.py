@@ -180,6 +180,31 @@ def test_gpu_root_parallel_lane_layout(require_gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_engines", [1, 3])
+def test_gpu_c_abi_root_parallel_matches_oracle(require_gpu, n_engines):
+  """os_root_parallel (one process, several engines; on a 1-GPU box they share
+  device 0, which exercises the same peer-copy + fixed-order device sum)."""
+  import torch as _t
+  from os_amd import engine as E
+  ndev = _t.cuda.device_count()
+  engines = [E.Engine(HEX5, device=g % ndev) for g in range(n_engines)]
+  T = 5
+  v, w, sims = E.root_parallel(engines, [12], T, seed_base=0, max_simulations=SIMS)
+  ov, ow = _oracle_root_parallel(HEX5, [12], n_engines * T, SIMS)
+  np.testing.assert_array_equal(v, ov.numpy())
+  np.testing.assert_array_equal(w, ow.numpy())
+  assert sims == n_engines * T * SIMS
+
+
+@pytest.mark.gpu
+def test_gpu_c_abi_root_parallel_rejects_duplicate_engine(require_gpu):
+  from os_amd import engine as E
+  e = E.Engine(HEX5, device=0)
+  with pytest.raises(RuntimeError):
+    E.root_parallel([e, e], [12], 2, max_simulations=SIMS)
+
+
+@pytest.mark.gpu
 def test_gpu_playout_counts(require_gpu):
   be = D.HipBackend("go(board_size=9)")
   seeds_total = 300
