@@ -53,7 +53,7 @@ int os_game_load(const char* game_string, os_game** out);
 void os_game_free(os_game* game);
 
 typedef struct {
-  int32_t kind;               /* 0 ttt, 1 connect_four, 2 breakthrough, 3 hex, 4 go */
+  int32_t kind;               /* 0 ttt, 1 connect_four, 2 breakthrough, 3 hex, 4 go, 5 pig */
   int32_t num_distinct_actions;  /* Game::NumDistinctActions (spiel.h:601-750) */
   int32_t max_game_length;    /* Game::MaxGameLength */
   int32_t num_players;        /* 2 */
@@ -76,6 +76,12 @@ int os_state_apply(os_state* s, int64_t action);            /* ApplyAction (spie
 int32_t os_state_current_player(const os_state* s);         /* CurrentPlayer (-4 terminal) */
 int32_t os_state_is_terminal(const os_state* s);            /* IsTerminal (spiel.h:283) */
 int os_state_returns(const os_state* s, double* out2);      /* Returns (spiel.h:309) */
+/* IsChanceNode (spiel.h:331; CurrentPlayer() is then -1, kChancePlayerId). */
+int32_t os_state_is_chance_node(const os_state* s);
+/* ChanceOutcomes (spiel.h:322-327): (action, probability) pairs in outcome
+ * order; returns the count (may exceed cap; 0 unless a chance node). */
+int32_t os_state_chance_outcomes(const os_state* s, int64_t* actions, double* probs,
+                                 int32_t cap);
 /* LegalActions (spiel.h:240), ascending; returns the count (may exceed cap). */
 int32_t os_state_legal_actions(const os_state* s, int64_t* out, int32_t cap);
 int32_t os_state_history(const os_state* s, int64_t* out, int32_t cap);
@@ -320,7 +326,8 @@ int32_t os_engine_state_bytes(os_engine* e);
 /* Deterministic benchmark roots: root i = initial state plus
  * k_i = g() % (max_plies + 1) uniformly random legal plies drawn from
  * std::mt19937 g(seed_base + i), stopping before any ply that would end the
- * game.  Writes histories (offsets has num_roots + 1 entries); returns the
+ * game; a root left at a chance node (pig) gets drawn outcomes until it is a
+ * decision node.  Writes histories (offsets has num_roots + 1 entries); returns the
  * total action count, or < 0 on error.  actions may be NULL to size. */
 int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base,
                       int32_t max_plies, int64_t* actions, int64_t* offsets);

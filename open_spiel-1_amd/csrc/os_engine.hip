@@ -197,8 +197,12 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
     return Fail(OS_ERR_INVALID, "unknown layout");
   if (e->game.cfg.max_children > kMaxChildren)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxChildren");
-  if (e->game.cfg.max_game_length >= kMaxPath)
+  // Games with chance nodes bound the tree depth instead (kChancePathCap;
+  // a deeper tree fails the search with kPathOverflow).
+  if (e->game.cfg.max_game_length >= kMaxPath && e->game.cfg.kind != kPig)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxPath");
+  if (e->game.cfg.kind == kPig && p->layout == OS_LAYOUT_WAVE)
+    return Fail(OS_ERR_UNSUPPORTED, "games with chance nodes run the lane layout only");
   return OS_OK;
 }
 
@@ -210,6 +214,7 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
   (void)R;
   if (layout != OS_LAYOUT_AUTO) return layout;
+  if (cfg.kind == kPig) return OS_LAYOUT_LANE;  // chance nodes: os_chance.h
   if (cfg.kind == kHex)
     return policy == OS_POLICY_CPP && cfg.rows >= 3 ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
   return OS_LAYOUT_WAVE;
@@ -269,6 +274,8 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
       return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
     if (StateTerminal(hs))
       return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
+    if (StateIsChance(hs))  // a bot is only asked to move at decision nodes
+      return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is a chance node");
     std::memcpy(roots.data() + r * sb, hs.raw, sb);
     if (go) {
       const int64_t nh = static_cast<int64_t>(hs.hashes.size());
@@ -680,7 +687,7 @@ int os_debug_phase_cycles(uint64_t* out, int32_t n) {
   if (!out || n < kNumPhases) return Fail(OS_ERR_INVALID, "need kNumPhases slots");
   // Each game's kernels live in their own code object: sum the counters.
   std::vector<uint64_t> acc(kNumPhases, 0), one(kNumPhases, 0);
-  for (int k = kTicTacToe; k <= kGo; ++k) {
+  for (int k = kTicTacToe; k <= kPig; ++k) {
     const int rc = LaunchersFor(k)->phase_cycles(one.data(), true);
     if (rc) return rc;
     for (int i = 0; i < kNumPhases; ++i) acc[i] += one[i];
@@ -774,6 +781,17 @@ int32_t os_state_is_terminal(const os_state* s) { return StateTerminal(s->s) ? 1
 int os_state_returns(const os_state* s, double* out2) {
   StateReturns(s->s, out2);
   return OS_OK;
+}
+int32_t os_state_is_chance_node(const os_state* s) { return StateIsChance(s->s) ? 1 : 0; }
+int32_t os_state_chance_outcomes(const os_state* s, int64_t* actions, double* probs,
+                                 int32_t cap) {
+  std::vector<std::pair<int64_t, double>> o;
+  StateChanceOutcomes(s->s, &o);
+  for (int32_t i = 0; i < static_cast<int32_t>(o.size()) && i < cap; ++i) {
+    actions[i] = o[i].first;
+    probs[i] = o[i].second;
+  }
+  return static_cast<int32_t>(o.size());
 }
 int64_t os_game_observation_shape(const os_game* game, int32_t* shape3) {
   if (!game) return Fail(OS_ERR_INVALID, "null game");
@@ -1249,6 +1267,23 @@ int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base
       HostState t = s;
       StateApply(&t, a);
       if (StateTerminal(t)) break;
+      s = t;
+    }
+    // A bot moves at decision nodes only: resolve a pending chance node with
+    // drawn outcomes (pig), never ending the game.
+    while (StateIsChance(s)) {
+      StateLegal(s, &legal);
+      HostState t = s;
+      StateApply(&t, legal[g() % legal.size()]);
+      if (StateTerminal(t)) {
+        s.history.pop_back();  // undo the roll that led here
+        HostState r;
+        r.game = s.game;
+        StateInit(&r);
+        for (int64_t a : s.history) StateApply(&r, a);
+        s = r;
+        break;
+      }
       s = t;
     }
     all.insert(all.end(), s.history.begin(), s.history.end());

@@ -276,6 +276,7 @@ extern GameLaunchers kConnectFourLaunchers;
 extern GameLaunchers kBreakthroughLaunchers;
 extern GameLaunchers kHexLaunchers;
 extern GameLaunchers kGoLaunchers;
+extern GameLaunchers kPigLaunchers;
 
 inline const GameLaunchers* LaunchersFor(int32_t kind) {
   switch (kind) {
@@ -284,6 +285,7 @@ inline const GameLaunchers* LaunchersFor(int32_t kind) {
     case kBreakthrough: return &kBreakthroughLaunchers;
     case kHex: return &kHexLaunchers;
     case kGo: return &kGoLaunchers;
+    case kPig: return &kPigLaunchers;
   }
   return nullptr;
 }

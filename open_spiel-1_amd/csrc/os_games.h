@@ -18,6 +18,12 @@
 //   breakthrough  open_spiel/games/breakthrough.cc:119-320
 //   hex           open_spiel/games/hex.cc:55-255
 //   go            open_spiel/games/go.cc:124-216, go/go_board.cc:217-597
+//   pig           open_spiel/games/pig.cc:81-244 (two players; chance nodes)
+// Games with chance nodes (G::kHasChance) also provide
+//   chance(const S&)                    IsChanceNode()
+//   chance_count(cfg), chance_prob(cfg) ChanceOutcomes(): actions kth(0..count)
+//                                       of legal(), each with chance_prob
+// and to_move() is -1 (kChancePlayerId) at a chance node.
 #ifndef OS_GAMES_H_
 #define OS_GAMES_H_
 
@@ -31,6 +37,7 @@ enum GameKind : int32_t {
   kBreakthrough = 2,
   kHex = 3,
   kGo = 4,
+  kPig = 5,
 };
 
 // Runtime game parameters plus precomputed masks.  POD: copied by value into
@@ -43,6 +50,7 @@ struct GameCfg {
   int32_t max_game_length;    // MaxGameLength()
   float komi;
   int32_t handicap;
+  int32_t pig_dice, pig_horizon, pig_win;         // pig diceoutcomes / horizon / winscore
   uint64_t board64, notcol0_64, notcollast_64;   // breakthrough (<= 64 cells)
   B128 board, notcol0, notcollast;               // hex / go (<= 128 cells)
   // Hex side-neighbour masks.  Equal to notcol0 / notcollast except on n = 2,
@@ -789,6 +797,104 @@ struct GoT {
 };
 using Go = GoT<B128>;
 using GoBig = GoT<B384>;  // board_size 12..19 (host State API)
+
+// ----------------------------------------------------------------------------
+// pig (pig.cc:81-244), two players.  A decision node offers roll (0) and stop
+// (1) -- only stop once the turn total would reach winscore (:225-229).  Roll
+// moves to a chance node whose outcomes are 1..diceoutcomes, each with
+// probability 1 / diceoutcomes (:233-244): outcome 1 loses the turn total and
+// passes the turn, outcome k > 1 adds k + 1 (:204-213, as written).  Stop
+// banks the turn total and passes.  total_moves counts decisions only;
+// terminal at total_moves >= horizon or a score >= winscore (:81-92); the
+// winner gets +1 and the other -1, nobody 0 (:94-111).
+struct Pig {
+  struct State {
+    int32_t score0, score1;
+    int32_t turn_total;
+    int32_t cur;          // player to move, -1 at a chance node
+    int32_t turn_player;
+    int32_t moves;        // total_moves_
+    static constexpr bool kNeedsLog = false;
+  };
+  using Ctx = NoCtx;
+  static constexpr bool kHasChance = true;
+  struct Legal {
+    uint32_t mask;
+    int count;
+    OS_HD int kth(int k) const { return select64(mask, k); }
+  };
+  OS_HD static void init(State& s, const GameCfg&) {
+    s.score0 = s.score1 = 0;
+    s.turn_total = 0;
+    s.cur = 0;
+    s.turn_player = 0;
+    s.moves = 0;
+  }
+  OS_HD static bool terminal(const State& s, const GameCfg& g) {
+    return s.moves >= g.pig_horizon || s.score0 >= g.pig_win || s.score1 >= g.pig_win;
+  }
+  OS_HD static int to_move(const State& s) { return s.cur; }
+  OS_HD static bool chance(const State& s) { return s.cur < 0; }
+  OS_HD static int chance_count(const GameCfg& g) { return g.pig_dice; }
+  OS_HD static double chance_prob(const GameCfg& g) { return 1.0 / g.pig_dice; }
+  OS_HD static Legal legal(const State& s, const GameCfg& g, Ctx&) {
+    Legal l;
+    if (s.cur < 0) {
+      l.mask = ((1u << g.pig_dice) - 1u) << 1;  // outcomes 1..dice
+      l.count = g.pig_dice;
+    } else {
+      const int mine = s.cur ? s.score1 : s.score0;
+      l.mask = mine + s.turn_total >= g.pig_win ? 2u : 3u;
+      l.count = popc64(l.mask);
+    }
+    return l;
+  }
+  OS_HD static void apply(State& s, const GameCfg&, Ctx&, int a) {
+    if (s.cur >= 0) {
+      s.moves++;
+      if (a == 0) {
+        s.cur = -1;
+        return;
+      }
+      if (s.turn_player) s.score1 += s.turn_total;
+      else s.score0 += s.turn_total;
+      s.turn_total = 0;
+      s.turn_player ^= 1;
+      s.cur = s.turn_player;
+    } else if (a == 1) {
+      s.turn_total = 0;
+      s.turn_player ^= 1;
+      s.cur = s.turn_player;
+    } else {
+      s.turn_total += a + 1;
+      s.cur = s.turn_player;
+    }
+  }
+  OS_HD static int ret0(const State& s, const GameCfg& g, Ctx&) {
+    if (s.score0 >= g.pig_win) return 1;
+    if (s.score1 >= g.pig_win) return -1;
+    return 0;
+  }
+  // ObservationTensor (pig.cc:119-168): [1 + 2][winscore + 1] one-hot bins of
+  // the turn total, then each player's score (the last bin holds >= winscore);
+  // as a [3][1][winscore + 1] CHW image (rows = 1, cols = winscore + 1).
+  static constexpr int kObsPlanes = 3;
+  OS_HD static float obs(const State& s, const GameCfg& g, int, int plane, int cell) {
+    const int v = plane == 0 ? s.turn_total : (plane == 1 ? s.score0 : s.score1);
+    const int bin = v < g.pig_win ? v : g.pig_win;
+    return cell == bin ? 1.0f : 0.0f;
+  }
+};
+
+// Chance-node traits (games without them never reach the chance branches).
+template <class G, class = void>
+struct HasChance {
+  static constexpr bool value = false;
+};
+template <class G>
+struct HasChance<G, decltype(void(G::kHasChance))> {
+  static constexpr bool value = G::kHasChance;
+};
 
 }  // namespace osm
 

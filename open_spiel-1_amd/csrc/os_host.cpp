@@ -143,6 +143,7 @@ auto WithGame(const GameCfg& g, F&& f) {
     case kConnectFour: return f(ConnectFour{});
     case kBreakthrough: return f(Breakthrough{});
     case kHex: return g.rows > kB128Side ? f(HexBig{}) : f(Hex{});
+    case kPig: return f(Pig{});
     default: return g.rows > kB128Side ? f(GoBig{}) : f(Go{});
   }
 }
@@ -289,10 +290,44 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
     }
     g->canonical = canon + ")";
     g->state_bytes = n > kB128Side ? sizeof(GoBig::State) : sizeof(Go::State);
+  } else if (name == "pig") {
+    std::string e = reject_unknown({"players", "horizon", "winscore", "diceoutcomes"});
+    if (!e.empty()) return e;
+    int players, horizon, win, dice;
+    if (!GetInt(kv, "players", 2, &players) || !GetInt(kv, "horizon", 1000, &horizon) ||
+        !GetInt(kv, "winscore", 100, &win) || !GetInt(kv, "diceoutcomes", 6, &dice))
+      return "bad pig parameter";
+    if (players < 2 || players > 10 || horizon < 1 || win < 1 || dice < 1)
+      return "bad pig parameter";
+    if (players != 2) {
+      *unsupported = true;
+      return "pig with more than two players is not supported by this engine";
+    }
+    if (dice > 30 || win > 4096) {
+      *unsupported = true;
+      return "pig diceoutcomes must be <= 30 and winscore <= 4096 for this engine";
+    }
+    c.kind = kPig;
+    c.rows = 1;                 // ObservationTensor [3][winscore + 1]
+    c.cols = win + 1;
+    c.num_actions = 6;          // pig.h:83 (NumDistinctActions is fixed)
+    c.max_children = dice > 2 ? dice : 2;
+    c.max_game_length = horizon;
+    c.pig_dice = dice;
+    c.pig_horizon = horizon;
+    c.pig_win = win;
+    std::string canon = "pig(";
+    bool first = true;
+    for (auto& it : kv) {  // sorted by key, as GameParametersToString
+      canon += (first ? "" : ",") + it.first + "=" + std::to_string(std::atoi(it.second.c_str()));
+      first = false;
+    }
+    g->canonical = canon + ")";
+    g->state_bytes = sizeof(Pig::State);
   } else {
     *unsupported = true;
     return "game '" + name + "' is not supported by this engine (supported: "
-           "tic_tac_toe, connect_four, breakthrough, hex, go)";
+           "tic_tac_toe, connect_four, breakthrough, hex, go, pig)";
   }
   g->cfg = c;
   g->name = name;
@@ -385,6 +420,29 @@ bool StateApply(HostState* s, int64_t a) {
   });
   s->history.push_back(a);
   return true;
+}
+
+bool StateIsChance(const HostState& s) {
+  if (StateTerminal(s)) return false;
+  return WithGame(s.game->cfg, [&](auto tag) {
+    using G = decltype(tag);
+    if constexpr (HasChance<G>::value) return G::chance(St<G>(s));
+    else return false;
+  });
+}
+
+void StateChanceOutcomes(const HostState& s, std::vector<std::pair<int64_t, double>>* out) {
+  out->clear();
+  if (!StateIsChance(s)) return;
+  WithGame(s.game->cfg, [&](auto tag) {
+    using G = decltype(tag);
+    if constexpr (HasChance<G>::value) {
+      NoCtx nc;
+      const typename G::Legal l = G::legal(St<G>(s), s.game->cfg, nc);
+      for (int k = 0; k < l.count; ++k)
+        out->emplace_back(l.kth(k), G::chance_prob(s.game->cfg));
+    }
+  });
 }
 
 void StateReturns(const HostState& s, double* r) {
@@ -543,6 +601,12 @@ std::string StateToString(const HostState& s) {
     case kGo:
       return g.rows > kB128Side ? GoString(St<GoBig>(s), g, s.history.size())
                                 : GoString(St<Go>(s), g, s.history.size());
+    case kPig: {  // pig.cc:246-251
+      const Pig::State& p = St<Pig>(s);
+      return "Scores: " + std::to_string(p.score0) + " " + std::to_string(p.score1) +
+             ", Turn total: " + std::to_string(p.turn_total) + "\nCurrent player: " +
+             std::to_string(p.turn_player) + (p.cur < 0 ? " (rolling)\n" : "\n");
+    }
   }
   return "";
 }
@@ -589,6 +653,9 @@ std::string StateActionToString(const HostState& s, int player, int64_t a) {
       if (col >= 'i') ++col;
       return out + std::string(1, col) + std::to_string(r + 1);
     }
+    case kPig:  // pig.cc:71-79
+      if (player < 0) return "chance outcome " + std::to_string(a);
+      return a == 0 ? "roll" : "stop";
   }
   return "";
 }

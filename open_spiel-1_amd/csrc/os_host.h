@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "os_games.h"
@@ -72,6 +73,10 @@ void StateLegal(const HostState& s, std::vector<int64_t>* out);
 // Returns false if the action is illegal.
 bool StateApply(HostState* s, int64_t a);
 void StateReturns(const HostState& s, double* r);
+// IsChanceNode (spiel.h:331) and ChanceOutcomes (spiel.h:322-327, outcome
+// order); empty unless the state is a chance node.
+bool StateIsChance(const HostState& s);
+void StateChanceOutcomes(const HostState& s, std::vector<std::pair<int64_t, double>>* out);
 // ObservationTensorShape: {C, H, W}; returns C * H * W.
 int ObservationShape(const HostGame& g, int32_t* shape3);
 // ObservationTensor(player) as float [C][H][W] (size ObservationShape).

@@ -14,9 +14,25 @@
 #ifndef OS_KERNELS_H_
 #define OS_KERNELS_H_
 
+#include "os_chance.h"
 #include "os_engine_impl.h"
 
 namespace osx {
+
+// The single-search engine of the lane layout: mcts_search, or its chance-node
+// form for games that have chance nodes (os_chance.h).
+template <class G, class R, int Policy, class Rng>
+__device__ SearchResult lane_search(const GameCfg& g, const SearchParams& sp,
+                                    const typename G::State& root, typename G::Ctx& ctx,
+                                    Node<R>* nodes, uint32_t cap, Rng& bot, Rng& ev,
+                                    PathEnt<R>* path, uint16_t* actbuf, int path_cap) {
+  if constexpr (HasChance<G>::value)
+    return mcts_search_chance<G, R, Policy>(g, sp, root, ctx, nodes, cap, bot, ev, path,
+                                            actbuf, path_cap);
+  else
+    return mcts_search<G, R, Policy>(g, sp, root, ctx, nodes, cap, bot, ev, path, actbuf,
+                                     path_cap);
+}
 
 
 
@@ -96,10 +112,10 @@ __global__ void k_mcts(DevArgs a) {
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   SearchResult res;
   if (Policy == kPolicyNumpy && a.shared_stream)
-    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
+    res = lane_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
                                     path, actbuf, a.path_cap);
   else
-    res = mcts_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
+    res = lane_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
                                     path, actbuf, a.path_cap);
   res.rng_words = bot.words + ((Policy == kPolicyNumpy && a.shared_stream) ? 0u : ev.words);
   a.results[gr] = res;
@@ -580,6 +596,12 @@ __global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   uint32_t moves = 0;
   for (int k = 0; k < a.n_rollouts; ++k) {
     ctx.reset();
+    if constexpr (HasChance<G>::value) {
+      const int r0 = rollout_ret0_chance<G, kPolicyCpp>(root, a.cfg, ctx, ev);
+      s0 += static_cast<double>(r0);
+      s1 += static_cast<double>(-r0);
+      continue;
+    }
     // rollout_ret0 (mcts.cc:46-55), counting the moves for the byte model.
     typename G::State s = root;
     while (!G::terminal(s, a.cfg)) {
@@ -632,7 +654,13 @@ int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
 
 template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
-  if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
+  if constexpr (HasChance<G>::value) {
+    if (e->params.layout == OS_LAYOUT_WAVE)
+      return Fail(OS_ERR_UNSUPPORTED, "games with chance nodes run the lane layout only");
+    if (a.path_cap > kChancePathCap) a.path_cap = kChancePathCap;
+  } else {
+    if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
+  }
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
   const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
   if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
@@ -719,6 +747,11 @@ size_t AzSlotBytes() { return sizeof(AzSlot<G>); }
 
 template <class G>
 int AzLaunch(os_engine* e, hipStream_t stream) {
+  if constexpr (HasChance<G>::value) {
+    (void)e;
+    (void)stream;
+    return Fail(OS_ERR_UNSUPPORTED, "external-evaluator search of games with chance nodes");
+  } else {
   AzArgs a;
   std::memset(&a, 0, sizeof a);
   const DevArgs d = MakeArgs(e);
@@ -769,6 +802,7 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
                      dim3(bs), 0, stream, a);
   HIP_TRY(hipGetLastError());
   return OS_OK;
+  }
 }
 
 template <class G>
@@ -789,9 +823,15 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
   a.n_root_hashes = e->roll_nhash;
   const int64_t n = e->roll_n;
-  if (e->rollout_layout == OS_LAYOUT_WAVE) {
-    hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream, a);
-  } else {
+  if constexpr (!HasChance<G>::value) {
+    if (e->rollout_layout == OS_LAYOUT_WAVE) {
+      hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream,
+                         a);
+      HIP_TRY(hipGetLastError());
+      return OS_OK;
+    }
+  }
+  {
     const int bs = 64;
     hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
                        dim3(bs), 0, stream, a);
@@ -819,8 +859,11 @@ static int PhaseCycles(uint64_t*, bool) {
 
 template <class G>
 int SelfPlayEntry(os_engine* e, hipStream_t stream) {
-  return e->params.n_rollouts != 1 ? SpLaunch<G, double>(e, stream)
-                                   : SpLaunch<G, int32_t>(e, stream);
+  if constexpr (HasChance<G>::value)
+    return Fail(OS_ERR_UNSUPPORTED, "self-play of games with chance nodes");
+  else
+    return e->params.n_rollouts != 1 ? SpLaunch<G, double>(e, stream)
+                                     : SpLaunch<G, int32_t>(e, stream);
 }
 
 }  // namespace osx

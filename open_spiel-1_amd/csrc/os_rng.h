@@ -186,6 +186,68 @@ OS_HD void CppShuffle(T* a, int n, G& g) {
   }
 }
 
+// absl::Uniform(g, 0.0, 1.0) (spiel.cc:339, SampleAction): abseil 20200225
+// uniform_real_distribution<double> over FastUniformBits<uint64> (two words,
+// first high, as AbslUniform) through GenerateRealFromBits<double,
+// GeneratePositiveTag, true>: the leading zeros set the exponent, the 52 bits
+// after the leading one the mantissa.  Pure integer work, so bit-exact on the
+// device.
+template <class G>
+OS_HD double AbslUniformDouble01(G& g) {
+  const uint64_t hi = g.next();
+  uint64_t bits = (hi << 32) | g.next();
+  if (bits == 0) return 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int clz = __clzll(static_cast<long long>(bits));
+#else
+  const int clz = __builtin_clzll(bits);
+#endif
+  bits <<= clz;
+  const uint64_t val = (static_cast<uint64_t>(1022 - clz) << 52) |
+                       ((bits >> 11) & ((1ull << 52) - 1));  // leading one -> bit 52
+  double d;
+  __builtin_memcpy(&d, &val, 8);
+  return d;
+}
+
+// numpy legacy RandomState.random_sample(): (a >> 5, b >> 6) -> 53 bits.
+template <class G>
+OS_HD double NpRandomSample(G& g) {
+  const uint32_t a = g.next() >> 5;
+  const uint32_t b = g.next() >> 6;
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+// spiel.cc:341-366 SampleAction(outcomes, z) over n equiprobable outcomes
+// (probability p each, accumulated in order): index of the first outcome with
+// sum <= z < sum + p.  The reference's fall-through is a fatal error (z is
+// never that close to 1); the last index stands in for it.
+OS_HD int SampleEquiprobable(int n, double p, double z) {
+  double sum = 0.0;
+  for (int k = 0; k < n; ++k) {
+    if (sum <= z && z < sum + p) return k;
+    sum += p;
+  }
+  return n - 1;
+}
+
+// numpy legacy RandomState.choice(n outcomes, p=[p] * n) index (replace=True,
+// size=None): cdf = p.cumsum(); cdf /= cdf[-1]; searchsorted(random_sample(),
+// side='right') == the number of cdf entries <= u.
+template <class G>
+OS_HD int NpChoiceEquiprobable(G& g, int n, double p) {
+  double acc = 0.0, last = 0.0;
+  for (int k = 0; k < n; ++k) last = acc = acc + p;
+  const double u = NpRandomSample(g);
+  int idx = 0;
+  acc = 0.0;
+  for (int k = 0; k < n; ++k) {
+    acc = acc + p;
+    idx += (acc / last <= u) ? 1 : 0;
+  }
+  return idx;
+}
+
 OS_HD uint32_t np_mask(uint32_t m) {
   m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
   return m;

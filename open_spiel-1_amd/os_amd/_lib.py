@@ -133,6 +133,8 @@ _sig("os_rollouts_fetch", ctypes.c_int, [_vp, _P])
 _sig("os_rollouts_outcomes_async", ctypes.c_int, [_vp, _vp, _vp])
 _sig("os_rollouts_stats", ctypes.c_int, [_vp, _vp])
 _sig("os_engine_root_sums_async", ctypes.c_int, [_vp, _i32, _vp, _vp, _vp])
+_sig("os_state_is_chance_node", _i32, [_vp])
+_sig("os_state_chance_outcomes", _i32, [_vp, _P, _P, _i32])
 _sig("os_root_parallel", ctypes.c_int,
      [_P, _i32, ctypes.POINTER(MctsParams), _P, _i64, _i64, _u32, _i32, _P, _P, _P])
 _sig("os_selfplay", ctypes.c_int,

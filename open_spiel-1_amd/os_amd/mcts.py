@@ -5,7 +5,8 @@ RandomRolloutEvaluator :46-82, SearchNode :85-196, MCTSBot :199-443).
 
 `MCTSBot.mcts_search` runs on the MI355X whenever the search is the hot path
 the engine implements — a `RandomRolloutEvaluator`, UCT child selection, no
-Dirichlet noise, one of the five supported games — continuing the bot's and
+Dirichlet noise, one of the supported games (the five, and pig with its chance
+nodes) — continuing the bot's and
 the evaluator's `np.random.RandomState` streams in place, bit-exact with the
 reference module (one shared RandomState, as in mcts_test.py:41-54, or two).
 Searches the engine does not implement (user evaluators, custom
@@ -130,17 +131,21 @@ class SearchNode(object):
 def tree_to_search_nodes(flat, state, game, root_action=None):
   """Materialises the engine's flat arena (os_engine_tree) as SearchNodes.
 
-  Node players follow from depth (the five games alternate turns); priors are
-  the uniform 1/|legal| of RandomRolloutEvaluator.prior; outcomes are
-  [v, -v] vectors as the reference stores Returns().
+  Node players follow from depth where turns alternate; in games with chance
+  nodes (pig) they are read off the replayed states (a chance node's children
+  have player PlayerId.CHANCE and the outcome probabilities as priors).
+  Other priors are the uniform 1/|legal| of RandomRolloutEvaluator.prior;
+  outcomes are [v, -v] vectors as the reference stores Returns().
   """
   first, n, w = flat["first"], flat["n"], flat["w"]
   action, nchild, out0 = flat["action"], flat["nchild"], flat["out0"]
   p0 = state.current_player()
+  chance = (game.get_type().chance_mode !=
+            pyspiel.GameType.ChanceMode.DETERMINISTIC)
   root = SearchNode(root_action, p0, 1)
-  stack = [(0, root, 0)]
+  stack = [(0, root, 0, state if chance else None)]
   while stack:
-    idx, node, depth = stack.pop()
+    idx, node, depth, st = stack.pop()
     node.explore_count = int(n[idx])
     node.total_reward = float(w[idx])
     if out0[idx] != 2:
@@ -148,13 +153,18 @@ def tree_to_search_nodes(flat, state, game, root_action=None):
       node.outcome = [v, -v]
     nc = int(nchild[idx])
     if nc:
-      child_player = p0 ^ (depth & 1)
-      prior = 1.0 / nc
       base = int(first[idx])
-      node.children = [SearchNode(int(action[base + k]), child_player, prior)
-                       for k in range(nc)]
+      acts = [int(action[base + k]) for k in range(nc)]
+      if chance:
+        child_player = st.current_player()
+        probs = dict(st.chance_outcomes()) if st.is_chance_node() else {}
+        node.children = [SearchNode(a, child_player, probs.get(a, 1.0 / nc))
+                         for a in acts]
+      else:
+        child_player = p0 ^ (depth & 1)
+        node.children = [SearchNode(a, child_player, 1.0 / nc) for a in acts]
       for k, c in enumerate(node.children):
-        stack.append((base + k, c, depth + 1))
+        stack.append((base + k, c, depth + 1, st.child(c.action) if chance else None))
   return root
 
 

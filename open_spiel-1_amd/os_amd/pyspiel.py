@@ -103,7 +103,14 @@ _TYPES = {
                         info_string=False),
     3: _two_player_type("hex", "Hex", {"board_size": 11}),
     4: _two_player_type("go", "Go", {"komi": 7.5, "board_size": 19, "handicap": 0}),
+    # pig.cc:42-62 (this engine: two players)
+    5: GameType("pig", "Pig", GameType.Dynamics.SEQUENTIAL,
+                GameType.ChanceMode.EXPLICIT_STOCHASTIC,
+                GameType.Information.PERFECT_INFORMATION, GameType.Utility.ZERO_SUM,
+                GameType.RewardModel.TERMINAL, 10, 2, False, False, True, True,
+                {"players": 2, "horizon": 1000, "winscore": 100, "diceoutcomes": 6}),
 }
+_PIG = 5
 
 
 def _game_string(name, params):
@@ -138,7 +145,8 @@ class Game:
     return [self._info.num_distinct_actions]
 
   def max_chance_outcomes(self):
-    return 0
+    # pig.h:88: diceoutcomes (the largest chance branching); 0 for the others
+    return self._info.max_children if self._info.kind == _PIG else 0
 
   def num_players(self):
     return 2
@@ -158,6 +166,8 @@ class Game:
   def observation_tensor_shape(self):
     shape = np.zeros(3, np.int32)
     lib.os_game_observation_shape(self._h, shape.ctypes.data)
+    if self._info.kind == _PIG:  # pig.cc:119-122: [1 + players, winscore + 1]
+      return [int(shape[0]), int(shape[2])]
     return [int(x) for x in shape]
 
   def observation_tensor_size(self):
@@ -186,7 +196,15 @@ class Game:
     if k == 4:
       return {"board_size": self._info.rows, "handicap": self._info.handicap,
               "komi": self._info.komi}
+    if k == _PIG:
+      return {"diceoutcomes": self._pig_dice(), "horizon": self._info.max_game_length,
+              "players": 2, "winscore": self._info.cols - 1}
     return {}
+
+  def _pig_dice(self):
+    st = self.new_initial_state()
+    st.apply_action(0)
+    return len(st.chance_outcomes())
 
   def deserialize_state(self, s):
     """Inverse of State.serialize() (history form, spiel.cc:375-420)."""
@@ -254,13 +272,13 @@ class State:
     return bool(lib.os_state_is_terminal(self._h))
 
   def is_chance_node(self):
-    return False
+    return bool(lib.os_state_is_chance_node(self._h))
 
   def is_simultaneous_node(self):
     return False
 
   def is_player_node(self):
-    return not self.is_terminal()
+    return self.current_player() >= 0
 
   def apply_action(self, action):
     check(lib.os_state_apply(self._h, int(action)))
@@ -342,7 +360,13 @@ class State:
     return [float(x) for x in out]
 
   def chance_outcomes(self):
-    return []
+    """ChanceOutcomes() (spiel.h:322-327): [(action, probability)] in outcome
+    order; [] at a decision node."""
+    cap = self._game._info.num_distinct_actions
+    acts = np.zeros(cap, np.int64)
+    probs = np.zeros(cap, np.float64)
+    n = lib.os_state_chance_outcomes(self._h, acts.ctypes.data, probs.ctypes.data, cap)
+    return [(int(acts[i]), float(probs[i])) for i in range(n)]
 
   def num_distinct_actions(self):
     return self._game.num_distinct_actions()

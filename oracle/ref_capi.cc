@@ -123,8 +123,23 @@ int64_t oref_state_json(void* g, const int64_t* actions, int64_t n, char* buf,
   j += ",\"current_player\":" + std::to_string(s->CurrentPlayer());
   auto r = s->Returns();
   char tmp[64];
-  std::snprintf(tmp, sizeof tmp, ",\"returns\":[%.17g,%.17g]", r[0], r[1]);
-  j += tmp;
+  j += ",\"returns\":[";
+  for (size_t i = 0; i < r.size(); ++i) {
+    std::snprintf(tmp, sizeof tmp, "%s%.17g", i ? "," : "", r[i]);
+    j += tmp;
+  }
+  j += "],\"is_chance_node\":";
+  j += s->IsChanceNode() ? "true" : "false";
+  if (s->IsChanceNode()) {
+    j += ",\"chance_outcomes\":[";
+    auto co = s->ChanceOutcomes();
+    for (size_t i = 0; i < co.size(); ++i) {
+      std::snprintf(tmp, sizeof tmp, "%s[%lld,%.17g]", i ? "," : "",
+                    static_cast<long long>(co[i].first), co[i].second);
+      j += tmp;
+    }
+    j += "]";
+  }
   j += ",\"legal_actions\":[";
   auto la = s->LegalActions();
   for (size_t i = 0; i < la.size(); ++i) {

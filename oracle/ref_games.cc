@@ -933,6 +933,114 @@ float GoScore(const RState& s) {
   return dynamic_cast<const go::State&>(s).Score();
 }
 
+
+// ---------------------------------------------------------------------------
+// pig (pig.cc:81-244): n players; a decision node offers roll (0) / stop (1)
+// (only stop once the turn would reach winscore); a roll goes to a chance
+// node with outcomes 1..diceoutcomes, each 1/diceoutcomes.  Outcome 1 loses
+// the turn total and passes the turn; outcome k > 1 adds k + 1 to the turn
+// total (pig.cc:211, as written).  Stop banks the turn total and passes.
+// Terminal at total_moves >= horizon or any score >= winscore; the winner gets
+// 1, the others -1 / (n - 1); nobody: all 0.
+namespace pig {
+class State : public RState {
+ public:
+  State(int players, int dice, int horizon, int win)
+      : n_(players), dice_(dice), horizon_(horizon), win_(win), scores_(players, 0) {}
+  Player CurrentPlayer() const override { return IsTerminal() ? kTerminalPlayerId : cur_; }
+  bool IsTerminal() const override {
+    if (moves_ >= horizon_) return true;
+    for (int p = 0; p < n_; ++p)
+      if (scores_[p] >= win_) return true;
+    return false;
+  }
+  std::vector<Action> LegalActions() const override {
+    if (IsTerminal()) return {};
+    if (cur_ == kChancePlayerId) {
+      std::vector<Action> v;
+      for (int i = 0; i < dice_; ++i) v.push_back(i + 1);
+      return v;
+    }
+    if (scores_[cur_] + turn_total_ >= win_) return {1};
+    return {0, 1};
+  }
+  std::vector<std::pair<Action, double>> ChanceOutcomes() const override {
+    std::vector<std::pair<Action, double>> o;
+    for (int i = 0; i < dice_; ++i) o.emplace_back(i + 1, 1.0 / dice_);
+    return o;
+  }
+  std::vector<double> Returns() const override {
+    if (!IsTerminal()) return std::vector<double>(n_, 0.0);
+    std::vector<double> r(n_, -1.0 / (n_ - 1));
+    for (int p = 0; p < n_; ++p)
+      if (scores_[p] >= win_) {
+        r[p] = 1.0;
+        return r;
+      }
+    return std::vector<double>(n_, 0.0);
+  }
+  std::unique_ptr<RState> Clone() const override { return std::make_unique<State>(*this); }
+  std::string ToString() const override {
+    std::string s = "Scores:";
+    for (int p = 0; p < n_; ++p) s += " " + std::to_string(scores_[p]);
+    s += ", Turn total: " + std::to_string(turn_total_) + "\nCurrent player: " +
+         std::to_string(turn_player_) + (cur_ == kChancePlayerId ? " (rolling)\n" : "\n");
+    return s;
+  }
+  std::string ActionToString(Player p, Action a) const override {
+    if (p == kChancePlayerId) return "chance outcome " + std::to_string(a);
+    return a == 0 ? "roll" : "stop";
+  }
+
+ protected:
+  void DoApplyAction(Action a) override {
+    if (cur_ >= 0 && a == 0) {
+      cur_ = kChancePlayerId;
+      ++moves_;
+    } else if (cur_ >= 0 && a == 1) {
+      scores_[turn_player_] += turn_total_;
+      turn_total_ = 0;
+      turn_player_ = (turn_player_ + 1) % n_;
+      cur_ = turn_player_;
+      ++moves_;
+    } else if (cur_ == kChancePlayerId) {
+      if (a == 1) {
+        turn_total_ = 0;
+        turn_player_ = (turn_player_ + 1) % n_;
+        cur_ = turn_player_;
+      } else {
+        turn_total_ += static_cast<int>(a) + 1;
+        cur_ = turn_player_;
+      }
+    }
+  }
+
+ private:
+  int n_, dice_, horizon_, win_;
+  int moves_ = 0;
+  Player cur_ = 0;
+  int turn_player_ = 0;
+  std::vector<int> scores_;
+  int turn_total_ = 0;
+};
+
+class Game : public RGame {
+ public:
+  Game(int players, int dice, int horizon, int win)
+      : n_(players), dice_(dice), horizon_(horizon), win_(win) {}
+  std::unique_ptr<RState> NewInitialState() const override {
+    return std::make_unique<State>(n_, dice_, horizon_, win_);
+  }
+  int NumDistinctActions() const override { return 6; }  // pig.h:83
+  int MaxGameLength() const override { return horizon_; }
+  std::string ShortName() const override { return "pig"; }
+  int NumPlayers() const override { return n_; }
+
+ private:
+  int n_, dice_, horizon_, win_;
+};
+}  // namespace pig
+
 std::unique_ptr<RGame> LoadGame(const std::string& gs, std::string* err) {
   std::string name;
   GameParams p;
@@ -966,6 +1074,15 @@ std::unique_ptr<RGame> LoadGame(const std::string& gs, std::string* err) {
     }
     return std::make_unique<go::Game>(n, static_cast<float>(p.GetDouble("komi", 7.5)),
                                       p.GetInt("handicap", 0));
+  }
+  if (name == "pig") {
+    const int players = p.GetInt("players", 2), dice = p.GetInt("diceoutcomes", 6);
+    const int horizon = p.GetInt("horizon", 1000), win = p.GetInt("winscore", 100);
+    if (players < 2 || players > 10 || dice < 1 || horizon < 1 || win < 1) {
+      *err = "bad pig parameters";
+      return nullptr;
+    }
+    return std::make_unique<pig::Game>(players, dice, horizon, win);
   }
   *err = "unknown game: " + name;
   return nullptr;

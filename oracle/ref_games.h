@@ -11,6 +11,7 @@
 //   breakthrough  open_spiel/games/breakthrough.cc:119-320
 //   hex           open_spiel/games/hex.cc:55-255
 //   go            open_spiel/games/go.cc:124-216, go/go_board.cc:217-597
+//   pig           open_spiel/games/pig.cc:81-244 (chance nodes)
 #ifndef OS_ORACLE_REF_GAMES_H_
 #define OS_ORACLE_REF_GAMES_H_
 
@@ -20,6 +21,7 @@
 #include <memory>
 #include <string>
 #include <unordered_set>
+#include <utility>
 #include <vector>
 
 namespace oref {
@@ -27,6 +29,7 @@ namespace oref {
 using Action = int64_t;
 using Player = int;
 constexpr Player kTerminalPlayerId = -4;   // spiel.h PlayerId::TERMINAL
+constexpr Player kChancePlayerId = -1;     // spiel.h PlayerId::CHANCE
 constexpr Player kInvalidPlayer = -3;
 constexpr Action kInvalidAction = -1;
 
@@ -52,6 +55,10 @@ class RState {
   virtual std::unique_ptr<RState> Clone() const = 0;
   virtual std::string ToString() const = 0;
   virtual std::string ActionToString(Player p, Action a) const = 0;
+  // spiel.h:331 IsChanceNode (CurrentPlayer() == kChancePlayerId) and
+  // ChanceOutcomes (:322-327); only pig has chance nodes.
+  bool IsChanceNode() const { return CurrentPlayer() == kChancePlayerId; }
+  virtual std::vector<std::pair<Action, double>> ChanceOutcomes() const { return {}; }
   // spiel.h:205-210: ApplyAction = DoApplyAction + history_.push_back.
   void ApplyAction(Action a) {
     DoApplyAction(a);
@@ -73,6 +80,7 @@ class RGame {
   virtual double MaxUtility() const { return 1.0; }
   virtual double MinUtility() const { return -1.0; }
   virtual std::string ShortName() const = 0;
+  virtual int NumPlayers() const { return 2; }
 };
 
 // Returns nullptr (and sets *err) for unknown games / unsupported params.

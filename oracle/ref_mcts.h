@@ -30,6 +30,17 @@ class Evaluator {
   virtual std::vector<std::pair<Action, double>> Prior(const RState& state) = 0;
 };
 
+// spiel.cc:337-372 SampleAction(outcomes, z): the first outcome whose
+// [sum, sum + prob) holds z.
+inline Action SampleAction(const std::vector<std::pair<Action, double>>& outcomes, double z) {
+  double sum = 0;
+  for (const auto& o : outcomes) {
+    if (sum <= z && z < sum + o.second) return o.first;
+    sum += o.second;
+  }
+  return outcomes.back().first;  // the reference raises SpielFatalError here
+}
+
 // mcts.h:92-106 / mcts.cc:42-71
 class RandomRolloutEvaluator : public Evaluator {
  public:
@@ -40,6 +51,10 @@ class RandomRolloutEvaluator : public Evaluator {
     for (int i = 0; i < n_rollouts_; ++i) {
       std::unique_ptr<RState> ws = state.Clone();
       while (!ws->IsTerminal()) {
+        if (ws->IsChanceNode()) {  // mcts.cc:47-49
+          ws->ApplyAction(SampleAction(ws->ChanceOutcomes(), AbslUniformDouble01(rng_)));
+          continue;
+        }
         std::vector<Action> actions = ws->LegalActions();
         ws->ApplyAction(actions[AbslUniformU64(rng_, actions.size())]);
       }
@@ -53,8 +68,9 @@ class RandomRolloutEvaluator : public Evaluator {
     for (double& v : result) v /= n_rollouts_;
     return result;
   }
-  // mcts.cc:73-86 (deterministic games only: no chance branch needed).
+  // mcts.cc:73-86
   std::vector<std::pair<Action, double>> Prior(const RState& state) override {
+    if (state.IsChanceNode()) return state.ChanceOutcomes();
     std::vector<Action> legal = state.LegalActions();
     std::vector<std::pair<Action, double>> prior;
     prior.reserve(legal.size());
@@ -173,9 +189,19 @@ class MCTSBot {
       }
       for (auto it = visit_path.rbegin(); it != visit_path.rend(); ++it) {
         SearchNode* node = *it;
-        node->total_reward += returns[node->player];
+        node->total_reward +=
+            returns[node->player == kChancePlayerId ? player_id : node->player];
         node->explore_count += 1;
-        if (solved && !node->children.empty()) {
+        if (solved && !node->children.empty() &&
+            node->children[0].player == kChancePlayerId) {  // mcts.cc:361-374
+          const std::vector<double>& outcome = node->children[0].outcome;
+          if (!outcome.empty() &&
+              std::all_of(node->children.begin() + 1, node->children.end(),
+                          [&outcome](const SearchNode& c) { return c.outcome == outcome; }))
+            node->outcome = outcome;
+          else
+            solved = false;
+        } else if (solved && !node->children.empty()) {
           Player player = node->children[0].player;
           const SearchNode* best = nullptr;
           bool all_solved = true;
@@ -237,13 +263,22 @@ class MCTSBot {
         nodes_ += static_cast<int>(cur->children.capacity());
       }
       SearchNode* chosen = nullptr;
-      double max_value = -std::numeric_limits<double>::infinity();
-      for (SearchNode& child : cur->children) {
-        double val = puct_ ? child.PUCTValue(cur->explore_count, uct_c_)
-                           : child.UCTValue(cur->explore_count, uct_c_);
-        if (val > max_value) {
-          max_value = val;
-          chosen = &child;
+      if (ws->IsChanceNode()) {  // mcts.cc:285-296: sample with the bot rng_
+        const Action a = SampleAction(ws->ChanceOutcomes(), AbslUniformDouble01(rng_));
+        for (SearchNode& child : cur->children)
+          if (child.action == a) {
+            chosen = &child;
+            break;
+          }
+      } else {
+        double max_value = -std::numeric_limits<double>::infinity();
+        for (SearchNode& child : cur->children) {
+          double val = puct_ ? child.PUCTValue(cur->explore_count, uct_c_)
+                             : child.UCTValue(cur->explore_count, uct_c_);
+          if (val > max_value) {
+            max_value = val;
+            chosen = &child;
+          }
         }
       }
       ws->ApplyAction(chosen->action);
@@ -301,9 +336,13 @@ class NumpyMCTSBot {
       SearchNode* cur = root.get();
       while (!ws->IsTerminal() && cur->explore_count > 0) {
         if (cur->children.empty()) {
-          std::vector<Action> legal = ws->LegalActions();
           std::vector<std::pair<Action, double>> la;
-          for (Action a : legal) la.emplace_back(a, 1.0 / legal.size());
+          if (ws->IsChanceNode()) {  // mcts.py:78-79 prior = chance_outcomes()
+            la = ws->ChanceOutcomes();
+          } else {
+            std::vector<Action> legal = ws->LegalActions();
+            for (Action a : legal) la.emplace_back(a, 1.0 / legal.size());
+          }
           for (size_t k = la.size() - 1; k >= 1; --k) {  // numpy shuffle
             size_t j = NpRandomInterval(*rng_, k);
             std::swap(la[k], la[j]);
@@ -313,12 +352,21 @@ class NumpyMCTSBot {
           nodes += static_cast<int>(la.size());
         }
         SearchNode* chosen = nullptr;
-        double max_value = -std::numeric_limits<double>::infinity();
-        for (SearchNode& child : cur->children) {
-          double val = child.UCTValue(cur->explore_count, uct_c_);
-          if (chosen == nullptr || val > max_value) {
-            max_value = val;
-            chosen = &child;
+        if (ws->IsChanceNode()) {  // mcts.py:326-333
+          const Action a = ChanceChoice(*ws);
+          for (SearchNode& child : cur->children)
+            if (child.action == a) {
+              chosen = &child;
+              break;
+            }
+        } else {
+          double max_value = -std::numeric_limits<double>::infinity();
+          for (SearchNode& child : cur->children) {
+            double val = child.UCTValue(cur->explore_count, uct_c_);
+            if (chosen == nullptr || val > max_value) {
+              max_value = val;
+              chosen = &child;
+            }
           }
         }
         ws->ApplyAction(chosen->action);
@@ -337,9 +385,17 @@ class NumpyMCTSBot {
       }
       for (auto it = path.rbegin(); it != path.rend(); ++it) {
         SearchNode* node = *it;
-        node->total_reward += returns[node->player];
+        node->total_reward +=
+            returns[node->player == kChancePlayerId ? root_player : node->player];
         node->explore_count += 1;
-        if (solved && !node->children.empty()) {
+        if (solved && !node->children.empty() &&
+            node->children[0].player == kChancePlayerId) {  // mcts.py:415-424
+          const std::vector<double>& outcome = node->children[0].outcome;
+          bool same = !outcome.empty();
+          for (const SearchNode& c : node->children) same = same && c.outcome == outcome;
+          if (same) node->outcome = outcome;
+          else solved = false;
+        } else if (solved && !node->children.empty()) {
           Player player = node->children[0].player;
           const SearchNode* best = nullptr;
           bool all_solved = true;
@@ -372,6 +428,10 @@ class NumpyMCTSBot {
     for (int r = 0; r < n_rollouts_; ++r) {
       std::unique_ptr<RState> ws = state.Clone();
       while (!ws->IsTerminal()) {
+        if (ws->IsChanceNode()) {  // mcts.py:64-67
+          ws->ApplyAction(ChanceChoice(*ws));
+          continue;
+        }
         std::vector<Action> legal = ws->LegalActions();
         ws->ApplyAction(legal[NpChoiceIndex(*rng_, legal.size())]);
       }
@@ -381,6 +441,14 @@ class NumpyMCTSBot {
     }
     for (double& v : result) v /= n_rollouts_;
     return result;
+  }
+
+  // random_state.choice(action_list, p=prob_list) over chance_outcomes().
+  Action ChanceChoice(const RState& ws) {
+    const auto o = ws.ChanceOutcomes();
+    std::vector<double> p;
+    for (const auto& e : o) p.push_back(e.second);
+    return o[NpChoiceP(*rng_, p)].first;
   }
 
   double uct_c_;

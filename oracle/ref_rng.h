@@ -26,6 +26,7 @@
 
 #include <cstdint>
 #include <random>
+#include <vector>
 
 namespace oref {
 
@@ -78,6 +79,48 @@ inline uint64_t NpChoiceIndex(std::mt19937& g, uint64_t n) {
   uint64_t value;
   while ((value = (static_cast<uint64_t>(g()) & mask)) > rng) {}
   return value;
+}
+
+// absl::Uniform(g, 0.0, 1.0) (spiel.cc:339, SampleAction): abseil 20200225
+// uniform_real_distribution<double> = GenerateRealFromBits<double,
+// GeneratePositiveTag, /*IncludeZero=*/true>(FastUniformBits<uint64>(g)):
+// the leading-zero count of the 64 bits sets the exponent (2^-(clz+1)), the 52
+// bits after the leading one the mantissa (value in [0, 1)); then
+// a + sample * (b - a) = sample.  The
+// 64-bit word order is the one of AbslUniformU64 (parity unpinned, as there).
+inline double AbslUniformDouble01(std::mt19937& g) {
+  uint64_t bits = static_cast<uint64_t>(g());
+  bits = (bits << 32) + static_cast<uint64_t>(g());
+  if (bits == 0) return 0.0;
+  const int clz = __builtin_clzll(bits);
+  bits <<= clz;
+  const uint64_t exp = static_cast<uint64_t>(1022 - clz);
+  bits >>= 11;  // 63 - kExp: the leading one lands on the implicit bit 52
+  const uint64_t val = (exp << 52) | (bits & ((uint64_t{1} << 52) - 1));
+  double d;
+  __builtin_memcpy(&d, &val, 8);
+  return 0.0 + d * (1.0 - 0.0);
+}
+
+// numpy legacy RandomState.random_sample(): 53 bits from two words.
+inline double NpRandomSample(std::mt19937& g) {
+  const uint32_t a = static_cast<uint32_t>(g()) >> 5, b = static_cast<uint32_t>(g()) >> 6;
+  return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+// numpy legacy RandomState.choice(a, p=p) index (replace=True, size=None):
+// cdf = p.cumsum(); cdf /= cdf[-1]; cdf.searchsorted(random_sample(),
+// side='right').
+inline size_t NpChoiceP(std::mt19937& g, const std::vector<double>& p) {
+  std::vector<double> cdf(p.size());
+  double acc = 0.0;
+  for (size_t i = 0; i < p.size(); ++i) cdf[i] = acc = acc + p[i];
+  const double last = cdf.back();
+  for (double& c : cdf) c /= last;
+  const double u = NpRandomSample(g);
+  size_t k = 0;
+  while (k < cdf.size() && cdf[k] <= u) ++k;
+  return k;
 }
 
 }  // namespace oref

@@ -11,6 +11,7 @@
 
 #include "os_host.h"
 #include "os_az.h"
+#include "os_chance.h"
 #include "os_mcts.h"
 
 using namespace osm;
@@ -42,8 +43,13 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
     ctx.init_filters();
   }
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
-  SearchResult res = mcts_search<G, R, Policy>(game.cfg, sp, rs, ctx, nodes.data(), cap,
-                                               bot, ev, path, actbuf, kMaxPath);
+  SearchResult res;
+  if constexpr (HasChance<G>::value)
+    res = mcts_search_chance<G, R, Policy>(game.cfg, sp, rs, ctx, nodes.data(), cap, bot, ev,
+                                           path, actbuf, kChancePathCap);
+  else
+    res = mcts_search<G, R, Policy>(game.cfg, sp, rs, ctx, nodes.data(), cap, bot, ev, path,
+                                    actbuf, kMaxPath);
   if (res.status != kOk) {
     g_err = "search status " + std::to_string(res.status);
     return -4;
@@ -147,6 +153,7 @@ int hc_mcts_batch(const char* game_string, int64_t num_roots,
       HC_CASE(kBreakthrough, Breakthrough)
       HC_CASE(kHex, Hex)
       HC_CASE(kGo, Go)
+      HC_CASE(kPig, Pig)
 #undef HC_CASE
     }
     if (rc) return rc;
@@ -304,6 +311,20 @@ void hc_absl_uniform(uint32_t seed, uint32_t n, int64_t k, uint64_t* out) {
   MtStream g{s.data(), kMtN, 0, 0};
   for (int64_t i = 0; i < k; ++i) out[i] = AbslUniform(g, n);
 }
+// absl::Uniform(rng, 0.0, 1.0) draws (os_rng.h AbslUniformDouble01).
+void hc_absl_double(uint32_t seed, int64_t k, double* out) {
+  std::vector<uint32_t> s(kMtN);
+  mt_seed(s.data(), seed);
+  MtStream g{s.data(), kMtN, 0, 0};
+  for (int64_t i = 0; i < k; ++i) out[i] = AbslUniformDouble01(g);
+}
+// numpy RandomState(seed).choice(n, p=[p] * n) indices (NpChoiceEquiprobable).
+void hc_np_choice_p(uint32_t seed, int32_t n, int64_t k, int32_t* out) {
+  std::vector<uint32_t> s(kMtN);
+  mt_seed(s.data(), seed);
+  MtStream g{s.data(), kMtN, 0, 0};
+  for (int64_t i = 0; i < k; ++i) out[i] = NpChoiceEquiprobable(g, n, 1.0 / n);
+}
 void hc_cpp_shuffle(uint32_t seed, int32_t n, int32_t* out) {
   std::vector<uint32_t> s(kMtN);
   mt_seed(s.data(), seed);
@@ -371,6 +392,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
       case kConnectFour: { NoCtx c; r0 = rollout_ret0<ConnectFour, kPolicyCpp>(*reinterpret_cast<ConnectFour::State*>(hs.raw), game.cfg, c, ev); break; }
       case kBreakthrough: { NoCtx c; r0 = rollout_ret0<Breakthrough, kPolicyCpp>(*reinterpret_cast<Breakthrough::State*>(hs.raw), game.cfg, c, ev); break; }
       case kHex: { NoCtx c; r0 = rollout_ret0<Hex, kPolicyCpp>(*reinterpret_cast<Hex::State*>(hs.raw), game.cfg, c, ev); break; }
+      case kPig: { NoCtx c; r0 = rollout_ret0_chance<Pig, kPolicyCpp>(*reinterpret_cast<Pig::State*>(hs.raw), game.cfg, c, ev); break; }
       case kGo: {
         GoCtx c;
         std::memset(&c, 0, sizeof c);

@@ -97,6 +97,19 @@ def absl_uniform(seed, n, k):
   return out
 
 
+def absl_double(seed, k):
+  out = np.zeros(k, np.float64)
+  lib().hc_absl_double(ctypes.c_uint32(seed), ctypes.c_int64(k), out.ctypes.data_as(ctypes.c_void_p))
+  return out
+
+
+def np_choice_p(seed, n, k):
+  out = np.zeros(k, np.int32)
+  lib().hc_np_choice_p(ctypes.c_uint32(seed), ctypes.c_int32(n), ctypes.c_int64(k),
+                       out.ctypes.data_as(ctypes.c_void_p))
+  return out
+
+
 def cpp_shuffle(seed, n):
   out = np.zeros(n, np.int32)
   lib().hc_cpp_shuffle(seed, n, out.ctypes.data)

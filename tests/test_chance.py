@@ -1,0 +1,185 @@
+"""Chance nodes: pig (pig.cc) on the product, against
+the oracle, which the reference's own pig playthroughs pin (test_oracle.py)
+and the unmodified reference mcts.py pins on the numpy path
+(test_python_goldens.py, python_mcts_pig*.json).
+
+  * CPU: the product's host State API (two-player pig) equals the oracle's on
+    random games; the search engine compiled for the host (csrc/os_chance.h)
+    equals the oracle's MCTSBot / numpy bot; product rollouts equal the
+    oracle's RandomRolloutEvaluator.
+  * GPU: the same through the lane-layout kernel, the rollout kernel and the
+    Python MCTSBot drop-ins.
+"""
+import numpy as np
+import pytest
+
+import hostcheck_lib as H
+import oracle_lib as O
+from os_amd import engine as E
+from os_amd import pyspiel
+
+PIGS = ["pig", "pig(horizon=30,winscore=8)", "pig(diceoutcomes=4,winscore=25)"]
+
+
+def _random_games(gs, n, seed):
+  rs = np.random.RandomState(seed)
+  g = pyspiel.load_game(gs)
+  for _ in range(n):
+    st = g.new_initial_state()
+    hist = []
+    while not st.is_terminal() and len(hist) < 400:
+      yield hist, st
+      a = int(rs.choice(st.legal_actions()))
+      st.apply_action(a)
+      hist.append(a)
+    yield hist, st
+
+
+@pytest.mark.parametrize("gs", PIGS)
+def test_host_state_matches_oracle(gs):
+  og = O.Game(gs)
+  for hist, st in _random_games(gs, 6, 3):
+    ref = og.state_info(hist)
+    assert st.is_terminal() == ref["is_terminal"]
+    assert st.current_player() == ref["current_player"]
+    assert st.legal_actions() == ref["legal_actions"]
+    assert st.returns() == ref["returns"]
+    assert st.is_chance_node() == ref["is_chance_node"]
+    assert str(st) == ref["observation_string"]
+    assert [st.action_to_string(a) for a in st.legal_actions()] == \
+        ref["string_legal_actions"]
+    if st.is_chance_node():
+      assert [list(x) for x in st.chance_outcomes()] == ref["chance_outcomes"]
+    else:
+      assert st.chance_outcomes() == []
+
+
+def test_observation_tensor_bins():
+  g = pyspiel.load_game("pig(winscore=10)")
+  assert g.observation_tensor_shape() == [3, 11]
+  st = g.new_initial_state()
+  for a in (0, 6, 1, 0, 3, 1):  # p0 rolls 6 (+7), stops; p1 rolls 3 (+4), stops
+    st.apply_action(a)
+  t = np.array(st.observation_tensor()).reshape(3, 11)
+  assert t.sum(axis=1).tolist() == [1, 1, 1]
+  assert [int(np.argmax(r)) for r in t] == [0, 7, 4]
+
+
+def _roots(gs, R, plies=12, seed=1000):
+  return E.make_roots(gs, R, seed, plies)
+
+
+def test_make_roots_are_decision_nodes():
+  acts, offs = _roots("pig", 64)
+  g = pyspiel.load_game("pig")
+  for r in range(64):
+    st = g.new_initial_state()
+    for a in acts[offs[r]:offs[r + 1]]:
+      st.apply_action(int(a))
+    assert not st.is_chance_node() and not st.is_terminal()
+
+
+@pytest.mark.parametrize("gs", PIGS)
+@pytest.mark.parametrize("n_rollouts,solve", [(1, True), (2, True), (1, False)])
+def test_engine_cpp_policy_matches_oracle(gs, n_rollouts, solve):
+  R = 8
+  acts, offs = _roots(gs, R)
+  bs = np.arange(R, dtype=np.uint32) * 5 + 3
+  es = bs + np.uint32(1 << 20)
+  kw = dict(uct_c=2.0, max_simulations=300, n_rollouts=n_rollouts, solve=solve)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=6, **kw)
+  got = H.mcts_batch(gs, acts, offs, bs, es, 6, **kw)
+  bad = [k for k in H.KEYS if not np.array_equal(got[k], ref[k])]
+  assert not bad, bad
+
+
+@pytest.mark.parametrize("gs", PIGS)
+def test_engine_rollouts_match_oracle(gs):
+  seeds = np.arange(200, dtype=np.uint32)
+  for hist in ([], [0], [0, 3], [1, 0, 4]):
+    np.testing.assert_array_equal(H.rollouts(gs, hist, seeds),
+                                  O.Game(gs).rollouts(hist, seeds))
+
+
+def test_solver_proves_short_games():
+  # pig(horizon=2): two decisions end the game, every leaf is a draw, so each
+  # chance node's children share one outcome and the root is proven a draw.
+  gs = "pig(horizon=2)"
+  acts, offs = E.roots_from_histories([[], [0, 6]])
+  bs = np.array([1, 2], np.uint32)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, bs + 9, max_simulations=2000, max_children=6)
+  got = H.mcts_batch(gs, acts, offs, bs, bs + 9, 6, max_simulations=2000)
+  for k in H.KEYS:
+    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+  assert (ref["root_out"] == 0).all()  # proven through chance nodes
+
+
+def test_chance_node_api():
+  g = pyspiel.load_game("pig")
+  assert g.get_type().chance_mode == pyspiel.GameType.ChanceMode.EXPLICIT_STOCHASTIC
+  assert g.max_chance_outcomes() == 6
+  st = g.new_initial_state()
+  st.apply_action(0)
+  assert st.is_chance_node() and st.current_player() == pyspiel.PlayerId.CHANCE
+  assert not st.is_player_node()
+  assert st.action_to_string(pyspiel.PlayerId.CHANCE, 3) == "chance outcome 3"
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs", PIGS)
+@pytest.mark.parametrize("policy", ["cpp", "numpy"])
+def test_gpu_search_matches_oracle(require_gpu, gs, policy):
+  from os_amd import _lib
+  R = 64
+  acts, offs = _roots(gs, R)
+  bs = np.arange(R, dtype=np.uint32) * 5 + 3
+  es = bs + np.uint32(1 << 20)
+  eng = E.Engine(gs)
+  if policy == "cpp":
+    ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_simulations=300, max_children=6)
+    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300)
+  else:
+    ref = H.mcts_batch(gs, acts, offs, bs, es, 6, max_simulations=300,
+                       policy=_lib.POLICY_NUMPY)
+    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300,
+                         policy=_lib.POLICY_NUMPY)
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got[k], ref[k][:, :got[k].shape[1]] if ref[k].ndim == 2
+                                  else ref[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_rollouts_match_oracle(require_gpu):
+  eng = E.Engine("pig")
+  seeds = np.arange(4096, dtype=np.uint32)
+  got = eng.rollouts([0, 4], seeds)
+  np.testing.assert_array_equal(got, O.Game("pig").rollouts([0, 4], seeds))
+
+
+@pytest.mark.gpu
+def test_gpu_wave_layout_is_refused(require_gpu):
+  from os_amd import _lib
+  eng = E.Engine("pig")
+  acts, offs = _roots("pig", 4)
+  with pytest.raises(ValueError):
+    eng.mcts_batch(acts, offs, np.arange(4, dtype=np.uint32), np.arange(4, dtype=np.uint32),
+                   max_simulations=10, layout=_lib.LAYOUT_WAVE)
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_bot_plays_pig(require_gpu):
+  """pyspiel.MCTSBot steps at decision nodes; chance outcomes are sampled by
+  the driver (evaluate_bots.cc:32-37 style)."""
+  g = pyspiel.load_game("pig(winscore=20)")
+  ev = pyspiel.RandomRolloutEvaluator(1, 5)
+  bots = [pyspiel.MCTSBot(g, ev, 2.0, 200, 1000, True, s, False) for s in (1, 2)]
+  rs = np.random.RandomState(0)
+  st = g.new_initial_state()
+  while not st.is_terminal():
+    if st.is_chance_node():
+      acts, probs = zip(*st.chance_outcomes())
+      st.apply_action(int(rs.choice(acts, p=probs)))
+    else:
+      st.apply_action(bots[st.current_player()].step(st))
+  assert st.returns() in ([1.0, -1.0], [-1.0, 1.0])

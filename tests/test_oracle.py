@@ -13,9 +13,12 @@ import oracle_lib as O
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 PLAYTHROUGHS = [("tic_tac_toe", "tic_tac_toe"), ("connect_four", "connect_four"),
                 ("breakthrough", "breakthrough"), ("hex", "hex(board_size=5)"),
-                ("go", "go(board_size=7,komi=4.5)")]
+                ("go", "go(board_size=7,komi=4.5)"),
+                ("pig_3p", "pig(players=3,horizon=10,winscore=10)"),
+                ("pig_4p", "pig(players=4,horizon=10,winscore=10)"),
+                ("pig_5p", "pig(players=5,horizon=100,winscore=20)")]
 FIELDS = ("is_terminal", "current_player", "returns", "legal_actions",
-          "string_legal_actions", "observation_string")
+          "string_legal_actions", "observation_string", "is_chance_node")
 
 
 def probes():
@@ -33,7 +36,11 @@ def test_oracle_replays_playthroughs(short, gs):
   for st in d["states"]:
     info = g.state_info(st["history"])
     for k in FIELDS:
-      assert info[k] == st[k], (short, st["history"], k)
+      if k in st:  # chance states record no Returns()
+        assert info[k] == st[k], (short, st["history"], k)
+    if st.get("chance_outcomes"):  # printed with 12 significant digits
+      got = [[a, float("%.12g" % p)] for a, p in info["chance_outcomes"]]
+      assert got == st["chance_outcomes"], (short, st["history"])
 
 
 def test_mt_known_answers():

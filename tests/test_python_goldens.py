@@ -82,7 +82,7 @@ def _check_tree(root, c):
 
 def test_fixture_coverage():
   games = {p.values[0].split("(")[0] for p in CASES}
-  assert games == {"tic_tac_toe", "connect_four", "breakthrough", "hex", "go"}
+  assert games == {"tic_tac_toe", "connect_four", "breakthrough", "hex", "go", "pig"}
   assert any(not p.values[1]["shared"] for p in CASES)
   assert any(p.values[1]["n_rollouts"] > 1 for p in CASES)
 

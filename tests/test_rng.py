@@ -50,3 +50,38 @@ def test_numpy_state_roundtrip(k):
   st2 = rs.get_state()
   assert pos == st2[2]
   assert np.array_equal(key, st2[1])
+
+
+def _py_absl_double(words):
+  """abseil 20200225 GenerateRealFromBits<double, GeneratePositiveTag, true>
+  over FastUniformBits<uint64> (first word high), restated in Python."""
+  import struct
+  out = []
+  for i in range(0, len(words) - 1, 2):
+    bits = (int(words[i]) << 32) | int(words[i + 1])
+    if bits == 0:
+      out.append(0.0)
+      continue
+    clz = 64 - bits.bit_length()
+    bits = (bits << clz) & (2**64 - 1)
+    val = ((1022 - clz) << 52) | ((bits >> 11) & (2**52 - 1))
+    out.append(struct.unpack("<d", struct.pack("<Q", val))[0])
+  return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42])
+def test_absl_uniform_double_matches_restatement(seed):
+  got = H.absl_double(seed, 2000)
+  want = _py_absl_double(O.mt19937(seed, 4000))
+  assert got.tolist() == want
+  assert (got >= 0).all() and (got < 1).all()
+  hist = np.histogram(got, bins=10, range=(0, 1))[0]
+  assert hist.min() > 150  # uniform over [0, 1)
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 6, 7])
+def test_numpy_choice_with_p_matches_numpy(n):
+  for seed in (0, 5, 42):
+    rs = np.random.RandomState(seed)
+    want = [int(rs.choice(n, p=[1.0 / n] * n)) for _ in range(300)]
+    assert H.np_choice_p(seed, n, 300).tolist() == want

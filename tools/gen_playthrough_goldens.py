@@ -27,6 +27,10 @@ FILES = {
     "breakthrough": "breakthrough.txt",
     "hex(board_size=5)": "hex(board_size=5).txt",
     "go(board_size=7,komi=4.5)": "go.txt",
+    # chance nodes: n-player playthroughs pin the rules
+    "pig(players=3,horizon=10,winscore=10)": "pig_3p.txt",
+    "pig(players=4,horizon=10,winscore=10)": "pig_4p.txt",
+    "pig(players=5,horizon=100,winscore=20)": "pig_5p.txt",
 }
 
 
@@ -104,6 +108,12 @@ def parse(path):
       cur["legal_actions"] = _int_list(line.split(" = ", 1)[1])
     elif line.startswith("StringLegalActions() = "):
       cur["string_legal_actions"] = _str_list(line.split(" = ", 1)[1])
+    elif line.startswith("IsChanceNode() = "):
+      cur["is_chance_node"] = line.endswith("True")
+    elif line.startswith("ChanceOutcomes() = "):
+      body = line.split(" = ", 1)[1].strip()[1:-1]
+      cur["chance_outcomes"] = [[int(a), float(p)] for a, p in
+                                re.findall(r"\{(\d+), ([0-9.e-]+)\}", body)]
     elif line.startswith("ObservationString(0) = "):
       cur["observation_string"] = _unquote(line.split(" = ", 1)[1])
   for s in states:
@@ -125,6 +135,8 @@ def main():
   for game, fname in FILES.items():
     meta, states = parse(os.path.join(REF, fname))
     short = game.split("(")[0]
+    if short == "pig":
+      short = os.path.splitext(fname)[0]
     rec = {"game": game, "source": "open_spiel/integration_tests/playthroughs/"
            + fname, "meta": meta, "states": states}
     out = os.path.join(OUT, "playthrough_%s.json" % short)

@@ -18,6 +18,8 @@ How the reference runs here:
     run the search on the host (mcts.py:46-82, 199-443): every state operation
     goes through `os_amd.pyspiel.State` (the host C++ game code in
     libos_mcts.so; no GPU is used or needed).
+  * pig exercises the chance-node branches of mcts.py (:64-67, :78-79,
+    :326-333, :409-424) through the drop-in's chance_outcomes().
   * tic_tac_toe is also searched on the reference's pure-Python game, which
     does not touch this repo's game code at all; the generator asserts both
     give the same tree.
@@ -125,6 +127,10 @@ def main():
       "hex(board_size=11)": dict(positions=[[], ("random", 20, 4)], seeds=[0, 42], sims=400),
       "hex(board_size=5)": dict(positions=[[], ("random", 6, 5)], seeds=[0, 42], sims=1000),
       "go(board_size=9)": dict(positions=[[], ("random", 15, 6)], seeds=[0, 42], sims=200),
+      # chance nodes: the default pig and a short one whose
+      # trees reach terminal states (solver, chance-node proof rule)
+      "pig": dict(positions=[[], [0, 4, 0, 3], [1, 0, 5, 1]], seeds=[0, 42], sims=300),
+      "pig(horizon=30,winscore=8)": dict(positions=[[], [0, 5]], seeds=[0, 42], sims=1000),
   }
   for gs, p in plan.items():
     base = gs.split("(")[0] + ("" if "(" not in gs else "_" + gs.split("=")[-1].rstrip(")"))
