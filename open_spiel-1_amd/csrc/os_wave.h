@@ -478,6 +478,22 @@ __device__ __forceinline__ double uct_value(const Node<R>& c, int cp, double log
   return static_cast<double>(c.w) / dn + uct_c * __builtin_sqrt(logN / dn);
 }
 
+// The same value for lane-distributed children, computed on every lane and
+// selected (no exec-mask branches: the scalar unit is the wave kernels'
+// binding pipe, and a masked-off f64 division costs the VALU the same cycles).
+// Lanes outside the children score -inf.  A zero count divides to inf / NaN
+// only in lanes whose value is then discarded.
+template <class R>
+__device__ __forceinline__ double uct_value_sel(const Node<R>& c, bool in, int cp, double logN,
+                                                double uct_c) {
+  const double dn = static_cast<double>(c.n);
+  const double u = static_cast<double>(c.w) / dn + uct_c * __builtin_sqrt(logN / dn);
+  const double o = outcome_for(c.out, cp);
+  double v = c.n == 0 ? __builtin_huge_val() : u;
+  v = c.out != kUnsolved ? o : v;
+  return in ? v : -__builtin_huge_val();
+}
+
 // Inclusive prefix (OR / sum) over the 16 lanes of each DPP row; lanes that
 // would read across the row boundary read 0 (bound_ctrl), the identity.
 template <int Shift>
@@ -941,6 +957,27 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
   return G::ret0(s, g, ctx);
 }
 
+// A child node as ONE 16-byte load (Node<int32_t> is 16-byte aligned in the
+// arena): copying the struct field-wise costs three loads (dwordx3 + two
+// ushort) per lane and scan level.
+template <class R>
+__device__ __forceinline__ Node<R> load_node(const Node<R>* p) {
+  return *p;
+}
+template <>
+__device__ __forceinline__ Node<int32_t> load_node(const Node<int32_t>* p) {
+  static_assert(sizeof(Node<int32_t>) == 16, "16-byte node");
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  Node<int32_t> c;
+  c.first = v.x;
+  c.n = static_cast<int32_t>(v.y);
+  c.w = static_cast<int32_t>(v.z);
+  c.action = static_cast<uint16_t>(v.w & 0xFFFFu);
+  c.nchild = static_cast<uint8_t>((v.w >> 16) & 0xFFu);
+  c.out = static_cast<int8_t>(v.w >> 24);
+  return c;
+}
+
 // One search, executed by the whole wave.  `path` (LDS) has path_cap
 // entries.  Same contract as mcts_search.
 template <class G, class R, int Policy, class C>
@@ -1120,12 +1157,12 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             lg1 = rlg1;
           }
         } else {
-          if (in0) {
-            c0 = nodes[cur_first + l];
-            lg0 = sp.log_lut[c0.n];
-          }
+          // Every lane loads (lanes past the last child re-read child 0, so
+          // no exec-mask branch); their values are masked by in0 / in1.
+          c0 = load_node(nodes + cur_first + (in0 ? l : 0));
+          lg0 = sp.log_lut[c0.n];
           if (in1) {
-            c1 = nodes[cur_first + l + 64];
+            c1 = load_node(nodes + cur_first + l + 64);
             lg1 = sp.log_lut[c1.n];
           }
         }
@@ -1139,8 +1176,8 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         if (f0 | f1) {
           chosen = f0 ? ctz64(f0) : 64 + ctz64(f1);
         } else {
-          const double v0 = in0 ? uct_value(c0, cp, cur_logN, sp.uct_c) : -inf;
-          const double v1 = in1 ? uct_value(c1, cp, cur_logN, sp.uct_c) : -inf;
+          const double v0 = uct_value_sel(c0, in0, cp, cur_logN, sp.uct_c);
+          const double v1 = WW::kTwoSlots ? uct_value_sel(c1, in1, cp, cur_logN, sp.uct_c) : -inf;
           chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
         }
         if (depth == 0) root_k = chosen;
