@@ -468,17 +468,8 @@ struct WaveWidth<ConnectFour> {  // <= 7 children
   static constexpr bool kTwoSlots = false;
 };
 
-// SearchNode::UCTValue (mcts.cc:89-100) for the player to move at the parent.
-template <class R>
-__device__ __forceinline__ double uct_value(const Node<R>& c, int cp, double logN,
-                                            double uct_c) {
-  if (c.out != kUnsolved) return outcome_for(c.out, cp);
-  if (c.n == 0) return __builtin_huge_val();
-  const double dn = static_cast<double>(c.n);
-  return static_cast<double>(c.w) / dn + uct_c * __builtin_sqrt(logN / dn);
-}
-
-// The same value for lane-distributed children, computed on every lane and
+// SearchNode::UCTValue (mcts.cc:89-100) for the player to move at the parent,
+// for lane-distributed children, computed on every lane and
 // selected (no exec-mask branches: the scalar unit is the wave kernels'
 // binding pipe, and a masked-off f64 division costs the VALU the same cycles).
 // Lanes outside the children score -inf.  A zero count divides to inf / NaN
