@@ -727,13 +727,20 @@ def cpu_baseline_playouts(game, seconds):
                                                     secs, cores_desc)}
 
 
+# Host-side units: the C-ABI, batch preparation and the small reduction
+# kernels (k_root_*, k_outcome_counts, k_sum_devices); the PMC'd kernels
+# (k_wsearch, k_mcts, k_rollouts, k_az_step, k_wselfplay) do not include them.
+HOST_UNITS = ("os_engine.hip", "os_host.cpp", "os_host.h", "Makefile")
+
+
 def kernel_source_hash():
-  """sha256 over the kernel sources (csrc/*): ties a PMC record to the code
-  it was collected on (tools/pmc_summary.py stores the same hash)."""
+  """sha256 over the sources of the PMC'd kernels (csrc/* minus the host
+  units): ties a PMC record to the code it was collected on
+  (tools/pmc_summary.py stores the same hash)."""
   h = hashlib.sha256()
   src = os.path.join(ROOT, "open_spiel-1_amd", "csrc")
   for name in sorted(os.listdir(src)):
-    if name.endswith((".h", ".hip", ".cpp")):
+    if name.endswith((".h", ".hip", ".cpp")) and name not in HOST_UNITS:
       with open(os.path.join(src, name), "rb") as f:
         h.update(name.encode() + b"\0" + f.read())
   return h.hexdigest()[:16]

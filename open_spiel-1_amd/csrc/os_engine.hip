@@ -89,9 +89,12 @@ __global__ void k_sum_devices(const int64_t* n, const double* w, int32_t ndev, i
 }
 
 // Outcome counts of a rollout batch: [0] player 0 ahead, [1] player 1 ahead,
-// [2] draws (sign of the mean player-0 return of each evaluator).
+// [2] draws (sign of the mean player-0 return of each evaluator).  Grid-stride
+// counting, a wave then a workgroup reduction, one atomic per counter per
+// workgroup (integer sums: order-independent).
 __global__ __launch_bounds__(256) void k_outcome_counts(const double* out, int64_t n,
                                                         unsigned long long* counts) {
+  __shared__ unsigned long long part[3][4];
   unsigned long long c0 = 0, c1 = 0, c2 = 0;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
@@ -105,12 +108,20 @@ __global__ __launch_bounds__(256) void k_outcome_counts(const double* out, int64
     c1 += __shfl_xor(c1, off);
     c2 += __shfl_xor(c2, off);
   }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&counts[0], c0);
-    atomicAdd(&counts[1], c1);
-    atomicAdd(&counts[2], c2);
+    part[0][w] = c0;
+    part[1][w] = c1;
+    part[2][w] = c2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const unsigned long long t = part[threadIdx.x][0] + part[threadIdx.x][1] +
+                                 part[threadIdx.x][2] + part[threadIdx.x][3];
+    atomicAdd(&counts[threadIdx.x], t);
   }
 }
+
 
 }  // namespace
 
@@ -1119,7 +1130,7 @@ int os_rollouts_outcomes_async(os_engine* e, int64_t* dev_counts, void* hip_stre
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipMemsetAsync(dev_counts, 0, 3 * sizeof(int64_t), st));
   if (e->roll_n == 0) return OS_OK;
-  const int64_t blocks = std::min<int64_t>((e->roll_n + 255) / 256, 4096);
+  const int64_t blocks = std::min<int64_t>((e->roll_n + 255) / 256, 512);
   hipLaunchKernelGGL(k_outcome_counts, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
                      static_cast<const double*>(e->d_rollout_out.p), e->roll_n,
                      reinterpret_cast<unsigned long long*>(dev_counts));
