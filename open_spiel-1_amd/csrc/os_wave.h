@@ -239,6 +239,34 @@ struct WaveMt {
     }
     return AbslUniform(*this, n);
   }
+  // absl::Uniform(rng, 0u, n) for any n (< 2^32) with the Lemire arithmetic
+  // on the vector unit: lane l evaluates the word pair (w_l, w_{l+1}) of the
+  // window and the draw reads lane pos.  A pair that straddles the window or
+  // whose product could need absl's rejection step (os_rng.h AbslUniform)
+  // takes the exact scalar path, so the stream is consumed identically.
+  __device__ uint32_t uniform_lanes(uint32_t n) {
+    if (pos + 2 <= valid) {
+      const uint32_t hi = cur;
+      const uint32_t lo = static_cast<uint32_t>(__shfl_down(static_cast<int>(cur), 1));
+      uint32_t r;
+      bool slow = false;
+      if ((n & (n - 1)) == 0) {
+        r = lo & (n - 1);
+      } else {
+        const uint64_t b = static_cast<uint64_t>(lo) * n;
+        const uint64_t mid = static_cast<uint64_t>(hi) * n + (b >> 32);
+        slow = static_cast<uint32_t>(mid) == 0 && static_cast<uint32_t>(b) < n;
+        r = static_cast<uint32_t>(mid >> 32);
+      }
+      const uint32_t v = rl32(slow ? 0x80000000u : r, pos);
+      if (!(v >> 31)) {
+        pos += 2;
+        words.add(2);
+        return v;
+      }
+    }
+    return AbslUniform(*this, n);
+  }
   // Stream offset of the next word, counted from the start of the block in s
   // (kMtN when that block is used up and the next draw twists).
   __device__ int offset() const { return base >= kMtN ? kMtN : base + pos; }
@@ -836,77 +864,74 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
 }
 
 // breakthrough random playout (mcts.cc:46-55) with lanes as board squares.
-// The legal set changes every move, so the moves stay serial, but each move's
-// LegalActions()[k] (breakthrough.cc:217-256: ascending action = source
-// square, then direction) is found without a scalar search: lane q holds
-// square q, and the number of legal actions from sources below q is the
-// mbcnt of the three per-direction source masks.  The source of action k is
-// the highest square with a move whose count-below is <= k (counts are
-// non-decreasing); its k - count-below picks the direction among the set
-// bits, in (left, forward, right) order.  Draws (absl or numpy), the move and
-// the win test (breakthrough.cc:306-319) stay on the scalar unit; the action
-// is never encoded, only its source / target squares are used.
+// The legal set changes every move, so the moves stay serial, but the board
+// lives in the lanes: lane q holds its square's black / white bit, and the
+// move generation (breakthrough.cc:217-256) is per-lane vector work -- each
+// lane tests its own piece's left / forward / right targets against the
+// occupancy masks (ballots, so they cost no scalar instruction) and counts
+// its legal actions.  LegalActions()[k] (ascending: source square, then
+// direction) is the highest lane whose count-below (mbcnt of the three
+// per-direction ballots) is <= k; its k - count-below picks the direction in
+// (left, forward, right) order.  The scalar unit -- the pipe that binds the
+// wave kernels -- keeps only the draw (absl or numpy), the chosen move's
+// squares and the win test (breakthrough.cc:306-319).
 template <int Policy, class Rng>
 __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev) {
   s = make_uniform(s);
   ev.uniformize();
+  const int q = lane_id();
   const int c = g.cols;
   const int last_row0 = (g.rows - 1) * c;  // first square of black's goal row
-  uint64_t b0 = s.pc[0], b1 = s.pc[1];
+  const int col = q % c;
+  const bool notcol0 = col != 0, notcollast = col != c - 1;
+  // Per-lane square bits, kept as 0 / 1 words.
+  uint32_t bk = static_cast<uint32_t>(s.pc[0] >> q) & 1u;
+  uint32_t wt = static_cast<uint32_t>(s.pc[1] >> q) & 1u;
   int p = s.to_play;
   int winner = s.winner;
-  for (;;) {
-    if (winner >= 0 || b0 == 0 || b1 == 0) break;
-    const uint64_t mine = p ? b1 : b0, theirs = p ? b0 : b1;
-    const uint64_t E = g.board64 & ~(b0 | b1);
-    const uint64_t EO = E | theirs;
-    uint64_t L, F, R;
-    if (p == 0) {
-      L = mine & g.notcol0_64 & (EO >> (c - 1));
-      F = mine & (E >> c);
-      R = mine & g.notcollast_64 & (EO >> (c + 1));
-    } else {
-      L = mine & g.notcol0_64 & (EO << (c + 1));
-      F = mine & (E << c);
-      R = mine & g.notcollast_64 & (EO << (c - 1));
-    }
-    const uint32_t n = static_cast<uint32_t>(popc64(L) + popc64(F) + popc64(R));
-    // The topmost piece always has a diagonal move unless cols == 1, where
-    // the reference indexes an empty LegalActions(); end the playout there.
-    if (n == 0) return 0;
-    const uint32_t k = Policy == kPolicyCpp ? AbslUniform(ev, n) : NpChoice(ev, n);
-    // Legal actions from the squares below this lane.
+  if (winner < 0 && (s.pc[0] == 0 || s.pc[1] == 0)) winner = s.pc[0] == 0 ? 1 : 0;
+  while (winner < 0) {
+    const uint32_t mine = p ? wt : bk, theirs = p ? bk : wt;
+    const uint64_t occ = ballot((bk | wt) != 0);
+    const uint64_t eo = ~occ | ballot(theirs != 0);  // empty or opponent
+    const int dq = p == 0 ? c : -c;
+    const int tf = q + dq;
+    const uint32_t fl = mine & notcol0 & static_cast<uint32_t>(eo >> ((tf - 1) & 63));
+    const uint32_t ff = mine & static_cast<uint32_t>(~occ >> (tf & 63));
+    const uint32_t fr = mine & notcollast & static_cast<uint32_t>(eo >> ((tf + 1) & 63));
+    const uint64_t L = ballot(fl & 1u), F = ballot(ff & 1u), R = ballot(fr & 1u);
     uint32_t below = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(L), 0u);
     below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(L >> 32), below);
     below = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(F), below);
     below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(F >> 32), below);
     below = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(R), below);
     below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(R >> 32), below);
-    const uint64_t cand = ballot(below <= k) & (L | F | R);
+    const uint32_t code = (fl & 1u) | ((ff & 1u) << 1) | ((fr & 1u) << 2);
+    const uint32_t n = rl32(below + __builtin_popcount(code), 63);
+    // The topmost piece always has a diagonal move unless cols == 1, where
+    // the reference indexes an empty LegalActions(); end the playout there.
+    if (n == 0) return 0;
+    const uint32_t k = Policy == kPolicyCpp ? ev.uniform_lanes(n) : NpChoice(ev, n);
+    const uint64_t cand = ballot(code != 0 && below <= k);
     const int src = 63 - __builtin_clzll(cand);
-    uint32_t rem = k - rl32(below, src);
-    int o;  // 0 left, 1 forward, 2 right (direction order within a source)
-    if ((L >> src) & 1) {
-      if (rem == 0) {
-        o = 0;
-        goto chosen;
-      }
-      --rem;
-    }
-    o = ((F >> src) & 1) && rem == 0 ? 1 : 2;
-  chosen:
-    const int tgt = src + (p == 0 ? c : -c) + (o - 1);
-    const uint64_t tb = 1ull << tgt;
-    const uint64_t nm = (mine & ~(1ull << src)) | tb;
-    const uint64_t nt = theirs & ~tb;
-    b0 = p ? nt : nm;
-    b1 = p ? nm : nt;
+    const uint32_t rem = k - rl32(below, src);
+    const uint32_t cs = rl32(code, src);
+    // rem-th set direction of cs in (left, forward, right) order.
+    const uint32_t low = cs & (0u - cs);               // first set direction
+    const uint32_t rest = cs & ~low;
+    const uint32_t second = rest & (0u - rest);
+    const uint32_t pick = rem == 0 ? low : (rem == 1 ? second : rest & ~second);
+    const int o = pick == 1u ? 0 : (pick == 2u ? 1 : 2);
+    const int tgt = src + dq + (o - 1);
+    const uint32_t nm = (mine & (q != src ? 1u : 0u)) | (q == tgt ? 1u : 0u);
+    const uint32_t nt = theirs & (q != tgt ? 1u : 0u);
+    bk = p ? nt : nm;
+    wt = p ? nm : nt;
     if (p == 0 ? tgt >= last_row0 : tgt < c) winner = p;
+    else if (!ballot(nt != 0)) winner = p;  // captured every opposing piece
     p ^= 1;
   }
-  if (winner == 0 || b1 == 0) return 1;
-  if (winner == 1 || b0 == 0) return -1;
-  return 0;
+  return winner == 0 ? 1 : -1;
 }
 
 template <class G, int Policy, class Rng, class C>
@@ -940,7 +965,7 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
     if (Policy == kPolicyCpp && SmallAbsl<G>::value)
       k = ev.uniform_small(static_cast<uint32_t>(l.count));
     else if (Policy == kPolicyCpp)
-      k = AbslUniform(ev, static_cast<uint32_t>(l.count));
+      k = ev.uniform_lanes(static_cast<uint32_t>(l.count));
     else
       k = NpChoice(ev, static_cast<uint32_t>(l.count));
     G::apply(s, g, ctx, l.kth(static_cast<int>(k)));
