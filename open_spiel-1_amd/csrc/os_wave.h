@@ -403,6 +403,33 @@ struct LaneArr {
   }
 };
 
+// x / d for the shuffle's pair draw without the integer-division sequence:
+// x * (floor(2^21 / d) + 1) >> 21 is exact for every x < (d - 1) * d,
+// 2 <= d <= 131 (checked exhaustively), which covers x < b0 * b1 for every
+// supported |LegalActions| (<= 128).
+static __constant__ const uint32_t kDivMagic[132] = {
+    0u, 2097153u, 1048577u, 699051u, 524289u, 419431u, 349526u, 299594u,
+    262145u, 233017u, 209716u, 190651u, 174763u, 161320u, 149797u, 139811u,
+    131073u, 123362u, 116509u, 110377u, 104858u, 99865u, 95326u, 91181u,
+    87382u, 83887u, 80660u, 77673u, 74899u, 72316u, 69906u, 67651u,
+    65537u, 63551u, 61681u, 59919u, 58255u, 56680u, 55189u, 53774u,
+    52429u, 51151u, 49933u, 48771u, 47663u, 46604u, 45591u, 44621u,
+    43691u, 42800u, 41944u, 41121u, 40330u, 39569u, 38837u, 38131u,
+    37450u, 36793u, 36158u, 35545u, 34953u, 34380u, 33826u, 33289u,
+    32769u, 32264u, 31776u, 31301u, 30841u, 30394u, 29960u, 29538u,
+    29128u, 28729u, 28340u, 27963u, 27595u, 27236u, 26887u, 26547u,
+    26215u, 25891u, 25576u, 25267u, 24967u, 24673u, 24386u, 24106u,
+    23832u, 23564u, 23302u, 23046u, 22796u, 22551u, 22311u, 22076u,
+    21846u, 21621u, 21400u, 21184u, 20972u, 20764u, 20561u, 20361u,
+    20165u, 19973u, 19785u, 19600u, 19419u, 19240u, 19066u, 18894u,
+    18725u, 18559u, 18397u, 18237u, 18079u, 17925u, 17773u, 17624u,
+    17477u, 17332u, 17190u, 17051u, 16913u, 16778u, 16645u, 16514u,
+    16385u, 16257u, 16132u, 16009u,
+};
+__device__ __forceinline__ uint32_t div_pair(uint32_t x, uint32_t d) {
+  return (x * kDivMagic[d]) >> 21;
+}
+
 template <int Policy, class Rng>
 __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
   if (Policy == kPolicyCpp) {  // libstdc++ 11 std::shuffle, pair path
@@ -415,8 +442,9 @@ __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
     while (i != n) {
       const uint32_t b0 = static_cast<uint32_t>(i) + 1u, b1 = b0 + 1u;
       const uint32_t x = Lemire32(g, b0 * b1);
-      a.swap(i, static_cast<int>(x / b1));
-      a.swap(i + 1, static_cast<int>(x % b1));
+      const uint32_t q = div_pair(x, b1);
+      a.swap(i, static_cast<int>(q));
+      a.swap(i + 1, static_cast<int>(x - q * b1));
       i += 2;
     }
   } else {  // numpy RandomState.shuffle
