@@ -119,6 +119,7 @@ __device__ __forceinline__ T make_uniform(const T& v) {
 struct WaveMt {
   uint32_t* s;     // LDS, 624 words
   uint32_t cur;    // per lane
+  uint32_t nxt;    // per lane: tempered word base + lane + 1 (cur of the next lane)
   int base;        // first word index held in cur; kMtN => block exhausted
   int valid;       // words held in cur
   int pos;         // next word (offset in cur)
@@ -137,6 +138,7 @@ struct WaveMt {
     twist_cycles = 0;
 #endif
     cur = 0;
+    nxt = 0;
     pre7 = 0x80000000u;
     base = kMtN;
     valid = 0;
@@ -151,10 +153,16 @@ struct WaveMt {
     const bool live = p < kMtN;
     base = live ? (p & ~63) : kMtN;
     valid = live ? (kMtN - base < 64 ? kMtN - base : 64) : 0;
-    const int i = base + lane_id();
-    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    load_window(base + lane_id());
     pre7 = use7 && live ? small7() : 0x80000000u;
     pos = live ? p - base : 0;
+  }
+  // The pair (cur, nxt) of every lane is read once per window, so
+  // uniform_lanes() needs no cross-lane shuffle per draw (small7() reads the
+  // pairs once per window and shuffles instead).
+  __device__ void load_window(int i) {
+    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    nxt = !use7 && i + 1 < kMtN ? MtStream::temper(s[i + 1]) : 0u;
   }
   __device__ int export_pos() const { return base >= kMtN ? kMtN : base + pos; }
 
@@ -192,8 +200,7 @@ struct WaveMt {
     }
     base = nb;
     valid = kMtN - base < 64 ? kMtN - base : 64;
-    const int i = base + lane_id();
-    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    load_window(base + lane_id());
     if (use7) pre7 = small7();
     pos = 0;
   }
@@ -247,7 +254,7 @@ struct WaveMt {
   __device__ uint32_t uniform_lanes(uint32_t n) {
     if (pos + 2 <= valid) {
       const uint32_t hi = cur;
-      const uint32_t lo = static_cast<uint32_t>(__shfl_down(static_cast<int>(cur), 1));
+      const uint32_t lo = nxt;
       uint32_t r;
       bool slow = false;
       if ((n & (n - 1)) == 0) {
@@ -295,8 +302,7 @@ struct WaveMt {
     }
     base = q & ~63;
     valid = kMtN - base < 64 ? kMtN - base : 64;
-    const int i = base + lane_id();
-    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
+    load_window(base + lane_id());
     pre7 = use7 ? small7() : 0x80000000u;
     pos = q - base;
   }
@@ -915,15 +921,20 @@ __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev)
   // Per-lane square bits, kept as 0 / 1 words.
   uint32_t bk = static_cast<uint32_t>(s.pc[0] >> q) & 1u;
   uint32_t wt = static_cast<uint32_t>(s.pc[1] >> q) & 1u;
-  int p = s.to_play;
   int winner = s.winner;
   if (winner < 0 && (s.pc[0] == 0 || s.pc[1] == 0)) winner = s.pc[0] == 0 ? 1 : 0;
-  while (winner < 0) {
-    const uint32_t mine = p ? wt : bk, theirs = p ? bk : wt;
+  if (winner >= 0) return winner == 0 ? 1 : -1;
+  // One move of player P (compile-time, so the mover's and the opponent's
+  // squares, the step direction and the goal test need no per-move select).
+  // Returns kMore while the game goes on, else the playout's return.
+  constexpr int kMore = 2;
+  auto move = [&](auto pc) -> int {
+    constexpr int P = decltype(pc)::value;
+    uint32_t& mine = P ? wt : bk;
+    uint32_t& theirs = P ? bk : wt;
     const uint64_t occ = ballot((bk | wt) != 0);
     const uint64_t eo = ~occ | ballot(theirs != 0);  // empty or opponent
-    const int dq = p == 0 ? c : -c;
-    const int tf = q + dq;
+    const int tf = P == 0 ? q + c : q - c;
     const uint32_t fl = mine & notcol0 & static_cast<uint32_t>(eo >> ((tf - 1) & 63));
     const uint32_t ff = mine & static_cast<uint32_t>(~occ >> (tf & 63));
     const uint32_t fr = mine & notcollast & static_cast<uint32_t>(eo >> ((tf + 1) & 63));
@@ -942,24 +953,33 @@ __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev)
     const uint32_t k = Policy == kPolicyCpp ? ev.uniform_lanes(n) : NpChoice(ev, n);
     const uint64_t cand = ballot(code != 0 && below <= k);
     const int src = 63 - __builtin_clzll(cand);
-    const uint32_t rem = k - rl32(below, src);
-    const uint32_t cs = rl32(code, src);
-    // rem-th set direction of cs in (left, forward, right) order.
-    const uint32_t low = cs & (0u - cs);               // first set direction
-    const uint32_t rest = cs & ~low;
+    // Every lane works out the move it would make as the source (the
+    // (k - below)-th set direction of its code in (left, forward, right)
+    // order, its target and whether that reaches the goal row); the scalar
+    // unit then reads one packed word from lane src.
+    const uint32_t rem = k - below;
+    const uint32_t low = code & (0u - code);           // first set direction
+    const uint32_t rest = code & ~low;
     const uint32_t second = rest & (0u - rest);
     const uint32_t pick = rem == 0 ? low : (rem == 1 ? second : rest & ~second);
-    const int o = pick == 1u ? 0 : (pick == 2u ? 1 : 2);
-    const int tgt = src + dq + (o - 1);
-    const uint32_t nm = (mine & (q != src ? 1u : 0u)) | (q == tgt ? 1u : 0u);
-    const uint32_t nt = theirs & (q != tgt ? 1u : 0u);
-    bk = p ? nt : nm;
-    wt = p ? nm : nt;
-    if (p == 0 ? tgt >= last_row0 : tgt < c) winner = p;
-    else if (!ballot(nt != 0)) winner = p;  // captured every opposing piece
-    p ^= 1;
+    const int tl = tf + (pick == 1u ? -1 : (pick == 2u ? 0 : 1));
+    const bool goal = P == 0 ? tl >= last_row0 : tl < c;
+    const uint32_t mv = rl32(static_cast<uint32_t>(tl & 63) | (goal ? 64u : 0u), src);
+    const int tgt = static_cast<int>(mv & 63u);
+    mine = (mine & (q != src ? 1u : 0u)) | (q == tgt ? 1u : 0u);
+    theirs &= q != tgt ? 1u : 0u;
+    // Reaching the goal row or capturing every opposing piece wins.
+    if ((mv & 64u) || !ballot(theirs != 0)) return P == 0 ? 1 : -1;
+    return kMore;
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  int r = s.to_play == 1 ? move(P1{}) : kMore;
+  while (r == kMore) {
+    r = move(P0{});
+    if (r == kMore) r = move(P1{});
   }
-  return winner == 0 ? 1 : -1;
+  return r;
 }
 
 template <class G, int Policy, class Rng, class C>
