@@ -255,17 +255,16 @@ struct WaveMt {
     if (pos + 2 <= valid) {
       const uint32_t hi = cur;
       const uint32_t lo = nxt;
-      uint32_t r;
-      bool slow = false;
-      if ((n & (n - 1)) == 0) {
-        r = lo & (n - 1);
-      } else {
-        const uint64_t b = static_cast<uint64_t>(lo) * n;
-        const uint64_t mid = static_cast<uint64_t>(hi) * n + (b >> 32);
-        slow = static_cast<uint32_t>(mid) == 0 && static_cast<uint32_t>(b) < n;
-        r = static_cast<uint32_t>(mid >> 32);
-      }
-      const uint32_t v = rl32(slow ? 0x80000000u : r, pos);
+      // Both forms are evaluated and selected (no branch on n).
+      const uint32_t m = n - 1;
+      const bool pow2 = (n & m) == 0;
+      const uint64_t b = static_cast<uint64_t>(lo) * n;
+      const uint64_t mid = static_cast<uint64_t>(hi) * n + (b >> 32);
+      const bool slow = static_cast<uint32_t>(mid) == 0 && static_cast<uint32_t>(b) < n;
+      const uint32_t pm = 0u - static_cast<uint32_t>(pow2);  // all ones for a power of two
+      const uint32_t lem = slow ? 0x80000000u : static_cast<uint32_t>(mid >> 32);
+      const uint32_t r = (lo & m & pm) | (lem & ~pm);
+      const uint32_t v = rl32(r, pos);
       if (!(v >> 31)) {
         pos += 2;
         words.add(2);
@@ -909,7 +908,7 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
 // (left, forward, right) order.  The scalar unit -- the pipe that binds the
 // wave kernels -- keeps only the draw (absl or numpy), the chosen move's
 // squares and the win test (breakthrough.cc:306-319).
-template <int Policy, class Rng>
+template <int Policy, bool kOneCol, class Rng>
 __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev) {
   s = make_uniform(s);
   ev.uniformize();
@@ -949,7 +948,7 @@ __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev)
     const uint32_t n = rl32(below + __builtin_popcount(code), 63);
     // The topmost piece always has a diagonal move unless cols == 1, where
     // the reference indexes an empty LegalActions(); end the playout there.
-    if (n == 0) return 0;
+    if (kOneCol && n == 0) return 0;
     const uint32_t k = Policy == kPolicyCpp ? ev.uniform_lanes(n) : NpChoice(ev, n);
     const uint64_t cand = ballot(code != 0 && below <= k);
     const int src = 63 - __builtin_clzll(cand);
@@ -986,7 +985,8 @@ template <class G, int Policy, class Rng, class C>
 __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
   if constexpr (std::is_same<G, Breakthrough>::value) {
     (void)ctx;
-    return bt_rollout_wave<Policy>(s, g, ev);
+    return g.cols == 1 ? bt_rollout_wave<Policy, true>(s, g, ev)
+                       : bt_rollout_wave<Policy, false>(s, g, ev);
   }
   if constexpr (Policy == kPolicyCpp && SmallAbsl<G>::value) {
     if (ev.use7) return c4_rollout_lanes(s, ctx, ev);

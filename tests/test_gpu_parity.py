@@ -21,6 +21,8 @@ CASES = [
     ("connect_four", 128, 1024, 8),
     ("breakthrough", 16, 512, 6),
     ("breakthrough(rows=6,columns=5)", 16, 300, 6),
+    ("breakthrough(rows=4,columns=3)", 16, 300, 2),  # narrow boards: edge columns,
+    ("breakthrough(rows=5,columns=2)", 16, 200, 2),  # short games, solver proofs
     ("hex(board_size=5)", 32, 400, 6),
     ("hex", 8, 400, 4),
     ("go(board_size=7,komi=4.5)", 8, 200, 6),
