@@ -76,6 +76,9 @@ def parse():
   ap.add_argument("--arena-nodes", type=int, default=0)
   ap.add_argument("--layout", default="auto", choices=("auto", "wave", "lane"),
                   help="search kernel: one wave per search / one lane per search")
+  ap.add_argument("--arena", default="paged", choices=("paged", "reserved"),
+                  help="search-tree arena (c2/c3): a page pool sized from the warmup "
+                       "run, or the worst case per root")
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
                   help="target CPU-baseline sample duration")
@@ -294,11 +297,19 @@ def bench_search(args, ctx, layout):
   bot_seeds, eval_seeds = gid, gid + np.uint32(EVAL_OFFSET)
 
   eng = ctx.engine(game)
+  eng.set_arena_mode(args.arena)
   eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
   handle = ctx.handle
   for _ in range(args.warmup):
     eng.run_async(handle)
   out = eng.fetch()  # synchronises; validates per-root status
+  if args.arena == "paged":
+    # The warmup run (reserved arena) sized the page pool: prepare again on
+    # it and check one run before timing.
+    eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
+    eng.run_async(handle)
+    out = eng.fetch()
+  arena0 = eng.arena_info()
   sims_per_step = eng.last_sims()
   alg_bytes = eng.algorithmic_bytes(R)
   stats = eng.stats()
@@ -314,6 +325,10 @@ def bench_search(args, ctx, layout):
 
   elapsed, kernel_ms = ctx.timed(lambda: eng.run_async(handle), args.steps)
   total_sims = ctx.total(sims_per_step * args.steps)
+  eng.fetch()
+  arena = eng.arena_info()
+  if arena["reruns"] != arena0["reruns"] or eng.last_sims() != sims_per_step:
+    raise RuntimeError("a timed run overflowed the page pool: %r" % (arena,))
 
   cpu = None
   if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
@@ -337,6 +352,7 @@ def bench_search(args, ctx, layout):
   line["cpu_baseline"] = cpu
   line["parity"] = parity
   line["tree_stats"] = stats
+  line["arena"] = dict(arena, mode=args.arena)
   return line
 
 

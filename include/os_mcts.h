@@ -164,6 +164,25 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
                    int32_t* n, double* w, int32_t* action, int32_t* nchild,
                    int8_t* out0);
 
+/* Search-tree arena (no reference counterpart: mcts.cc allocates SearchNode
+ * children on the heap).  RESERVED (default): every root gets the exact worst
+ * case 1 + max_simulations * max_children nodes.  PAGED: once a fetched run
+ * has shown how many nodes the searches take, later batches of the same
+ * shape (wave layout, >= 64 roots, GC unable to fire, arena_nodes == 0) share
+ * one pool of pages sized from it; a batch that still runs out of pages is
+ * rerun on the reserved arena inside os_engine_fetch (same seeds, same
+ * results).  Device outputs read before the fetch (os_engine_root_sums_async)
+ * are those of the overflowed run then: check os_engine_arena_info. */
+#define OS_ARENA_RESERVED 0
+#define OS_ARENA_PAGED 1
+int os_engine_set_arena_mode(os_engine* e, int32_t mode);
+/* out[0] 1 if the prepared batch is paged, [1] nodes per page (paged) or per
+ * root, [2] pool pages or roots per chunk, [3] arena bytes of the batch, [4]
+ * pages taken by the last run (paged; synchronises the device), [5] batches
+ * rerun on the reserved arena, [6] searches that ran out of pages, [7] bytes
+ * the reserved arena would take for the whole batch.  out has 8 entries. */
+int os_engine_arena_info(os_engine* e, int64_t* out);
+
 /* RandomRolloutEvaluator::Evaluate (mcts.cc:42-71) for n independent
  * evaluators, seeds[i], from one root; out_returns[2*i+{0,1}]. */
 int os_rollouts_batch(os_engine* e, const int64_t* root_actions,

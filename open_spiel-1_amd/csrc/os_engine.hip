@@ -6,9 +6,12 @@
 // This unit prepares batches (root replay, arena sizing, uploads), launches
 // the per-game kernels through the launcher table (os_kernels.h,
 // os_game_*.hip), fetches results and reports errors.
+#include <algorithm>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <random>
+#include <unordered_map>
 
 #include "os_engine_impl.h"
 
@@ -145,6 +148,7 @@ DevArgs MakeArgs(os_engine* e) {
   a.mt = static_cast<uint32_t*>(e->d_mt.p);
   a.arena = e->d_arena.p;
   a.cap = e->cap;
+  a.pages = e->paged ? static_cast<uint32_t*>(e->d_page_next.p) : nullptr;
   // Paths hold depth + 1 <= MaxGameLength + 1 nodes; keep slices 4-byte even.
   a.path_cap = e->game.cfg.max_game_length + 2;
   a.child_cap = (e->game.cfg.max_children + 1) & ~1;
@@ -231,6 +235,116 @@ int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t pol
   return OS_LAYOUT_WAVE;
 }
 
+// Nodes per page of the paged arena: room for 64 expansions of the widest
+// node, at least 256.
+uint32_t PageNodes(int max_children) {
+  uint32_t pn = 256;
+  while (pn < 64u * static_cast<uint32_t>(max_children)) pn <<= 1;
+  return pn;
+}
+constexpr int64_t kPagedMinRoots = 64;  // below this the reservation is small
+
+// Sizes the search arena of the prepared batch (e->params, e->num_roots):
+//  * reserved: the exact worst case 1 + sims * max_children per root (one
+//    expansion per simulation at most; plus the GC stack when GC can fire),
+//    unless the caller caps it, with roots chunked to fit ~60% of HBM;
+//  * paged (arena_mode OS_ARENA_PAGED, wave layout, no GC, >= 64 roots, and
+//    a hint from an earlier fetched run of the same shape): one pool of pages
+//    for the whole batch, sized from the pages the earlier runs needed per
+//    root (x 1.25 + slack).  A batch that still runs out of pages is rerun on
+//    the reserved arena by the fetch (os_engine_arena_info counts it).
+int SizeArena(os_engine* e, bool allow_paged) {
+  const os_mcts_params* p = &e->params;
+  const GameCfg& cfg = e->game.cfg;
+  const int64_t R = e->num_roots;
+  int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * cfg.max_children;
+  // GC (mcts.cc:402-424) can fire only if the node budget can be reached; its
+  // DFS stack then lives in the arena tail, so reserve room for it.
+  const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+  const bool gc_possible = max_nodes > 1 && worst >= max_nodes;
+  if (gc_possible) worst += GcStackReserve(cfg.max_children);
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  // The arena this engine already holds is released before a larger one.
+  const size_t budget = static_cast<size_t>((free_b + e->d_arena.bytes) * 0.6);
+  const size_t mt_bytes = 2 * kMtN * 4;
+  e->paged = false;
+  e->page_nodes = 0;
+  e->pool_pages = 0;
+  const uint32_t pn = PageNodes(cfg.max_children);
+  const auto& h = e->arena_hint;
+  if (allow_paged && e->arena_mode == OS_ARENA_PAGED && p->layout == OS_LAYOUT_WAVE &&
+      !gc_possible && p->arena_nodes == 0 && R >= kPagedMinRoots &&
+      h.sims == p->max_simulations && h.node_bytes == e->node_bytes && h.page_nodes == pn &&
+      2 * static_cast<int64_t>(pn) <= worst) {
+    const double extra = h.extra_per_root * static_cast<double>(R) * 1.25 +
+                         static_cast<double>(R) / 16.0 + 16.0;
+    const int64_t pages = R + static_cast<int64_t>(std::ceil(extra));
+    const size_t bytes = static_cast<size_t>(pages) * pn * e->node_bytes +
+                         static_cast<size_t>(R) * mt_bytes;
+    if (pages * static_cast<int64_t>(pn) < (int64_t(1) << 32) && bytes <= budget) {
+      e->paged = true;
+      e->page_nodes = pn;
+      e->pool_pages = static_cast<uint32_t>(pages);
+      e->cap = pn;
+      e->chunk_roots = R;
+      return OS_OK;
+    }
+  }
+  int64_t cap = p->arena_nodes > 0 ? std::min<int64_t>(p->arena_nodes, worst) : worst;
+  if (cap < 1) cap = 1;
+  if (cap > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "arena too large per root");
+  e->cap = static_cast<uint32_t>(cap);
+  // Chunk roots so that arena + MT state stay within ~60% of free HBM.
+  const size_t per_root = static_cast<size_t>(cap) * e->node_bytes + mt_bytes;
+  int64_t chunk = per_root ? static_cast<int64_t>(budget / per_root) : R;
+  if (chunk < 1) return Fail(OS_ERR_CAPACITY, "not enough device memory for one root");
+  e->chunk_roots = std::max<int64_t>(1, std::min<int64_t>(chunk, std::max<int64_t>(R, 1)));
+  return OS_OK;
+}
+
+// Allocates the arena SizeArena chose (a pool much smaller than the buffer
+// held from an earlier reserved run replaces it, so the footprint shrinks).
+int AllocArena(os_engine* e) {
+  const size_t need = e->paged
+      ? static_cast<size_t>(e->pool_pages) * e->page_nodes * e->node_bytes
+      : static_cast<size_t>(e->chunk_roots) * static_cast<size_t>(e->cap) * e->node_bytes;
+  if (e->d_arena.bytes > 2 * need) e->d_arena.release();
+  e->arena_bytes = need;
+  int rc = e->d_arena.ensure(need);
+  if (rc || !e->paged) return rc;
+  // The descriptor os_wave.h reads: {taken (zeroed per launch), page_nodes,
+  // pool_pages, first dynamic page = the roots' own pages}.
+  if ((rc = e->d_page_next.ensure(16))) return rc;
+  const uint32_t desc[4] = {0u, e->page_nodes, e->pool_pages,
+                            static_cast<uint32_t>(e->num_roots)};
+  HIP_TRY(hipMemcpy(e->d_page_next.p, desc, sizeof desc, hipMemcpyHostToDevice));
+  return OS_OK;
+}
+
+// Pages beyond its own that each root of the last fetched run would take in
+// the pool: a page fills to at least page_nodes - max_children + 1 nodes
+// before a child block spills into the next.
+void UpdateArenaHint(os_engine* e) {
+  if (e->params.layout != OS_LAYOUT_WAVE || e->last_results.empty()) return;
+  const int mc = e->game.cfg.max_children;
+  const uint32_t pn = PageNodes(mc);
+  const int64_t eff = static_cast<int64_t>(pn) - mc + 1;
+  double extra = 0.0;
+  for (const SearchResult& s : e->last_results) {
+    const int64_t a = s.used;
+    if (a > eff) extra += static_cast<double>((a - eff + eff - 1) / eff);
+  }
+  auto& h = e->arena_hint;
+  const double per_root = extra / static_cast<double>(e->last_results.size());
+  const bool same = h.sims == e->params.max_simulations && h.node_bytes == e->node_bytes &&
+                    h.page_nodes == pn;
+  h.extra_per_root = same ? std::max(h.extra_per_root, per_root) : per_root;
+  h.sims = e->params.max_simulations;
+  h.node_bytes = e->node_bytes;
+  h.page_nodes = pn;
+}
+
 // Uploads roots / seeds, sizes and allocates the arena and outputs.
 int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
             const int64_t* root_actions, const int64_t* root_offsets,
@@ -246,25 +360,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   e->max_children = cfg.max_children;
   e->node_bytes = p->n_rollouts == 1 ? static_cast<int>(sizeof(Node<int32_t>))
                                       : static_cast<int>(sizeof(Node<double>));
-  // Arena: exact worst case = 1 + sims * max_children (one expansion per
-  // simulation at most), unless the caller caps it.
-  int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * cfg.max_children;
-  // GC (mcts.cc:402-424) can fire only if the node budget can be reached; its
-  // DFS stack then lives in the arena tail, so reserve room for it.
-  const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
-  if (max_nodes > 1 && worst >= max_nodes) worst += GcStackReserve(cfg.max_children);
-  int64_t cap = p->arena_nodes > 0 ? std::min<int64_t>(p->arena_nodes, worst) : worst;
-  if (cap < 1) cap = 1;
-  if (cap > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "arena too large per root");
-  e->cap = static_cast<uint32_t>(cap);
-  // Chunk roots so that arena + MT state stay within ~60% of free HBM.
-  size_t free_b = 0, total_b = 0;
-  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const size_t per_root = static_cast<size_t>(cap) * e->node_bytes + 2 * kMtN * 4;
-  size_t budget = static_cast<size_t>(free_b * 0.6);
-  int64_t chunk = per_root ? static_cast<int64_t>(budget / per_root) : R;
-  if (chunk < 1) return Fail(OS_ERR_CAPACITY, "not enough device memory for one root");
-  e->chunk_roots = std::max<int64_t>(1, std::min<int64_t>(chunk, std::max<int64_t>(R, 1)));
+  if ((rc = SizeArena(e, true))) return rc;
 
   // Root states (+ go hash sets) on the host.
   const int sb = e->game.state_bytes;
@@ -322,7 +418,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   // Work buffers.
   const size_t C = static_cast<size_t>(e->chunk_roots);
   if ((rc = e->d_mt.ensure(C * 2 * kMtN * 4))) return rc;
-  if ((rc = e->d_arena.ensure(C * static_cast<size_t>(e->cap) * e->node_bytes))) return rc;
+  if ((rc = AllocArena(e))) return rc;
   const size_t MC = Rz * e->max_children;
   if ((rc = e->d_res.ensure(Rz * sizeof(SearchResult))) || (rc = e->d_cact.ensure(MC * 4)) ||
       (rc = e->d_cn.ensure(MC * 4)) || (rc = e->d_cw.ensure(MC * 8)) ||
@@ -345,7 +441,22 @@ int Run(os_engine* e, hipStream_t stream) {
   if (e->num_roots == 0) return OS_OK;
   const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
   if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  if (e->paged) HIP_TRY(hipMemsetAsync(e->d_page_next.p, 0, 4, stream));
   return L->search(e, MakeArgs(e), stream);
+}
+
+// A paged batch in which some search ran out of pool pages is run again on
+// the reserved arena (same seeds, so the same searches).
+int RerunReserved(os_engine* e) {
+  int rc;
+  if ((rc = SizeArena(e, false))) return rc;
+  if ((rc = e->d_mt.ensure(static_cast<size_t>(e->chunk_roots) * 2 * kMtN * 4))) return rc;
+  if ((rc = AllocArena(e))) return rc;
+  if ((rc = Run(e, nullptr))) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(e->last_results.data(), e->d_res.p, e->num_roots * sizeof(SearchResult),
+                    hipMemcpyDeviceToHost));
+  return OS_OK;
 }
 
 int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
@@ -362,6 +473,16 @@ int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
   e->last_results.resize(R);
   HIP_TRY(hipMemcpy(e->last_results.data(), e->d_res.p, R * sizeof(SearchResult),
                     hipMemcpyDeviceToHost));
+  if (e->paged) {
+    int64_t over = 0;
+    for (const SearchResult& s : e->last_results) over += s.status == kArenaOverflow;
+    if (over) {
+      e->arena_overflows += over;
+      e->arena_reruns += 1;
+      int rc = RerunReserved(e);
+      if (rc) return rc;
+    }
+  }
   e->last_sims = 0;
   for (int64_t r = 0; r < R; ++r) {
     const SearchResult& s = e->last_results[r];
@@ -375,6 +496,7 @@ int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
     e->last_sims += s.sims;
     if (nodes) nodes[r] = s.nodes;
   }
+  UpdateArenaHint(e);
   const int mcd = e->max_children;
   std::vector<int32_t> ca(R * mcd), cn(R * mcd);
   std::vector<double> cw(R * mcd);
@@ -439,6 +561,7 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
   HIP_TRY(hipSetDevice(e->device));
   e->params = *p;
   e->params.layout = OS_LAYOUT_WAVE;
+  e->paged = false;  // self-play trees use the reserved arena
   e->node_bytes = p->n_rollouts == 1 ? static_cast<int>(sizeof(Node<int32_t>))
                                       : static_cast<int>(sizeof(Node<double>));
   if ((rc = ArenaCap(e, p, &e->cap))) return rc;
@@ -972,6 +1095,20 @@ int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
   return OS_OK;
 }
 
+// Copies node i of a raw node array into the export arrays at slot o.
+static void ExportNode(const unsigned char* raw, size_t nb, uint32_t i, uint32_t o,
+                       uint32_t first, uint32_t* out_first, int32_t* n, double* w,
+                       int32_t* action, int32_t* nchild, int8_t* out0) {
+  if (nb == sizeof(Node<int32_t>)) {
+    const Node<int32_t>& x = reinterpret_cast<const Node<int32_t>*>(raw)[i];
+    n[o] = x.n; w[o] = x.w; action[o] = x.action; nchild[o] = x.nchild; out0[o] = x.out;
+  } else {
+    const Node<double>& x = reinterpret_cast<const Node<double>*>(raw)[i];
+    n[o] = x.n; w[o] = x.w; action[o] = x.action; nchild[o] = x.nchild; out0[o] = x.out;
+  }
+  out_first[o] = first;
+}
+
 int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
                    int32_t* n, double* w, int32_t* action, int32_t* nchild,
                    int8_t* out0) {
@@ -985,22 +1122,105 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
   if (!first) return OS_OK;
   HIP_TRY(hipSetDevice(e->device));
   const size_t nb = e->node_bytes;
-  std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
-  HIP_TRY(hipMemcpy(raw.data(),
-                    static_cast<unsigned char*>(e->d_arena.p) +
-                        static_cast<size_t>(r) * e->cap * nb,
-                    raw.size(), hipMemcpyDeviceToHost));
-  for (uint32_t i = 0; i < used; ++i) {
-    if (nb == sizeof(Node<int32_t>)) {
-      const Node<int32_t>& x = reinterpret_cast<const Node<int32_t>*>(raw.data())[i];
-      first[i] = x.first; n[i] = x.n; w[i] = x.w; action[i] = x.action;
-      nchild[i] = x.nchild; out0[i] = x.out;
-    } else {
-      const Node<double>& x = reinterpret_cast<const Node<double>*>(raw.data())[i];
-      first[i] = x.first; n[i] = x.n; w[i] = x.w; action[i] = x.action;
-      nchild[i] = x.nchild; out0[i] = x.out;
+  if (!e->paged) {
+    std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
+    HIP_TRY(hipMemcpy(raw.data(),
+                      static_cast<unsigned char*>(e->d_arena.p) +
+                          static_cast<size_t>(r) * e->cap * nb,
+                      raw.size(), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < used; ++i) {
+      const uint32_t f = nb == sizeof(Node<int32_t>)
+                             ? reinterpret_cast<const Node<int32_t>*>(raw.data())[i].first
+                             : reinterpret_cast<const Node<double>*>(raw.data())[i].first;
+      ExportNode(raw.data(), nb, i, i, f, first, n, w, action, nchild, out0);
+    }
+    return OS_OK;
+  }
+  // Paged: the tree's child blocks lie on the root's page and on pages taken
+  // later (higher page numbers, filled upward), so index order is allocation
+  // order.  Walk the tree from the root, reading each page once, and
+  // renumber the blocks in index order: the same arrays as the reserved arena.
+  const uint64_t pn = e->page_nodes;
+  const uint64_t base = static_cast<uint64_t>(r) * pn;  // node indices are relative to it
+  std::map<uint64_t, std::vector<unsigned char>> pages;
+  auto node_at = [&](uint64_t rel) -> const unsigned char* {
+    const uint64_t g = base + rel, pg = g / pn;
+    auto it = pages.find(pg);
+    if (it == pages.end()) {
+      std::vector<unsigned char> buf(pn * nb);
+      if (hipMemcpy(buf.data(), static_cast<unsigned char*>(e->d_arena.p) + pg * pn * nb,
+                    buf.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return nullptr;
+      it = pages.emplace(pg, std::move(buf)).first;
+    }
+    return it->second.data() + (g - pg * pn) * nb;
+  };
+  struct Blk { uint32_t rel, cnt; };
+  std::vector<Blk> blocks{{0u, 1u}};  // the root is a block of one
+  for (size_t b = 0; b < blocks.size(); ++b) {
+    for (uint32_t k = 0; k < blocks[b].cnt; ++k) {
+      const unsigned char* p = node_at(blocks[b].rel + k);
+      if (!p) return Fail(OS_ERR_DEVICE, "tree export copy failed");
+      uint32_t f;
+      uint8_t nc;
+      if (nb == sizeof(Node<int32_t>)) {
+        f = reinterpret_cast<const Node<int32_t>*>(p)->first;
+        nc = reinterpret_cast<const Node<int32_t>*>(p)->nchild;
+      } else {
+        f = reinterpret_cast<const Node<double>*>(p)->first;
+        nc = reinterpret_cast<const Node<double>*>(p)->nchild;
+      }
+      if (nc) blocks.push_back({f, nc});
     }
   }
+  std::sort(blocks.begin(), blocks.end(), [](const Blk& a, const Blk& b) { return a.rel < b.rel; });
+  std::unordered_map<uint32_t, uint32_t> renum;  // block start -> export index
+  uint32_t o = 0;
+  for (const Blk& b : blocks) { renum[b.rel] = o; o += b.cnt; }
+  if (o != used) return Fail(OS_ERR_DEVICE, "paged tree export: node count mismatch");
+  o = 0;
+  for (const Blk& b : blocks) {
+    for (uint32_t k = 0; k < b.cnt; ++k, ++o) {
+      const unsigned char* p = node_at(b.rel + k);
+      const bool i32 = nb == sizeof(Node<int32_t>);
+      const uint32_t f = i32 ? reinterpret_cast<const Node<int32_t>*>(p)->first
+                             : reinterpret_cast<const Node<double>*>(p)->first;
+      const uint8_t nc = i32 ? reinterpret_cast<const Node<int32_t>*>(p)->nchild
+                             : reinterpret_cast<const Node<double>*>(p)->nchild;
+      // A childless node keeps the reserved arena's first (0).
+      ExportNode(p, nb, 0, o, nc ? renum[f] : 0u, first, n, w, action, nchild, out0);
+    }
+  }
+  return OS_OK;
+}
+
+int os_engine_set_arena_mode(os_engine* e, int32_t mode) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (mode != OS_ARENA_RESERVED && mode != OS_ARENA_PAGED)
+    return Fail(OS_ERR_INVALID, "unknown arena mode");
+  e->arena_mode = mode;
+  return OS_OK;
+}
+
+int os_engine_arena_info(os_engine* e, int64_t* out) {
+  if (!e || !out) return Fail(OS_ERR_INVALID, "null argument");
+  out[0] = e->paged ? 1 : 0;
+  out[1] = e->paged ? e->page_nodes : e->cap;
+  out[2] = e->paged ? e->pool_pages : e->chunk_roots;
+  out[3] = static_cast<int64_t>(e->arena_bytes);
+  uint32_t dyn = 0;
+  if (e->paged && e->d_page_next.p) {
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&dyn, e->d_page_next.p, 4, hipMemcpyDeviceToHost));
+  }
+  out[4] = e->paged ? e->num_roots + dyn : 0;
+  out[5] = e->arena_reruns;
+  out[6] = e->arena_overflows;
+  // The reserved arena the batch would take: worst case per root x roots.
+  const GameCfg& cfg = e->game.cfg;
+  out[7] = (1 + static_cast<int64_t>(e->params.max_simulations) * cfg.max_children) *
+           e->num_roots * e->node_bytes;
   return OS_OK;
 }
 

@@ -51,8 +51,9 @@ struct DevArgs {
   const uint32_t* bot_seeds;
   const uint32_t* eval_seeds;
   uint32_t* mt;           // [num_roots][2][624]
-  void* arena;            // [num_roots][cap] Node<R>
-  uint32_t cap;
+  void* arena;            // [num_roots][cap] Node<R>, or the page pool
+  uint32_t cap;           // nodes per root, or per page when paged
+  uint32_t* pages;        // paged arena descriptor (os_wave.h kPg*), or null
   int32_t path_cap;       // >= MaxGameLength + 1 (LDS path slice per lane)
   int32_t child_cap;      // >= max |LegalActions| (LDS expansion slice)
   int32_t import_state;   // numpy (key, pos) import / export
@@ -244,6 +245,22 @@ struct os_engine {
       d_sp_obs, d_glog, d_glink, d_roll_cnt, d_rp_sum, d_rp_all;
   std::vector<osm::SearchResult> last_results;
   int64_t last_sims = 0;
+  // Paged arena (os_engine_set_arena_mode).  arena_mode is the
+  // caller's choice; `paged` says whether the prepared batch uses the pool.
+  int32_t arena_mode = 0;  // OS_ARENA_RESERVED
+  bool paged = false;
+  uint32_t page_nodes = 0;
+  uint32_t pool_pages = 0;
+  size_t arena_bytes = 0;  // arena of the prepared batch
+  osx::DevBuf d_page_next;
+  struct ArenaHint {  // pages beyond the roots' own, per root, of the last runs
+    int32_t sims = -1;
+    int32_t node_bytes = 0;
+    uint32_t page_nodes = 0;
+    double extra_per_root = 0.0;
+  } arena_hint;
+  int64_t arena_reruns = 0;     // batches rerun on the reserved arena
+  int64_t arena_overflows = 0;  // searches that ran out of pool pages
   ~os_engine() {
     osx::DevBuf* all[] = {&d_roots, &d_bseed, &d_eseed, &d_mt,  &d_arena, &d_lut,
                      &d_zob,   &d_rhash, &d_rnh,   &d_pos, &d_res,   &d_cact,
@@ -251,7 +268,7 @@ struct os_engine {
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
-                     &d_roll_cnt, &d_rp_sum, &d_rp_all};
+                     &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

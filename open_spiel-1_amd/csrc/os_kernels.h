@@ -173,7 +173,8 @@ struct WaveCtxMaker<Go> {
 
 template <class G, class R>
 __host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
-  return static_cast<size_t>(2 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+  return static_cast<size_t>(2 * kMtN * 4) + kPageDescLds +
+         static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
          (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
 }
 
@@ -190,6 +191,9 @@ struct WaveOcc<Hex> {
   static constexpr int value = OS_HEX_OCC;
 };
 
+#ifndef OS_PAGEABLE  // timing A/B only: 0 builds k_wsearch without the page pool
+#define OS_PAGEABLE true
+#endif
 template <class G, class R, int Policy>
 __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int64_t lr = blockIdx.x;
@@ -198,9 +202,12 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int l = lane_id();
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
-  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4);
+  // [MT bot | MT evaluator | page descriptor address | path | go log]
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4 + kPageDescLds);
   uint64_t* glog = reinterpret_cast<uint64_t*>(
-      smem + ((2 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+      smem + ((2 * kMtN * 4 + kPageDescLds + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  if (l == 0)
+    *reinterpret_cast<uint64_t*>(smem + 2 * kMtN * 4) = reinterpret_cast<uintptr_t>(a.pages);
   const bool shared = Policy == kPolicyNumpy && a.shared_stream;
   WaveMt bot, ev;
   bot.s = mt;
@@ -226,12 +233,12 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
       make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
   typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr, glog);
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
-  PhaseCycles ph = {};
+  PhaseCycles ph = {};  // paged: the root's page is page lr = blockIdx.x
   SearchResult res = shared
-      ? wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
-                                  a.path_cap, ph)
-      : wave_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
-                                  a.path_cap, ph);
+      ? wave_search<G, R, Policy, OS_PAGEABLE>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
+                                               path, a.path_cap, ph)
+      : wave_search<G, R, Policy, OS_PAGEABLE>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
+                                               path, a.path_cap, ph);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
   ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);

@@ -235,7 +235,7 @@ struct WaveMt {
   }
   // absl::Uniform(rng, 0u, n) for n <= 7 from the precomputed table, falling
   // back to the exact two-word draw (os_rng.h) when the table cannot answer.
-  __device__ uint32_t uniform_small(uint32_t n) {
+  __device__ __forceinline__ uint32_t uniform_small(uint32_t n) {
     if (pos + 2 <= valid) {
       const uint32_t pk = rl32(pre7, pos);
       if (!(pk >> 31)) {
@@ -251,7 +251,7 @@ struct WaveMt {
   // window and the draw reads lane pos.  A pair that straddles the window or
   // whose product could need absl's rejection step (os_rng.h AbslUniform)
   // takes the exact scalar path, so the stream is consumed identically.
-  __device__ uint32_t uniform_lanes(uint32_t n) {
+  __device__ __forceinline__ uint32_t uniform_lanes(uint32_t n) {
     if (pos + 2 <= valid) {
       const uint32_t hi = cur;
       const uint32_t lo = nxt;
@@ -1042,9 +1042,21 @@ __device__ __forceinline__ Node<int32_t> load_node(const Node<int32_t>* p) {
   return c;
 }
 
+// Paged arena: `pages` (global, null = the reserved
+// per-root arena of `cap` nodes) = {pages taken, page_nodes, pool_pages,
+// first dynamic page}.  The search starts on its own page (page blockIdx.x:
+// `nodes` points there, cap = page_nodes) and takes further pages off the
+// launch's counter when a child block does not fit the current one.  Node
+// indices stay relative to `nodes` (uint32; dynamic pages lie above).
+// k_wsearch leaves the descriptor's address in the kPageDescLds bytes of LDS
+// just below `path` (kPageable searches only): read on that rare path, it
+// holds no scalar registers across the search, which is at its SGPR budget.
+enum { kPgTaken = 0, kPgNodes = 1, kPgPool = 2, kPgFirstDynamic = 3 };
+constexpr int kPageDescLds = 16;
+
 // One search, executed by the whole wave.  `path` (LDS) has path_cap
 // entries.  Same contract as mcts_search.
-template <class G, class R, int Policy, class C>
+template <class G, class R, int Policy, bool kPageable = false, class C>
 __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     const typename G::State& root, C& ctx,
                                     Node<R>* nodes, uint32_t cap, WaveMt& bot,
@@ -1143,8 +1155,26 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         acts.a1 = l + 64 < nc ? static_cast<uint32_t>(lg.kth(l + 64)) : 0u;
         wave_shuffle<Policy>(acts, nc, bot);
         if (used + static_cast<uint32_t>(nc) > cap) {
-          res.status = kArenaOverflow;
-          goto done;
+          bool ok = false;
+          if constexpr (kPageable) {  // next page of the pool, if there is one
+            const uint64_t v = *reinterpret_cast<const volatile uint64_t*>(
+                reinterpret_cast<const unsigned char*>(path) - kPageDescLds);
+            uint32_t* const pg = reinterpret_cast<uint32_t*>(make_uniform(v));
+            if (pg) {
+              uint32_t np = 0;
+              if (l == 0) np = atomicAdd(pg + kPgTaken, 1u);  // one vector atomic
+              const uint4 d = make_uniform(*reinterpret_cast<const uint4*>(pg));
+              np = rl32(np, 0) + d.w;  // kPgFirstDynamic
+              const uint32_t pn = d.y;  // kPgNodes
+              ok = np < d.z;            // kPgPool
+              used = (np - blockIdx.x) * pn;
+              cap = used + pn;
+            }
+          }
+          if (!ok) {
+            res.status = kArenaOverflow;
+            goto done;
+          }
         }
         const uint32_t first = used;
         used += nc;
@@ -1449,7 +1479,7 @@ done:
   res.solver_scanned = c_solver.get();
   res.max_depth = static_cast<int32_t>(c_depth.get());
   res.nodes = nodes_count;
-  res.used = used;
+  res.used = 1 + res.expanded;  // nodes allocated (== used on the reserved arena)
   return res;
 }
 

@@ -126,6 +126,8 @@ _sig("os_engine_fetch", ctypes.c_int,
      [_vp, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P])
 _sig("os_engine_last_sims", _i64, [_vp])
 _sig("os_engine_stats", ctypes.c_int, [_vp, _P])
+_sig("os_engine_set_arena_mode", ctypes.c_int, [_vp, ctypes.c_int32])
+_sig("os_engine_arena_info", ctypes.c_int, [_vp, _P])
 _sig("os_engine_set_rollout_layout", ctypes.c_int, [_vp, _i32])
 _sig("os_rollouts_prepare", ctypes.c_int, [_vp, _P, _i64, _i64, _i32, _P])
 _sig("os_rollouts_run_async", ctypes.c_int, [_vp, _vp])

@@ -285,6 +285,24 @@ class Engine:
     d["state_bytes"] = int(lib.os_engine_state_bytes(self._h))
     return d
 
+  ARENA_KEYS = ("paged", "nodes_per_page_or_root", "pool_pages_or_chunk_roots",
+                "arena_bytes", "pages_used", "reruns", "overflowed_searches",
+                "reserved_bytes")
+
+  def set_arena_mode(self, mode):
+    """"reserved" (worst case per root) or "paged" (a page pool sized from
+    earlier fetched runs; include/os_mcts.h os_engine_set_arena_mode)."""
+    modes = {"reserved": 0, "paged": 1}
+    if mode not in modes:
+      raise ValueError("arena mode must be 'reserved' or 'paged'")
+    check(lib.os_engine_set_arena_mode(self._h, modes[mode]))
+
+  def arena_info(self):
+    """Arena of the prepared batch (os_engine_arena_info)."""
+    out = np.zeros(8, np.int64)
+    check(lib.os_engine_arena_info(self._h, ptr(out)))
+    return {k: int(v) for k, v in zip(self.ARENA_KEYS, out)}
+
   def algorithmic_bytes(self, num_roots):
     """HBM bytes the search must move, from the instrumentation.
 

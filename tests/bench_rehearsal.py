@@ -47,6 +47,12 @@ class HostEngine:
   def stats(self):
     return None
 
+  def set_arena_mode(self, mode):
+    assert mode in ("paged", "reserved")
+
+  def arena_info(self):
+    return {"paged": 0, "reruns": 0}  # no device arena on the host
+
   def algorithmic_bytes(self, num_roots):
     return 0
 

@@ -1,0 +1,103 @@
+"""Paged search arena (include/os_mcts.h os_engine_set_arena_mode).
+
+The reserved arena gives every root the worst case 1 + sims x max_children
+nodes.  In paged mode, once a fetched run has shown how many nodes the
+searches take, later batches of the same shape share one pool of pages; a
+batch that still runs out of pages is rerun on the reserved arena inside the
+fetch.  Either way the searches must be the oracle's, bit for bit.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def E(require_gpu):
+  from os_amd import engine
+  return engine
+
+
+def _batch(E, gs, R, sims, plies, seed=1000):
+  acts, offs = E.make_roots(gs, R, seed, plies)
+  bs = np.arange(R, dtype=np.uint32) + np.uint32(seed)
+  return acts, offs, bs, bs + np.uint32(1 << 20)
+
+
+def _run(eng, batch, sims):
+  acts, offs, bs, es = batch
+  eng.prepare(acts, offs, bs, es, uct_c=2.0, max_simulations=sims)
+  eng.run_async()
+  return eng.fetch(), eng.arena_info()
+
+
+def _check_oracle(E, gs, eng, out, batch, sims, roots=16):
+  acts, offs, bs, es = batch
+  ref = O.Game(gs).mcts_batch(acts[:offs[roots]], offs[:roots + 1], bs[:roots], es[:roots],
+                              uct_c=2.0, max_simulations=sims,
+                              max_children=eng.max_children, threads=8)
+  bad = [k for k in E.OUTPUT_KEYS if not np.array_equal(out[k][:roots], ref[k])]
+  assert not bad, bad
+
+
+@pytest.mark.parametrize("gs,R,sims,plies", [("connect_four", 256, 400, 6),
+                                             ("breakthrough", 128, 200, 4),
+                                             ("hex(board_size=7)", 96, 300, 4)])
+def test_paged_equals_reserved(E, gs, R, sims, plies):
+  eng = E.Engine(gs)
+  eng.set_arena_mode("paged")
+  batch = _batch(E, gs, R, sims, plies)
+  ref, info0 = _run(eng, batch, sims)       # no hint yet: reserved
+  assert info0["paged"] == 0
+  got, info = _run(eng, batch, sims)        # same shape: the pool
+  assert info["paged"] == 1 and info["reruns"] == 0
+  assert info["arena_bytes"] < info["reserved_bytes"]
+  assert info["pages_used"] <= info["pool_pages_or_chunk_roots"]
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+  _check_oracle(E, gs, eng, got, batch, sims)
+  # Tree export walks the pages and renumbers: the reserved arena's arrays.
+  eng2 = E.Engine(gs)
+  _run(eng2, batch, sims)
+  for r in (0, R // 2, R - 1):
+    a, b = eng.tree(r), eng2.tree(r)
+    for k in a:
+      np.testing.assert_array_equal(a[k], b[k], err_msg="root %d %s" % (r, k))
+
+
+def test_pool_overflow_reruns_reserved(E):
+  gs, R, sims = "connect_four", 128, 400
+  eng = E.Engine(gs)
+  eng.set_arena_mode("paged")
+  # Player 0 wins at once in column 0: the solver proves these roots within a
+  # few simulations, so the hint is about no pages beyond the roots' own.
+  acts, offs = E.roots_from_histories([[0, 1, 0, 1, 0, 1]] * R)
+  bs = np.arange(R, dtype=np.uint32)
+  late = (acts, offs, bs, bs + np.uint32(1 << 20))
+  _run(eng, late, sims)
+  assert _run(eng, late, sims)[1]["paged"] == 1
+  early = _batch(E, gs, R, sims, 0, seed=5000)  # opening roots: far bigger trees
+  got, info = _run(eng, early, sims)
+  assert info["reruns"] == 1 and info["overflowed_searches"] > 0
+  assert info["paged"] == 0  # the rerun's reserved arena
+  _check_oracle(E, gs, eng, got, early, sims)
+  # The hint now covers the big trees: the next batch fits the pool.
+  got2, info2 = _run(eng, early, sims)
+  assert info2["paged"] == 1 and info2["reruns"] == 1
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got2[k], got[k], err_msg=k)
+
+
+def test_reserved_is_default_and_small_batches_stay_reserved(E):
+  eng = E.Engine("tic_tac_toe")
+  batch = _batch(E, "tic_tac_toe", 128, 200, 2)
+  _run(eng, batch, 200)
+  assert _run(eng, batch, 200)[1]["paged"] == 0  # arena_mode defaults to reserved
+  eng.set_arena_mode("paged")
+  small = _batch(E, "tic_tac_toe", 16, 200, 2)
+  _run(eng, small, 200)
+  assert _run(eng, small, 200)[1]["paged"] == 0  # < 64 roots
+  with pytest.raises(ValueError):
+    eng.set_arena_mode("heap")
