@@ -61,6 +61,7 @@ CONFIGS = {
     "az": ("az", "connect_four", 16384, 128, 4),
 }
 KERNEL = {"wave": "k_wsearch", "lane": "k_mcts"}
+PAGED_ABOVE = 4 << 30  # --arena auto: page the arena when the reservation exceeds this
 
 
 def parse():
@@ -76,9 +77,10 @@ def parse():
   ap.add_argument("--arena-nodes", type=int, default=0)
   ap.add_argument("--layout", default="auto", choices=("auto", "wave", "lane"),
                   help="search kernel: one wave per search / one lane per search")
-  ap.add_argument("--arena", default="paged", choices=("paged", "reserved"),
+  ap.add_argument("--arena", default="auto", choices=("auto", "paged", "reserved"),
                   help="search-tree arena (c2/c3): a page pool sized from the warmup "
-                       "run, or the worst case per root")
+                       "run, the worst case per root, or (auto) the pool when the "
+                       "worst case would exceed %d GB" % (PAGED_ABOVE >> 30))
   ap.add_argument("--no-cpu-baseline", action="store_true")
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
                   help="target CPU-baseline sample duration")
@@ -297,13 +299,18 @@ def bench_search(args, ctx, layout):
   bot_seeds, eval_seeds = gid, gid + np.uint32(EVAL_OFFSET)
 
   eng = ctx.engine(game)
-  eng.set_arena_mode(args.arena)
+  eng.set_arena_mode("reserved" if args.arena == "reserved" else "paged")
   eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
   handle = ctx.handle
   for _ in range(args.warmup):
     eng.run_async(handle)
   out = eng.fetch()  # synchronises; validates per-root status
-  if args.arena == "paged":
+  arena_mode = args.arena
+  if arena_mode == "auto":
+    arena_mode = ("paged" if eng.arena_info().get("reserved_bytes", 0) > PAGED_ABOVE
+                  else "reserved")
+    eng.set_arena_mode(arena_mode)
+  if arena_mode == "paged":
     # The warmup run (reserved arena) sized the page pool: prepare again on
     # it and check one run before timing.
     eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
@@ -352,7 +359,7 @@ def bench_search(args, ctx, layout):
   line["cpu_baseline"] = cpu
   line["parity"] = parity
   line["tree_stats"] = stats
-  line["arena"] = dict(arena, mode=args.arena)
+  line["arena"] = dict(arena, mode=arena_mode)
   return line
 
 

@@ -168,7 +168,8 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
  * children on the heap).  RESERVED (default): every root gets the exact worst
  * case 1 + max_simulations * max_children nodes.  PAGED: once a fetched run
  * has shown how many nodes the searches take, later batches of the same
- * shape (wave layout, >= 64 roots, GC unable to fire, arena_nodes == 0) share
+ * shape (wave layout, C++ policy, >= 64 roots, GC unable to fire,
+ * arena_nodes == 0) share
  * one pool of pages sized from it; a batch that still runs out of pages is
  * rerun on the reserved arena inside os_engine_fetch (same seeds, same
  * results).  Device outputs read before the fetch (os_engine_root_sums_async)

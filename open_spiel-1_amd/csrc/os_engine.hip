@@ -248,8 +248,8 @@ constexpr int64_t kPagedMinRoots = 64;  // below this the reservation is small
 //  * reserved: the exact worst case 1 + sims * max_children per root (one
 //    expansion per simulation at most; plus the GC stack when GC can fire),
 //    unless the caller caps it, with roots chunked to fit ~60% of HBM;
-//  * paged (arena_mode OS_ARENA_PAGED, wave layout, no GC, >= 64 roots, and
-//    a hint from an earlier fetched run of the same shape): one pool of pages
+//  * paged (arena_mode OS_ARENA_PAGED, wave layout, C++ policy, no GC, >= 64
+//    roots, and a hint from an earlier fetched run of the same shape): one pool of pages
 //    for the whole batch, sized from the pages the earlier runs needed per
 //    root (x 1.25 + slack).  A batch that still runs out of pages is rerun on
 //    the reserved arena by the fetch (os_engine_arena_info counts it).
@@ -274,6 +274,7 @@ int SizeArena(os_engine* e, bool allow_paged) {
   const uint32_t pn = PageNodes(cfg.max_children);
   const auto& h = e->arena_hint;
   if (allow_paged && e->arena_mode == OS_ARENA_PAGED && p->layout == OS_LAYOUT_WAVE &&
+      p->policy == OS_POLICY_CPP &&
       !gc_possible && p->arena_nodes == 0 && R >= kPagedMinRoots &&
       h.sims == p->max_simulations && h.node_bytes == e->node_bytes && h.page_nodes == pn &&
       2 * static_cast<int64_t>(pn) <= worst) {

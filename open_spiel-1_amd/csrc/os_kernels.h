@@ -191,10 +191,10 @@ struct WaveOcc<Hex> {
   static constexpr int value = OS_HEX_OCC;
 };
 
-#ifndef OS_PAGEABLE  // timing A/B only: 0 builds k_wsearch without the page pool
-#define OS_PAGEABLE true
-#endif
-template <class G, class R, int Policy>
+// kPaged: the search may take pages from the pool (os_wave.h kPg*).  The
+// reserved-arena variant is a separate kernel: the cold page-switch path
+// costs the selection loop scalar registers (C2 +1.4% time).
+template <class G, class R, int Policy, bool kPaged>
 __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int64_t lr = blockIdx.x;
   if (lr >= a.num_roots) return;
@@ -235,9 +235,9 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   PhaseCycles ph = {};  // paged: the root's page is page lr = blockIdx.x
   SearchResult res = shared
-      ? wave_search<G, R, Policy, OS_PAGEABLE>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
+      ? wave_search<G, R, Policy, kPaged>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
                                                path, a.path_cap, ph)
-      : wave_search<G, R, Policy, OS_PAGEABLE>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
+      : wave_search<G, R, Policy, kPaged>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
                                                path, a.path_cap, ph);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
@@ -642,15 +642,24 @@ template <class G, class R, int Policy>
 int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   const size_t lds = WaveLdsBytes<G, R>(a.path_cap);
   if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsearch<G, R, Policy>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
+  // Paged batches run the C++ policy only (SizeArena).
+  constexpr bool kCanPage = Policy == kPolicyCpp;
+  const bool paged = kCanPage && a.pages != nullptr;
+  if (a.pages && !kCanPage) return Fail(OS_ERR_UNSUPPORTED, "paged arena needs the C++ policy");
+  const void* kfn = paged ? reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, kCanPage>)
+                          : reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, false>);
+  HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds)));
   for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
     a.root_base = base;
     a.num_roots = n;
-    hipLaunchKernelGGL((k_wsearch<G, R, Policy>), dim3(static_cast<unsigned>(n)), dim3(64),
-                       lds, stream, a);
+    if (paged)
+      hipLaunchKernelGGL((k_wsearch<G, R, Policy, kCanPage>), dim3(static_cast<unsigned>(n)),
+                         dim3(64), lds, stream, a);
+    else
+      hipLaunchKernelGGL((k_wsearch<G, R, Policy, false>), dim3(static_cast<unsigned>(n)),
+                         dim3(64), lds, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess)
       return Fail(OS_ERR_DEVICE, std::string("k_wsearch launch failed: ") +
