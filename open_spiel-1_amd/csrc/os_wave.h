@@ -435,9 +435,80 @@ __device__ __forceinline__ uint32_t div_pair(uint32_t x, uint32_t d) {
   return (x * kDivMagic[d]) >> 21;
 }
 
+// libstdc++ 11 std::shuffle (pair path; os_rng.h CppShuffle) on the lanes.
+// The serial form alternates a draw, a division and two swaps per step, all on
+// the scalar unit.  Here:
+//  1. lane k draws step k's Lemire32 word speculatively: window word pos + k,
+//     accepted unless its low product half is below the range (then Lemire
+//     could reject: that step is drawn exactly by the serial Lemire32, which
+//     refills and rejects as the reference, and the lanes resume after it);
+//  2. lane k splits its draw into the step's transposition targets;
+//  3. every lane traces its own final position back through the
+//     transpositions in reverse (the element at p after the last swap came
+//     from the partner of p), so the permutation costs a few vector compares
+//     per step instead of cross-lane swaps;
+//  4. one bpermute per slot gathers the shuffled array.
+// Step k: k < e (n even): (1, x), range 2; else i = 1 + e + 2 (k - e), range
+// (i + 1)(i + 2), x -> (i, x / (i + 2)) then (i + 1, x % (i + 2)).
+__device__ __forceinline__ void wave_shuffle_cpp(LaneArr& a, int n, WaveMt& g) {
+  if (n <= 1) return;
+  const int l = lane_id();
+  const int e = (n & 1) ? 0 : 1;
+  const int S = e + (n - 1 - e) / 2;  // <= 64 for n <= 128
+  const uint32_t ik = l < e ? 1u : static_cast<uint32_t>(1 + e + 2 * (l - e));
+  const uint32_t range = l < e ? 2u : (ik + 1u) * (ik + 2u);
+  uint32_t xs = 0;
+  for (int s = 0; s < S;) {
+    if (g.pos >= g.valid) g.refill();
+    const int cnt = min(S - s, g.valid - g.pos);
+    const uint32_t w = static_cast<uint32_t>(
+        __shfl(static_cast<int>(g.cur), (g.pos + l - s) & 63));
+    const uint64_t p = static_cast<uint64_t>(w) * range;
+    const bool mine = l >= s && l < s + cnt;
+    const uint64_t flagged = ballot(mine && static_cast<uint32_t>(p) < range);
+    const int acc = flagged ? ctz64(flagged) - s : cnt;
+    if (mine && l < s + acc) xs = static_cast<uint32_t>(p >> 32);
+    g.pos += acc;
+    g.words.add(static_cast<uint32_t>(acc));
+    s += acc;
+    if (acc < cnt) {  // a step Lemire could reject: drawn exactly
+      xs = wl32(Lemire32(g, rl32(range, s)), s, xs);
+      ++s;
+    }
+  }
+  const uint32_t b1 = ik + 2u;
+  const uint32_t qv = l < e ? xs : xs / b1;
+  const uint32_t rv = xs - qv * b1;  // unused for the single step
+  const bool two = n > 64;
+  int p0 = l, p1 = l + 64;
+  for (int k = S - 1; k >= 0; --k) {
+    const int i = k < e ? 1 : 1 + e + 2 * (k - e);
+    if (k >= e) {
+      const int r = static_cast<int>(rl32(rv, k));
+      p0 = p0 == i + 1 ? r : (p0 == r ? i + 1 : p0);
+      if (two) p1 = p1 == i + 1 ? r : (p1 == r ? i + 1 : p1);
+    }
+    const int q = static_cast<int>(rl32(qv, k));
+    p0 = p0 == i ? q : (p0 == q ? i : p0);
+    if (two) p1 = p1 == i ? q : (p1 == q ? i : p1);
+  }
+  const uint32_t s00 = static_cast<uint32_t>(__shfl(static_cast<int>(a.a0), p0 & 63));
+  const uint32_t s01 = static_cast<uint32_t>(__shfl(static_cast<int>(a.a1), p0 & 63));
+  uint32_t n1 = a.a1;
+  if (two) {
+    const uint32_t s10 = static_cast<uint32_t>(__shfl(static_cast<int>(a.a0), p1 & 63));
+    const uint32_t s11 = static_cast<uint32_t>(__shfl(static_cast<int>(a.a1), p1 & 63));
+    n1 = p1 < 64 ? s10 : s11;
+  }
+  a.a0 = p0 < 64 ? s00 : s01;
+  a.a1 = n1;
+}
+
 template <int Policy, class Rng>
 __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
-  if (Policy == kPolicyCpp) {  // libstdc++ 11 std::shuffle, pair path
+  if constexpr (Policy == kPolicyCpp && std::is_same<Rng, WaveMt>::value) {
+    wave_shuffle_cpp(a, n, g);
+  } else if (Policy == kPolicyCpp) {  // libstdc++ 11 std::shuffle, pair path
     if (n <= 1) return;
     int i = 1;
     if ((n & 1) == 0) {
