@@ -385,9 +385,20 @@ def bench_root_parallel(args, ctx, layout):
       ctx.dist.all_reduce(w)
     return v, w
 
+  be.eng.set_arena_mode("reserved" if args.arena == "reserved" else "paged")
   for _ in range(args.warmup):
     v, w = step()
   out = be.eng.fetch()
+  arena_mode = args.arena
+  if arena_mode == "auto":
+    arena_mode = ("paged" if be.eng.arena_info().get("reserved_bytes", 0) > PAGED_ABOVE
+                  else "reserved")
+    be.eng.set_arena_mode(arena_mode)
+  if arena_mode == "paged":  # as in bench_search: one checked run on the pool
+    be.prepare_root_parallel([], ids, ids + np.uint32(EVAL_OFFSET), **params)
+    v, w = step()
+    out = be.eng.fetch()
+  arena0 = be.eng.arena_info()
   sims_per_step = be.eng.last_sims()
   alg_bytes = be.eng.algorithmic_bytes(T)
   stats = be.eng.stats()
@@ -415,6 +426,10 @@ def bench_root_parallel(args, ctx, layout):
 
   elapsed, kernel_ms = ctx.timed(step, args.steps)
   total_sims = ctx.total(sims_per_step * args.steps)
+  be.eng.fetch()
+  arena = be.eng.arena_info()
+  if arena["reruns"] != arena0["reruns"] or be.eng.last_sims() != sims_per_step:
+    raise RuntimeError("a timed run overflowed the page pool: %r" % (arena,))
   cpu = None
   if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
     acts = np.zeros(0, np.int64)
@@ -434,6 +449,7 @@ def bench_root_parallel(args, ctx, layout):
                                                               be.num_actions),
                         "layout": lay, "sims_per_step_per_gpu": sims_per_step})
   line["roofline"] = _roofline(KERNEL[lay], game, alg_bytes, kernel_ms, sims_per_step, "sim")
+  line["arena"] = dict(arena, mode=arena_mode)
   line["cpu_baseline"] = cpu
   line["parity"] = parity
   line["root_visits_top5"] = sorted(
