@@ -76,27 +76,53 @@ struct MtStream {
 
 // The same stream over a structure-of-arrays batch: word i of this stream at
 // s[i * stride] (stride = streams in the batch), so lanes that draw in
-// lockstep read and write one contiguous line per word.  Seeded in place;
-// no numpy import.
+// lockstep read and write one contiguous line per word.  No numpy import.
+//
+// The seeded state is never stored.  During the first block, word i of the
+// twist reads seeded words i, i+1 and i+397, all in increasing order, so two
+// running cursors of the init_genrand recurrence supply them (`lo0`/`lo1` =
+// x_i / x_{i+1}, `hi` = x_{i+397}); only the twisted words are written (for
+// i+397 >= 624 and for the later blocks, which read them back).  The output is
+// std::mt19937's, and a playout writes 4 B per word drawn instead of the
+// 2.5 KB seed.
 struct MtStreamSoA {
   uint32_t* s;
   int64_t stride;
   int idx;
   uint32_t words;
+  int blk0;  // 1 while the first block is being drawn
+  uint32_t lo0, lo1, hi;
 
+  OS_HD static uint32_t seed_step(uint32_t x, int k) {
+    return 1812433253u * (x ^ (x >> 30)) + static_cast<uint32_t>(k);
+  }
   OS_HD uint32_t& at(int i) const { return s[static_cast<int64_t>(i) * stride]; }
   OS_HD void seed(uint32_t v) {
-    uint32_t x = v;
-    at(0) = x;
-    for (int i = 1; i < kMtN; ++i) {
-      x = 1812433253u * (x ^ (x >> 30)) + static_cast<uint32_t>(i);
-      at(i) = x;
-    }
-    idx = kMtN;
+    lo0 = v;
+    lo1 = seed_step(v, 1);
+    uint32_t x = lo1;
+    for (int k = 2; k <= kMtM; ++k) x = seed_step(x, k);
+    hi = x;
+    idx = 0;
+    blk0 = 1;
     words = 0;
   }
   OS_HD uint32_t next() {
     ++words;
+    if (blk0) {
+      const int i = idx;
+      const uint32_t b = (i + 1 == kMtN) ? at(0) : lo1;
+      const uint32_t m = (i + kMtM < kMtN) ? hi : at(i + kMtM - kMtN);
+      const uint32_t y = (lo0 & 0x80000000u) | (b & 0x7fffffffu);
+      const uint32_t v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      at(i) = v;
+      lo0 = lo1;
+      lo1 = seed_step(lo1, i + 2);
+      hi = seed_step(hi, i + kMtM + 1);
+      idx = i + 1;
+      if (idx == kMtN) blk0 = 0;
+      return MtStream::temper(v);
+    }
     if (idx >= kMtN) idx = 0;
     const int i = idx;
     const int i1 = (i + 1 == kMtN) ? 0 : i + 1;

@@ -305,6 +305,14 @@ void hc_mt_words(uint32_t seed, int64_t n, uint32_t* out) {
   MtStream g{s.data(), kMtN, 0, 0};
   for (int64_t i = 0; i < n; ++i) out[i] = g.next();
 }
+// k_rollouts' SoA stream (seeded words by cursors, never stored), interleaved
+// with `stride` - 1 other streams' words.
+void hc_mt_words_soa(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
+  std::vector<uint32_t> s(kMtN * stride, 0xdeadbeefu);
+  MtStreamSoA g{s.data() + stride - 1, stride, 0, 0};
+  g.seed(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = g.next();
+}
 void hc_absl_uniform(uint32_t seed, uint32_t n, int64_t k, uint64_t* out) {
   std::vector<uint32_t> s(kMtN);
   mt_seed(s.data(), seed);

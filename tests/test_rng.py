@@ -13,6 +13,14 @@ def test_mt_stream_matches_std_mt19937(seed):
   assert np.array_equal(H.mt_words(seed, 3000), O.mt19937(seed, 3000))
 
 
+@pytest.mark.parametrize("seed", [0, 1, 42, 5489, 2**32 - 1])
+@pytest.mark.parametrize("stride", [1, 3, 64])
+def test_soa_stream_matches_std_mt19937(seed, stride):
+  # k_rollouts' stream: the seeded block comes from running cursors (first
+  # block's reads of words i, i+1, i+397), the twisted words from memory.
+  assert np.array_equal(H.mt_words_soa(seed, stride, 2000), O.mt19937(seed, 2000))
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 48, 82, 121, 768])
 def test_absl_uniform_matches_oracle(n):
   for seed in (3, 99):
