@@ -36,6 +36,10 @@
 #ifndef OS_UNI_MT
 #define OS_UNI_MT 0
 #endif
+// 1: tic_tac_toe / connect_four keep the visit path in the lanes (LanePath).
+#ifndef OS_LANE_PATH
+#define OS_LANE_PATH 1
+#endif
 // Diagnostic build (-DOS_PHASE_TIMING=1): per-phase shader-clock cycles of the
 // wave search, summed over waves into PhaseCycles (os_debug_phase_cycles).
 #ifndef OS_PHASE_TIMING
@@ -1125,6 +1129,39 @@ __device__ __forceinline__ Node<int32_t> load_node(const Node<int32_t>* p) {
 enum { kPgTaken = 0, kPgNodes = 1, kPgPool = 2, kPgFirstDynamic = 3 };
 constexpr int kPageDescLds = 16;
 
+// The visit path held in the lanes (lane d <-> path entry d) for games whose
+// longest path fits a wave (MaxGameLength + 2 <= 64: tic_tac_toe,
+// connect_four).  Entries are written by per-lane selects (no exec-mask
+// branch, no LDS store), backup reads its own lane's entry, and the solver
+// reads entry d with one v_readlane per field.
+template <class G>
+struct LanePathGame : std::false_type {};
+template <>
+struct LanePathGame<TicTacToe> : std::true_type {};
+template <>
+struct LanePathGame<ConnectFour> : std::true_type {};
+
+template <class R>
+struct LanePath {
+  uint32_t idx = 0, first = 0;
+  int32_t n = 0, nc = 0;
+  R w = 0;
+  __device__ __forceinline__ void set(int d, uint32_t i, uint32_t f, int32_t cn, int32_t cnc,
+                                      R cw) {
+    const bool me = lane_id() == d;
+    idx = me ? i : idx;
+    first = me ? f : first;
+    n = me ? cn : n;
+    nc = me ? cnc : nc;
+    w = me ? cw : w;
+  }
+  __device__ __forceinline__ void set_children(int d, uint32_t f, int32_t cnc) {
+    const bool me = lane_id() == d;
+    first = me ? f : first;
+    nc = me ? cnc : nc;
+  }
+};
+
 // One search, executed by the whole wave.  `path` (LDS) has path_cap
 // entries.  Same contract as mcts_search.
 template <class G, class R, int Policy, bool kPageable = false, class C>
@@ -1179,6 +1216,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   Node<R> rc0 = zero_node, rc1 = zero_node;
   double rlg0 = 0.0, rlg1 = 0.0;
   int root_k = 0;
+  constexpr bool kLP = OS_LANE_PATH && LanePathGame<G>::value;
+  LanePath<R> lp;
+  if (kLP && path_cap > 64) path_cap = 64;
 
   for (int sim = 0; sim < sp.max_simulations; ++sim) {
     uint64_t t_ph = OS_PH_NOW();
@@ -1276,7 +1316,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           rlg0 = rlg1 = sp.log_lut[0];
           root_k = 0;
         } else {
-          if (l == 0) {
+          if constexpr (kLP) {
+            lp.set_children(depth, first, nc);
+          } else if (l == 0) {
             path[depth].first = first;
             path[depth].nc = nc;
           }
@@ -1370,7 +1412,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       cur_first = c_first;
       cur_n = c_n;
       cur_nc = c_nc;
-      if (l == 0) {
+      if constexpr (kLP) {
+        lp.set(depth, cur_idx, c_first, c_n, c_nc, c_w);
+      } else if (l == 0) {
         PathEnt<R>& pe = path[depth];
         pe.idx = cur_idx;
         pe.first = c_first;
@@ -1424,7 +1468,14 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       t_ph = OS_PH_NOW();
       // ---- backup: every path node at once (lane d <-> depth d) ----
       c_backed.add(depth + 1);
-      for (int d0 = 1; d0 <= depth; d0 += 64) {
+      if constexpr (kLP) {
+        if (l >= 1 && l <= depth) {
+          const int pl = P0 ^ ((l - 1) & 1);
+          Node<R>& nd = nodes[lp.idx];
+          nd.n = lp.n + 1;
+          nd.w = lp.w + (pl == 0 ? rv0 : rv1);
+        }
+      } else for (int d0 = 1; d0 <= depth; d0 += 64) {
         const int d = d0 + l;
         if (d <= depth) {
           const PathEnt<R>& pe = path[d];
@@ -1465,6 +1516,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             nfirst = root_first;
             nnc = root_nc;
             nidx = 0;
+          } else if constexpr (kLP) {
+            nfirst = rl32(lp.first, d);
+            nnc = rli(lp.nc, d);
+            nidx = rl32(lp.idx, d);
           } else {
             const PathEnt<R>& pe = path[d];
             nfirst = pe.first;

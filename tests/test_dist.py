@@ -73,18 +73,22 @@ def _free_port():
     return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, hip=False):
   os.environ["MASTER_ADDR"] = "127.0.0.1"
   os.environ["MASTER_PORT"] = str(port)
   dist.init_process_group("gloo", rank=rank, world_size=world)
   try:
-    be = HostBackend(HEX5)
+    # hip: every rank drives the real device engine (HipBackend) on cuda:0;
+    # gloo reduces the device tensors root_parallel / sharded_playouts return.
+    mk = (lambda gs: D.HipBackend(gs, device=0)) if hip else HostBackend
+    be = mk(HEX5)
     v, w = D.root_parallel(be, [12], trees_per_rank=3, max_simulations=SIMS)
-    c = D.sharded_playouts(HostBackend("connect_four"), [3, 3], total=37)
+    c = D.sharded_playouts(mk("connect_four"), [3, 3], total=37)
     acts, offs = _c4_roots(5)
-    g = D.independent_searches(HostBackend("connect_four"), acts, offs, gather=True,
+    g = D.independent_searches(mk("connect_four"), acts, offs, gather=True,
                                max_simulations=SIMS)
-    q.put((rank, v.numpy(), w.numpy(), c.numpy(), {k: np.asarray(x) for k, x in g.items()}))
+    q.put((rank, v.cpu().numpy(), w.cpu().numpy(), c.cpu().numpy(),
+           {k: np.asarray(x) for k, x in g.items()}))
   finally:
     dist.destroy_process_group()
 
@@ -129,10 +133,22 @@ def test_world1_matches_oracle():
 
 
 def test_gloo_world2_matches_single_process():
+  _check_world2(hip=False)
+
+
+@pytest.mark.gpu
+def test_gpu_gloo_world2_hip_backend(require_gpu):
+  """The same drivers over two rank processes that both drive the HIP engine
+  (one GPU on this box, so the ranks share device 0; gloo in place of RCCL,
+  which refuses two ranks on one device)."""
+  _check_world2(hip=True)
+
+
+def _check_world2(hip):
   world, port = 2, _free_port()
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
-  procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+  procs = [ctx.Process(target=_worker, args=(r, world, port, q, hip)) for r in range(world)]
   for p in procs:
     p.start()
   res = [q.get(timeout=300) for _ in range(world)]
