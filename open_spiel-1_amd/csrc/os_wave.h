@@ -36,6 +36,14 @@
 #ifndef OS_UNI_MT
 #define OS_UNI_MT 0
 #endif
+// 1: connect_four's win test in the tree walk on the vector unit (WaveApply).
+#ifndef OS_WAVE_APPLY
+#define OS_WAVE_APPLY 1
+#endif
+// 1: connect_four rollouts build their column / height nibbles on the lanes.
+#ifndef OS_C4_LANE_SETUP
+#define OS_C4_LANE_SETUP 1
+#endif
 // 1: tic_tac_toe / connect_four keep the visit path in the lanes (LanePath).
 #ifndef OS_LANE_PATH
 #define OS_LANE_PATH 1
@@ -671,6 +679,22 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
   const int l = lane_id();
   const int i = l & 15;  // run move index (every row computes the same run)
   // Ascending legal columns as nibbles, and column heights as nibbles.
+#if OS_C4_LANE_SETUP
+  // Lane c < 7 computes column c's nibbles (height at nibble c; c itself at
+  // nibble rank-of-c among the legal columns), one row scan sums them (the
+  // nibbles are disjoint) and lane 7 holds the total.
+  uint32_t cols, heights;
+  {
+    const uint32_t c = static_cast<uint32_t>(l & 7);
+    const uint64_t occ = s.bb[0] | s.bb[1];
+    const bool col = c < 7;
+    const uint32_t hc = col ? popc64((occ >> (7 * c)) & 0x3full) : 0u;
+    const bool lgl = col && ((s.legal >> c) & 1u);
+    const uint32_t rank = static_cast<uint32_t>(__builtin_popcount(s.legal & ((1u << c) - 1u)));
+    heights = rl32(row_scan_add(hc << (4 * c)), 7);
+    cols = rl32(row_scan_add(lgl ? c << (4 * rank) : 0u), 7);
+  }
+#else
   uint32_t cols = 0;
   {
     int q = 0;
@@ -682,6 +706,7 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
     for (int c = 0; c < 7; ++c)
       heights |= static_cast<uint32_t>(popc64((occ >> (7 * c)) & 0x3full)) << (4 * c);
   }
+#endif
   int p = s.to_play;
   int moves = s.moves;
   uint32_t legal = s.legal;
@@ -1129,6 +1154,41 @@ __device__ __forceinline__ Node<int32_t> load_node(const Node<int32_t>* p) {
 enum { kPgTaken = 0, kPgNodes = 1, kPgPool = 2, kPgFirstDynamic = 3 };
 constexpr int kPageDescLds = 16;
 
+// State::apply for the wave kernels' tree walk.  connect_four's four-in-a-row
+// test runs on the vector unit: lane j tests direction j & 3 (shift 1, 7, 6,
+// 8), one ballot ORs them -- the same predicate as ConnectFour::has_four, in
+// a handful of VALU ops instead of ~30 dependent 64-bit scalar ops and four
+// branches on the scalar unit (the wave kernels' binding pipe).
+template <class G>
+struct WaveApply {
+  template <class C>
+  __device__ __forceinline__ static void apply(typename G::State& s, const GameCfg& g, C& ctx,
+                                               int a) {
+    G::apply(s, g, ctx, a);
+  }
+};
+template <>
+struct WaveApply<ConnectFour> {
+  template <class C>
+  __device__ __forceinline__ static void apply(ConnectFour::State& s, const GameCfg&, C&,
+                                               int col) {
+    const int p = s.to_play;
+    const uint64_t occ = s.bb[0] | s.bb[1];
+    const uint64_t colmask = 0x3Full << (7 * col);
+    const uint64_t mv = (occ + (1ull << (7 * col))) & colmask;
+    const uint64_t mine = pick(s.bb, p) | mv;
+    put(s.bb, p, mine);
+    s.moves++;
+    if (mv & ConnectFour::kTopRow) s.legal &= ~(1u << col);
+    const int j = lane_id() & 3;
+    const uint32_t d = j == 0 ? 1u : (j == 1 ? 7u : (j == 2 ? 6u : 8u));
+    const uint64_t m = mine & (mine >> d);
+    if (ballot((m & (m >> (2 * d))) != 0)) s.outcome = p;
+    else if (s.moves == 42) s.outcome = 2;
+    s.to_play = 1 - p;
+  }
+};
+
 // The visit path held in the lanes (lane d <-> path entry d) for games whose
 // longest path fits a wave (MaxGameLength + 2 <= 64: tic_tac_toe,
 // connect_four).  Entries are written by per-lane selects (no exec-mask
@@ -1403,7 +1463,11 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         }
         cur_logN = rld(hi ? lg1 : lg0, src);
       }
+#if OS_WAVE_APPLY
+      WaveApply<G>::apply(s, g, ctx, static_cast<int>(c_action));
+#else
       G::apply(s, g, ctx, static_cast<int>(c_action));
+#endif
       if (++depth >= path_cap) {
         res.status = kPathOverflow;
         goto done;
