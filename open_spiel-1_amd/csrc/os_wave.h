@@ -44,6 +44,14 @@
 #ifndef OS_C4_LANE_SETUP
 #define OS_C4_LANE_SETUP 1
 #endif
+// 1: connect_four expansions take LegalActions()[lane] from a row scan.
+#ifndef OS_WAVE_KTH
+#define OS_WAVE_KTH 1
+#endif
+// 1: connect_four rollout lanes test four-in-a-row branch-free.
+#ifndef OS_C4_BF_FOUR
+#define OS_C4_BF_FOUR 1
+#endif
 // 1: tic_tac_toe / connect_four keep the visit path in the lanes (LanePath).
 #ifndef OS_LANE_PATH
 #define OS_LANE_PATH 1
@@ -742,7 +750,15 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
     }
     const uint64_t stones = row_scan_or_stride2(1ull << (7 * col + h));
     const uint64_t mine = ((i & 1) ? (p ? b0 : b1) : (p ? b1 : b0)) | stones;
+#if OS_C4_BF_FOUR
+    // Branch-free on the lanes (the early-exit form diverges per lane).
+    const uint64_t m1 = mine & (mine >> 1), m7 = mine & (mine >> 7);
+    const uint64_t m6 = mine & (mine >> 6), m8 = mine & (mine >> 8);
+    const bool win = ((m1 & (m1 >> 2)) | (m7 & (m7 >> 14)) | (m6 & (m6 >> 12)) |
+                      (m8 & (m8 >> 16))) != 0;
+#else
     const bool win = ConnectFour::has_four(mine);
+#endif
     const uint64_t term = ballot(l < Kr && (win || moves + i + 1 == 42));
     if (term) {
       const int t = ctz64(term);
@@ -1154,6 +1170,27 @@ __device__ __forceinline__ Node<int32_t> load_node(const Node<int32_t>* p) {
 enum { kPgTaken = 0, kPgNodes = 1, kPgPool = 2, kPgFirstDynamic = 3 };
 constexpr int kPageDescLds = 16;
 
+// LegalActions()[k] for lane k (k < count; other lanes get garbage) in the
+// wave kernels' expansion.  connect_four: the ascending legal columns as
+// nibbles from one row scan (lane c < 7 places c at nibble rank-of-c), then a
+// per-lane shift -- no per-lane loop over the mask.
+template <class G>
+struct WaveKth {
+  __device__ __forceinline__ static int kth(const typename G::Legal& lg, int k) {
+    return lg.kth(k);
+  }
+};
+template <>
+struct WaveKth<ConnectFour> {
+  __device__ __forceinline__ static int kth(const ConnectFour::Legal& lg, int k) {
+    const uint32_t c = static_cast<uint32_t>(lane_id() & 7);
+    const bool lgl = c < 7 && ((lg.mask >> c) & 1u);
+    const uint32_t rank = static_cast<uint32_t>(__builtin_popcount(lg.mask & ((1u << c) - 1u)));
+    const uint32_t cols = rl32(row_scan_add(lgl ? c << (4 * rank) : 0u), 7);
+    return static_cast<int>((cols >> (4 * (k & 7))) & 15u);
+  }
+};
+
 // State::apply for the wave kernels' tree walk.  connect_four's four-in-a-row
 // test runs on the vector unit: lane j tests direction j & 3 (shift 1, 7, 6,
 // 8), one ballot ORs them -- the same predicate as ConnectFour::has_four, in
@@ -1322,7 +1359,12 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         const typename G::Legal lg = G::legal(s, g, ctx);
         const int nc = lg.count;
         LaneArr acts;
+#if OS_WAVE_KTH
+        const int k0 = WaveKth<G>::kth(lg, l);  // every lane (row scan inside)
+        acts.a0 = l < nc ? static_cast<uint32_t>(k0) : 0u;
+#else
         acts.a0 = l < nc ? static_cast<uint32_t>(lg.kth(l)) : 0u;
+#endif
         acts.a1 = l + 64 < nc ? static_cast<uint32_t>(lg.kth(l + 64)) : 0u;
         wave_shuffle<Policy>(acts, nc, bot);
         if (used + static_cast<uint32_t>(nc) > cap) {
