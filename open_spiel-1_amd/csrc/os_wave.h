@@ -52,6 +52,10 @@
 #ifndef OS_C4_BF_FOUR
 #define OS_C4_BF_FOUR 1
 #endif
+// 1: the register mirror of the root's children is updated by selects.
+#ifndef OS_MIRROR_SEL
+#define OS_MIRROR_SEL 1
+#endif
 // 1: tic_tac_toe / connect_four keep the visit path in the lanes (LanePath).
 #ifndef OS_LANE_PATH
 #define OS_LANE_PATH 1
@@ -1575,11 +1579,12 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       // ---- backup: every path node at once (lane d <-> depth d) ----
       c_backed.add(depth + 1);
       if constexpr (kLP) {
-        if (l >= 1 && l <= depth) {
-          const int pl = P0 ^ ((l - 1) & 1);
-          Node<R>& nd = nodes[lp.idx];
-          nd.n = lp.n + 1;
-          nd.w = lp.w + (pl == 0 ? rv0 : rv1);
+        if (l <= depth) {  // lane 0 stores the root
+          const bool rt = l == 0;
+          const int pl = rt ? P0 : (P0 ^ ((l - 1) & 1));
+          Node<R>& nd = nodes[rt ? 0u : lp.idx];
+          nd.n = (rt ? root_n : lp.n) + 1;
+          nd.w = (rt ? root_w : lp.w) + (pl == 0 ? rv0 : rv1);
         }
       } else for (int d0 = 1; d0 <= depth; d0 += 64) {
         const int d = d0 + l;
@@ -1594,6 +1599,14 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       root_n += 1;
       root_logN = sp.log_lut[root_n];  // next simulation's root scan
       root_w += P0 == 0 ? rv0 : rv1;
+#if OS_MIRROR_SEL
+      if (!WW::kTwoSlots) {  // by selects: every lane reloads its log(n)
+        const bool me = depth >= 1 && l == root_k;
+        rc0.n += me ? 1 : 0;
+        rc0.w += me ? (P0 == 0 ? rv0 : rv1) : R(0);
+        rlg0 = sp.log_lut[rc0.n];
+      } else
+#endif
       if (depth >= 1 && l == (root_k & 63)) {  // mirror of path[1]'s update
         if (root_k < 64) {
           rc0.n += 1;
@@ -1605,7 +1618,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           rlg1 = sp.log_lut[rc1.n];
         }
       }
-      if (l == 0) {
+      if (!kLP && l == 0) {
         nodes[0].n = root_n;
         nodes[0].w = root_w;
       }
