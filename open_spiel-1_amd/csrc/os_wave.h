@@ -56,6 +56,10 @@
 #ifndef OS_MIRROR_SEL
 #define OS_MIRROR_SEL 1
 #endif
+// 1: narrow games screen the UCT argmax in f32 (exact f64 only on near ties).
+#ifndef OS_UCT_SCREEN
+#define OS_UCT_SCREEN 1
+#endif
 // 1: tic_tac_toe / connect_four keep the visit path in the lanes (LanePath).
 #ifndef OS_LANE_PATH
 #define OS_LANE_PATH 1
@@ -593,6 +597,49 @@ __device__ __forceinline__ int wave_argmax2(double v0, double v1) {
   const uint64_t b0 = ballot(v0 == m);
   if (b0) return ctz64(b0);
   return 64 + ctz64(ballot(v1 == m));
+}
+
+// Maximum of v over the first `Lanes` (<= 16) lanes by DPP, wave-uniform.
+template <int Lanes>
+__device__ __forceinline__ float wave_max_f32(float v) {
+  static_assert(Lanes <= 16, "row-local");
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
+                                                      decltype(ctrl)::value, 0xf, 0xf, false));
+  };
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0xB1>()));    // quad_perm [1,0,3,2]
+  if (Lanes > 2) v = fmaxf(v, dpp(v, std::integral_constant<int, 0x4E>()));   // [2,3,0,1]
+  if (Lanes > 4) v = fmaxf(v, dpp(v, std::integral_constant<int, 0x141>()));  // half mirror
+  if (Lanes > 8) v = fmaxf(v, dpp(v, std::integral_constant<int, 0x140>()));  // row mirror
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// UCT argmax screened in f32 (narrow games, integer rewards).  Every child's
+// f32 value A_k is within E = (1 + |c| sqrt(log N)) 2^-20 of the f64 value V_k
+// that mcts.cc:89-100 computes (each f32 step is within 2^-22 relative, the
+// inputs n, w < 2^24 convert exactly; solved outcomes are exact).  Let M be
+// the largest A and j the first lane holding it.  If every other child k has
+// A_k < M - 2E' (E' = 4E) or the same (n, w, out) as j -- then V_k == V_j and
+// the lower index j wins the strict '>' scan -- then j is the f64 argmax, and
+// it is returned.  Otherwise -1: the caller runs the exact f64 argmax.
+// Callers handle unvisited unsolved children (n == 0) first.
+template <int Lanes>
+__device__ __forceinline__ int uct_argmax_screen(const Node<int32_t>& c, bool in, int cp,
+                                                 double logN, double uct_c) {
+  const float r = __builtin_amdgcn_rcpf(static_cast<float>(c.n));  // 1 ulp
+  const float lf = static_cast<float>(logN);
+  const float cf = static_cast<float>(uct_c);
+  float a = static_cast<float>(c.w) * r + cf * __builtin_amdgcn_sqrtf(lf * r);  // 1 ulp
+  const float o = static_cast<float>(cp == 0 ? c.out : -c.out);
+  a = c.out != kUnsolved ? o : a;
+  a = in ? a : -__builtin_huge_valf();
+  const float m = wave_max_f32<Lanes>(a);
+  const int j = static_cast<int>(ctz64(ballot(a == m)));
+  const int32_t nj = rli(c.n, j), wj = rli(c.w, j);
+  const int32_t oj = rli(static_cast<int32_t>(c.out), j);
+  const float e2 = (1.0f + fabsf(cf) * __builtin_sqrtf(fmaxf(lf, 0.0f))) * 0x1p-17f;  // 2E'
+  const bool same = c.n == nj && c.w == wj && static_cast<int32_t>(c.out) == oj;
+  return ballot(in && a >= m - e2 && !same) ? -1 : j;
 }
 
 // Games whose rollout draws use WaveMt::uniform_small (|LegalActions| <= 7,
@@ -1461,10 +1508,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         double lg0 = 0.0, lg1 = 0.0;
         const bool in0 = l < cur_nc, in1 = WW::kTwoSlots && l + 64 < cur_nc;
         if (depth == 0) {  // root children: register-resident, no loads
-          if (in0) {
-            c0 = rc0;
-            lg0 = rlg0;
-          }
+          // Lanes past the last child hold zero_node in the mirror (every
+          // write to it keeps that), so no exec mask is needed here.
+          c0 = rc0;
+          lg0 = rlg0;
           if (in1) {
             c1 = rc1;
             lg1 = rlg1;
@@ -1489,6 +1536,13 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         if (f0 | f1) {
           chosen = f0 ? ctz64(f0) : 64 + ctz64(f1);
         } else {
+          chosen = -1;
+#if OS_UCT_SCREEN
+          if constexpr (!WW::kTwoSlots && WW::kLanes <= 16 && sizeof(R) == 4)
+            chosen = uct_argmax_screen<WW::kLanes>(c0, in0, cp, cur_logN, sp.uct_c);
+#endif
+        }
+        if (chosen < 0) {
           const double v0 = uct_value_sel(c0, in0, cp, cur_logN, sp.uct_c);
           const double v1 = WW::kTwoSlots ? uct_value_sel(c1, in1, cp, cur_logN, sp.uct_c) : -inf;
           chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);

@@ -1,0 +1,59 @@
+"""Error bound behind the wave kernel's f32-screened UCT argmax
+(csrc/os_wave.h uct_argmax_screen).
+
+The kernel computes A = w * rcp(n) + c * sqrt(logN * rcp(n)) in f32, with the
+hardware's 1-ulp v_rcp_f32 / v_sqrt_f32, and trusts the f32 argmax only when no
+other child is within 8E of it, E = (1 + |c| sqrt(logN)) 2^-20.  That is exact
+iff |A - V| <= E for the f64 value V of mcts.cc:89-100.  Here every f32 step is
+emulated with its worst-case error pushed both ways (rcp and sqrt off by one
+ulp up and down, each product / sum rounded to f32) over the count ranges the
+engine sees, and the deviation is checked against E.
+"""
+import numpy as np
+import pytest
+
+F = np.float32
+
+
+def _ulp_nudge(x, k):
+  """x moved by k ulps (f32)."""
+  x = np.asarray(x, F)
+  for _ in range(abs(k)):
+    x = np.nextafter(x, F(np.inf) if k > 0 else F(-np.inf))
+  return x
+
+
+def _screen_values(n, w, log_n, c, rcp_ulp, sqrt_ulp):
+  r = _ulp_nudge(F(1.0) / n.astype(F), rcp_ulp)
+  q = (w.astype(F) * r).astype(F)
+  t = (F(log_n) * r).astype(F)
+  s = _ulp_nudge(np.sqrt(t).astype(F), sqrt_ulp)
+  return (q + (F(c) * s).astype(F)).astype(F)
+
+
+@pytest.mark.parametrize("c", [2.0, 1.0, 0.5, 10.0])
+@pytest.mark.parametrize("parent", [1, 2, 3, 7, 100, 1023, 1024, 2048, 65535, 1 << 20])
+def test_f32_screen_within_bound(c, parent):
+  rng = np.random.default_rng(parent)
+  n = np.concatenate([np.arange(1, min(parent, 4096) + 1),
+                      rng.integers(1, parent + 1, 4096)]).astype(np.int64)
+  n = n[n <= parent]
+  w = np.concatenate([n, -n, np.zeros_like(n), rng.integers(-n, n + 1)])
+  n = np.tile(n, 4)
+  log_n = np.log(np.float64(parent))
+  v = w / n + c * np.sqrt(log_n / n)  # f64, as mcts.cc
+  e = (1.0 + abs(c) * np.sqrt(max(log_n, 0.0))) * 2.0 ** -20
+  for ru in (-1, 0, 1):
+    for su in (-1, 0, 1):
+      a = _screen_values(n, w, log_n, c, ru, su).astype(np.float64)
+      assert np.max(np.abs(a - v)) <= e
+
+
+def test_identical_children_give_identical_f32_values():
+  # The screen accepts near ties only between children with equal (n, w, out):
+  # their f32 values are bitwise equal, so the first lane holding the max is
+  # also the lowest index among the f64 maxima.
+  n = np.array([5, 5, 5], np.int64)
+  w = np.array([2, 2, 2], np.int64)
+  a = _screen_values(n, w, np.log(40.0), 2.0, 0, 0)
+  assert a[0] == a[1] == a[2]
