@@ -56,9 +56,10 @@
 #ifndef OS_MIRROR_SEL
 #define OS_MIRROR_SEL 1
 #endif
-// 1: narrow games screen the UCT argmax in f32 (exact f64 only on near ties).
+// UCT argmax screened in f32 (exact f64 only on near ties): 1 narrow games,
+// 2 every game.
 #ifndef OS_UCT_SCREEN
-#define OS_UCT_SCREEN 1
+#define OS_UCT_SCREEN 2
 #endif
 // 1: tic_tac_toe / connect_four keep the visit path in the lanes (LanePath).
 #ifndef OS_LANE_PATH
@@ -599,47 +600,69 @@ __device__ __forceinline__ int wave_argmax2(double v0, double v1) {
   return 64 + ctz64(ballot(v1 == m));
 }
 
-// Maximum of v over the first `Lanes` (<= 16) lanes by DPP, wave-uniform.
+// Maximum of v over the first `Lanes` lanes by DPP (as wave_max_f64),
+// wave-uniform.
+template <int Ctrl, int RowMask = 0xf>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), Ctrl, RowMask, 0xf, false));
+}
 template <int Lanes>
 __device__ __forceinline__ float wave_max_f32(float v) {
-  static_assert(Lanes <= 16, "row-local");
-  auto dpp = [](float x, auto ctrl) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
-                                                      decltype(ctrl)::value, 0xf, 0xf, false));
-  };
-  v = fmaxf(v, dpp(v, std::integral_constant<int, 0xB1>()));    // quad_perm [1,0,3,2]
-  if (Lanes > 2) v = fmaxf(v, dpp(v, std::integral_constant<int, 0x4E>()));   // [2,3,0,1]
-  if (Lanes > 4) v = fmaxf(v, dpp(v, std::integral_constant<int, 0x141>()));  // half mirror
-  if (Lanes > 8) v = fmaxf(v, dpp(v, std::integral_constant<int, 0x140>()));  // row mirror
+  v = fmaxf(v, dpp_f32<0xB1>(v));                   // quad_perm [1,0,3,2]
+  if (Lanes > 2) v = fmaxf(v, dpp_f32<0x4E>(v));    // quad_perm [2,3,0,1]
+  if (Lanes > 4) v = fmaxf(v, dpp_f32<0x141>(v));   // row_half_mirror
+  if (Lanes > 8) v = fmaxf(v, dpp_f32<0x140>(v));   // row_mirror
+  if (Lanes > 16) {
+    v = fmaxf(v, dpp_f32<0x142, 0xa>(v));  // row_bcast15 -> rows 1, 3
+    v = fmaxf(v, dpp_f32<0x143, 0xc>(v));  // row_bcast31 -> rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+  }
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
-// UCT argmax screened in f32 (narrow games, integer rewards).  Every child's
-// f32 value A_k is within E = (1 + |c| sqrt(log N)) 2^-20 of the f64 value V_k
-// that mcts.cc:89-100 computes (each f32 step is within 2^-22 relative, the
-// inputs n, w < 2^24 convert exactly; solved outcomes are exact).  Let M be
-// the largest A and j the first lane holding it.  If every other child k has
-// A_k < M - 2E' (E' = 4E) or the same (n, w, out) as j -- then V_k == V_j and
-// the lower index j wins the strict '>' scan -- then j is the f64 argmax, and
-// it is returned.  Otherwise -1: the caller runs the exact f64 argmax.
-// Callers handle unvisited unsolved children (n == 0) first.
-template <int Lanes>
-__device__ __forceinline__ int uct_argmax_screen(const Node<int32_t>& c, bool in, int cp,
-                                                 double logN, double uct_c) {
+// UCT argmax screened in f32 (integer rewards).  Every child's f32 value A_k
+// is within E = (1 + |c| sqrt(log N)) 2^-20 of the f64 value V_k that
+// mcts.cc:89-100 computes (each f32 step is within 2^-22 relative, the inputs
+// n, w < 2^24 convert exactly; solved outcomes are exact;
+// tests/test_uct_screen.py).  Let M be the largest A and j the first child
+// holding it.  If every other child k has A_k < M - 2E' (E' = 4E) or the same
+// (n, w, out) as j -- then V_k == V_j and the lower index j wins the strict
+// '>' scan -- then j is the f64 argmax, and it is returned.  Otherwise -1: the
+// caller runs the exact f64 argmax.  Child k = l + 64 h is in slot h of lane
+// l.  Callers handle unvisited unsolved children (n == 0) first.
+__device__ __forceinline__ float uct_screen_value(const Node<int32_t>& c, bool in, int cp,
+                                                  float lf, float cf) {
   const float r = __builtin_amdgcn_rcpf(static_cast<float>(c.n));  // 1 ulp
-  const float lf = static_cast<float>(logN);
-  const float cf = static_cast<float>(uct_c);
   float a = static_cast<float>(c.w) * r + cf * __builtin_amdgcn_sqrtf(lf * r);  // 1 ulp
   const float o = static_cast<float>(cp == 0 ? c.out : -c.out);
   a = c.out != kUnsolved ? o : a;
-  a = in ? a : -__builtin_huge_valf();
-  const float m = wave_max_f32<Lanes>(a);
-  const int j = static_cast<int>(ctz64(ballot(a == m)));
-  const int32_t nj = rli(c.n, j), wj = rli(c.w, j);
-  const int32_t oj = rli(static_cast<int32_t>(c.out), j);
+  return in ? a : -__builtin_huge_valf();
+}
+template <int Lanes, bool TwoSlots>
+__device__ __forceinline__ int uct_argmax_screen(const Node<int32_t>& c0, bool in0,
+                                                 const Node<int32_t>& c1, bool in1, int cp,
+                                                 double logN, double uct_c) {
+  const float lf = static_cast<float>(logN);
+  const float cf = static_cast<float>(uct_c);
+  const float a0 = uct_screen_value(c0, in0, cp, lf, cf);
+  const float a1 = TwoSlots ? uct_screen_value(c1, in1, cp, lf, cf) : -__builtin_huge_valf();
+  const float m = wave_max_f32<Lanes>(TwoSlots ? fmaxf(a0, a1) : a0);
+  const uint64_t t0 = ballot(a0 == m);
+  const int j = t0 ? static_cast<int>(ctz64(t0)) : 64 + static_cast<int>(ctz64(ballot(a1 == m)));
+  const bool hi = TwoSlots && j >= 64;  // wave-uniform
+  const int src = j & 63;
+  const int32_t nj = rli(hi ? c1.n : c0.n, src), wj = rli(hi ? c1.w : c0.w, src);
+  const int32_t oj = rli(static_cast<int32_t>(hi ? c1.out : c0.out), src);
   const float e2 = (1.0f + fabsf(cf) * __builtin_sqrtf(fmaxf(lf, 0.0f))) * 0x1p-17f;  // 2E'
-  const bool same = c.n == nj && c.w == wj && static_cast<int32_t>(c.out) == oj;
-  return ballot(in && a >= m - e2 && !same) ? -1 : j;
+  const float lo = m - e2;
+  const bool same0 = c0.n == nj && c0.w == wj && static_cast<int32_t>(c0.out) == oj;
+  bool near = in0 && a0 >= lo && !same0;
+  if (TwoSlots) {
+    const bool same1 = c1.n == nj && c1.w == wj && static_cast<int32_t>(c1.out) == oj;
+    near = near || (in1 && a1 >= lo && !same1);
+  }
+  return ballot(near) ? -1 : j;
 }
 
 // Games whose rollout draws use WaveMt::uniform_small (|LegalActions| <= 7,
@@ -1538,8 +1561,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         } else {
           chosen = -1;
 #if OS_UCT_SCREEN
-          if constexpr (!WW::kTwoSlots && WW::kLanes <= 16 && sizeof(R) == 4)
-            chosen = uct_argmax_screen<WW::kLanes>(c0, in0, cp, cur_logN, sp.uct_c);
+          if constexpr (sizeof(R) == 4 && (OS_UCT_SCREEN == 2 || !WW::kTwoSlots))
+            chosen = uct_argmax_screen<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
+                                                                  cur_logN, sp.uct_c);
 #endif
         }
         if (chosen < 0) {
