@@ -1728,7 +1728,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           c_solver.add(nnc);
           bool any_unsolved = false;
           int best_v = -128;
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < (WW::kTwoSlots ? 2 : 1); ++h) {
             const int k = l + 64 * h;
             int8_t co = kUnsolved;
             if (k < nnc) {
@@ -1738,13 +1738,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             }
             const bool uns = k < nnc && co == kUnsolved;
             if (ballot(uns)) any_unsolved = true;
-            int v = (k < nnc && co != kUnsolved) ? (cpl == 0 ? co : -co) : -128;
-            for (int off = 32; off >= 1; off >>= 1) {
-              const int ov = __shfl_xor(v, off);
-              v = ov > v ? ov : v;
-            }
-            v = rli(v, 0);
-            if (v > best_v) best_v = v;
+            const int v = (k < nnc && co != kUnsolved) ? (cpl == 0 ? co : -co) : -128;
+            // Solved values are -1 / 0 / +1: the maximum by three ballots.
+            const int m = ballot(v == 1) ? 1 : (ballot(v == 0) ? 0 : (ballot(v == -1) ? -1 : -128));
+            if (m > best_v) best_v = m;
           }
           if (best_v > -128 && (!any_unsolved || best_v == 1)) {
             const int8_t no = static_cast<int8_t>(cpl == 0 ? best_v : -best_v);
