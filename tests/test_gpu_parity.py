@@ -264,3 +264,25 @@ def test_cpp_style_bot_plays(E):
                                          [3], [7], uct_c=2.0, max_simulations=300)
   assert [c.action for c in root.children] == list(ref["child_action"][0][:9])
   assert [c.explore_count for c in root.children] == list(ref["child_n"][0][:9])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs", ["tic_tac_toe", "connect_four", "hex(board_size=5)",
+                                "breakthrough(rows=5,columns=5)"])
+@pytest.mark.parametrize("uct_c,solve", [(0.0, True), (0.0, False), (0.01, True),
+                                         (10.0, False), (2.0, False)])
+def test_uct_screen_ties_and_near_ties(E, gs, uct_c, solve):
+  """The wave kernel's f32 UCT screen (os_wave.h uct_argmax_screen) against the
+  oracle where its fallback matters: uct_c = 0 makes equal ratios w/n from
+  different (n, w) exact ties (1/2 vs 2/4), a tiny uct_c makes them near ties,
+  a large one stretches the bound."""
+  from os_amd import _lib
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, 24, 1000, 3)
+  bs = np.arange(24, dtype=np.uint32) * 7 + 5
+  es = bs + np.uint32(1 << 20)
+  kw = dict(uct_c=uct_c, max_simulations=600, solve=solve)
+  got = eng.mcts_batch(acts, offs, bs, es, layout=_lib.LAYOUT_WAVE, **kw)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, threads=8,
+                              **kw)
+  _cmp(E, got, ref)
