@@ -80,6 +80,13 @@ class ExternalEvaluatorSearch:
     self.steps = 0
     self.requests = 0
     self.events = []
+    # The evaluator of step k is queued right behind step k, before the host
+    # reads step k's request count, so the host launches the network while the
+    # GPU still runs the step and queues step k + 1 while the network runs.
+    # When the count comes back 0 that last evaluation answered no request:
+    # step k had left nothing pending, and its outputs are never read.
+    pend_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    done = torch.cuda.Event()
     while True:
       if time_steps:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -89,14 +96,17 @@ class ExternalEvaluatorSearch:
         e1.record(st)
         self.events.append((e0, e1))
       self.steps += 1
-      n = int(pending.item())  # synchronises the stream
-      if n == 0:
-        break
-      self.requests += n
       with torch.cuda.stream(st):
+        pend_host.copy_(pending, non_blocking=True)
+        done.record(st)
         pr, v = evaluator(obs, legal.bool(), kind)
         prior.copy_(pr)
         value.copy_(v)
+      done.synchronize()  # step k and its count, not the evaluation behind it
+      n = int(pend_host[0])
+      if n == 0:
+        break
+      self.requests += n
     o = E._alloc_outputs(R, self.eng.max_children)
     check(lib.os_az_fetch(self.eng._h, self.eng.max_children, *E._out_ptrs(o)))
     return o
