@@ -115,6 +115,11 @@ int os_engine_destroy(os_engine* e);
 #define OS_POLICY_CPP 0    /* mcts.cc: std::mt19937 bot + evaluator streams   */
 #define OS_POLICY_NUMPY 1  /* mcts.py: numpy RandomState (shared or separate) */
 
+/* Child selection (ChildSelectionPolicy, mcts.h:38-41).  PUCT with the
+ * built-in RandomRolloutEvaluator uses its uniform Prior (mcts.cc:73-86). */
+#define OS_SELECT_UCT 0
+#define OS_SELECT_PUCT 1
+
 typedef struct {
   double uct_c;                 /* MCTSBot uct_c */
   int32_t max_simulations;      /* MCTSBot max_simulations */
@@ -125,6 +130,10 @@ typedef struct {
   int32_t block_size;           /* OS_LAYOUT_LANE only: lanes per workgroup (0 = default) */
   int32_t layout;               /* OS_LAYOUT_WAVE (0), OS_LAYOUT_LANE, OS_LAYOUT_AUTO */
   int64_t arena_nodes;          /* 0 = exact worst case; else nodes per root */
+  int32_t child_selection;      /* OS_SELECT_UCT (mcts.cc:89-100) or OS_SELECT_PUCT
+                                   (mcts.cc:102-111; MCTSBot child_selection_policy,
+                                   mcts.h:152-159; mcts.py child_selection_fn) */
+  int32_t reserved;             /* 0 */
 } os_mcts_params;
 
 /* Batched independent searches: MCTSBot::MCTSearch (mcts.cc:325-428) on every

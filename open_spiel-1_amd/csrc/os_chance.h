@@ -128,13 +128,15 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
         for (int k = 0; k < nc; ++k)
           if (nodes[first + k].action == a) chosen = k;
       } else {
-        const double logN = sp.log_lut[nx.n];
+        const double logN = sp.log_lut[nx.n];  // sqrt(N) under PUCT
+        const double cprior = puct_prior_term(sp.uct_c, nc);
         double best = -inf;
         res.scanned += nc;
         for (int k = 0; k < nc; ++k) {
           const Node<R> c = nodes[first + k];
           double v;
           if (c.out != kUnsolved) v = outcome_for(c.out, cp);
+          else if (sp.puct) v = puct_unsolved(static_cast<double>(c.w), c.n, cprior, logN);
           else if (c.n == 0) v = inf;
           else v = static_cast<double>(c.w) / c.n + sp.uct_c * __builtin_sqrt(logN / c.n);
           if (v > best) {

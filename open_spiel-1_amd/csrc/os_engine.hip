@@ -141,6 +141,7 @@ DevArgs MakeArgs(os_engine* e) {
   const int64_t mn = (e->params.max_memory_mb << 20) / 80 + 1;
   a.sp.max_nodes = static_cast<int32_t>(mn);
   a.sp.policy = e->params.policy;
+  a.sp.puct = e->params.child_selection == OS_SELECT_PUCT ? 1 : 0;
   a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
   a.roots = e->d_roots.p;
   a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
@@ -199,7 +200,7 @@ bool ReplayRoot(const HostGame& g, const int64_t* a, int64_t n, HostState* s,
 
 
 
-int CheckParams(const os_engine* e, const os_mcts_params* p) {
+int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true) {
   if (!p) return Fail(OS_ERR_INVALID, "null params");
   if (p->max_simulations < 0) return Fail(OS_ERR_INVALID, "max_simulations < 0");
   if (p->n_rollouts < 1) return Fail(OS_ERR_INVALID, "n_rollouts must be >= 1");
@@ -218,6 +219,10 @@ int CheckParams(const os_engine* e, const os_mcts_params* p) {
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxPath");
   if (e->game.cfg.kind == kPig && p->layout == OS_LAYOUT_WAVE)
     return Fail(OS_ERR_UNSUPPORTED, "games with chance nodes run the lane layout only");
+  if (p->child_selection != OS_SELECT_UCT && p->child_selection != OS_SELECT_PUCT)
+    return Fail(OS_ERR_INVALID, "unknown child_selection");
+  if (search && e->game.cfg.kind == kGo && p->layout == OS_LAYOUT_LANE)
+    return Fail(OS_ERR_UNSUPPORTED, "go runs on the wave layout only (OS_LAYOUT_WAVE / AUTO)");
   return OS_OK;
 }
 
@@ -274,7 +279,7 @@ int SizeArena(os_engine* e, bool allow_paged) {
   const uint32_t pn = PageNodes(cfg.max_children);
   const auto& h = e->arena_hint;
   if (allow_paged && e->arena_mode == OS_ARENA_PAGED && p->layout == OS_LAYOUT_WAVE &&
-      p->policy == OS_POLICY_CPP &&
+      p->policy == OS_POLICY_CPP && p->child_selection == OS_SELECT_UCT &&
       !gc_possible && p->arena_nodes == 0 && R >= kPagedMinRoots &&
       h.sims == p->max_simulations && h.node_bytes == e->node_bytes && h.page_nodes == pn &&
       2 * static_cast<int64_t>(pn) <= worst) {
@@ -349,8 +354,8 @@ void UpdateArenaHint(os_engine* e) {
 // Uploads roots / seeds, sizes and allocates the arena and outputs.
 int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
             const int64_t* root_actions, const int64_t* root_offsets,
-            const uint32_t* bot_seeds, const uint32_t* eval_seeds) {
-  int rc = CheckParams(e, p);
+            const uint32_t* bot_seeds, const uint32_t* eval_seeds, bool search = true) {
+  int rc = CheckParams(e, p, search);
   if (rc) return rc;
   if (R < 0) return Fail(OS_ERR_INVALID, "num_roots < 0");
   HIP_TRY(hipSetDevice(e->device));
@@ -410,10 +415,13 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
                       hipMemcpyHostToDevice));
   }
-  // log(N) LUT from the host libm, N in [0, max_simulations] (UCTValue's
-  // std::log(parent_explore_count), mcts.cc:99).
+  // Parent-count LUT from the host libm, N in [0, max_simulations]: UCTValue's
+  // std::log(parent_explore_count) (mcts.cc:99), or PUCTValue's
+  // std::sqrt(parent_explore_count) (mcts.cc:109).
   std::vector<double> lut(static_cast<size_t>(p->max_simulations) + 2);
-  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  const bool puct = p->child_selection == OS_SELECT_PUCT;
+  for (size_t i = 0; i < lut.size(); ++i)
+    lut[i] = puct ? std::sqrt(static_cast<double>(i)) : std::log(static_cast<double>(i));
   if ((rc = e->d_lut.ensure(lut.size() * 8))) return rc;
   HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice));
   // Work buffers.
@@ -556,6 +564,8 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
   if (rc) return rc;
   if (p->policy != OS_POLICY_CPP)
     return Fail(OS_ERR_UNSUPPORTED, "self-play implements the C++ MCTSBot policy only");
+  if (p->child_selection != OS_SELECT_UCT)
+    return Fail(OS_ERR_UNSUPPORTED, "self-play with the random-rollout evaluator runs UCT");
   if (G < 0 || max_len < 0) return Fail(OS_ERR_INVALID, "negative size");
   if (G > 0 && (!bot_seeds || !eval_seeds || !start_offsets))
     return Fail(OS_ERR_INVALID, "null argument");
@@ -701,8 +711,10 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     return Fail(OS_ERR_INVALID, "null request / response buffer");
   os_mcts_params q = *p;
   q.n_rollouts = 2;  // f64 node rewards (Node<double>): values are not integral
+  q.child_selection = OS_SELECT_UCT;  // `puct` selects; the LUT stays log(N)
   q.layout = OS_LAYOUT_LANE;
-  int rc = Prepare(e, &q, R, root_actions, root_offsets, bot_seeds, bot_seeds);
+  int rc = Prepare(e, &q, R, root_actions, root_offsets, bot_seeds, bot_seeds,
+                   /*search=*/false);  // buffers only: k_az_step runs the search
   if (rc) return rc;
   if (e->chunk_roots < R)
     return Fail(OS_ERR_CAPACITY, "external-evaluator searches must all fit in HBM at once");
@@ -1457,6 +1469,24 @@ int os_root_parallel(os_engine* const* engines, int32_t ndev, const os_mcts_para
     HIP_TRY(hipDeviceSynchronize());
     std::vector<SearchResult> res(T);
     HIP_TRY(hipMemcpy(res.data(), e->d_res.p, T * sizeof(SearchResult), hipMemcpyDeviceToHost));
+    if (e->paged) {
+      // As os_engine_fetch: a paged batch that ran out of pool pages is rerun
+      // on the reserved arena (same seeds, same trees) and summed again.
+      int64_t over = 0;
+      for (const SearchResult& s : res) over += s.status == kArenaOverflow;
+      if (over) {
+        e->arena_overflows += over;
+        e->arena_reruns += 1;
+        e->last_results.resize(T);
+        if ((rc = RerunReserved(e))) return rc;
+        res = e->last_results;
+        int64_t* dn = static_cast<int64_t*>(e->d_rp_sum.p);
+        if ((rc = os_engine_root_sums_async(e, num_actions, dn,
+                                            reinterpret_cast<double*>(dn + A), nullptr)))
+          return rc;
+        HIP_TRY(hipDeviceSynchronize());
+      }
+    }
     for (int64_t t = 0; t < T; ++t) {
       if (res[t].status != kOk)
         return Fail(OS_ERR_CAPACITY, "engine " + std::to_string(g) + " tree " +

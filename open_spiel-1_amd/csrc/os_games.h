@@ -523,9 +523,20 @@ struct GoCtx {
     if (base_filt.has(fbit(h)))
       for (int i = 0; i < n_base; ++i)
         if (base[i] == h) return true;
+#if OS_DEBUG_GOLOG
+    int steps = 0;
+#endif
     for (int e = head[stones * head_stride]; e;
-         e = static_cast<int>(link[static_cast<int64_t>(e - 1) * stride] & 0xFFFFu))
+         e = static_cast<int>(link[static_cast<int64_t>(e - 1) * stride] & 0xFFFFu)) {
+#if OS_DEBUG_GOLOG
+      if (++steps > cap + 2) {
+        printf("golog cycle: stones %d head %d e %d n_log %d link %x\n", stones,
+               head[stones * head_stride], e, n_log, link[static_cast<int64_t>(e - 1) * stride]);
+        return false;
+      }
+#endif
       if (log[static_cast<int64_t>(e - 1) * stride] == h) return true;
+    }
     return false;
   }
   // Log position count, and dropping back to it (each rollout of a leaf

@@ -249,10 +249,13 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
       *unsupported = true;
       return "go board_size must be in [2, 19] for this engine";
     }
-    if (handicap >= 2) {
-      *unsupported = true;
-      return "go handicap stones (19x19 placement) are not supported by this engine";
-    }
+    // Handicap stones sit on 19 x 19 star points (go.cc:56-78): every one must
+    // be on the board, where GoBoard::PlayMove's SPIEL_CHECK_EQ(kEmpty, ...)
+    // (go_board.cc:263) would otherwise fail.
+    for (int p : GoHandicapStones(handicap, 19))
+      if (p / 19 >= n || p % 19 >= n)
+        return "go handicap " + std::to_string(handicap) + " places a stone off the " +
+               std::to_string(n) + "x" + std::to_string(n) + " board";
     c.kind = kGo;
     c.rows = c.cols = n;
     c.num_actions = n * n + 1;
@@ -346,6 +349,19 @@ GoCtx HostGoCtx(const HostState& s, HostGoLog* buf) {
   return ctx;
 }
 
+std::vector<int> GoHandicapStones(int handicap, int n) {
+  // go.cc:56-78 HandicapStones: d4 q16 d16 q4 d10 q10 k4 k16 k10 as (row, col),
+  // the centre k10 replacing the last stone of an odd count >= 5; none unless
+  // 2 <= handicap <= 9.
+  static const int kRC[9][2] = {{3, 3}, {15, 15}, {15, 3}, {3, 15}, {9, 3},
+                                {9, 15}, {3, 9}, {15, 9}, {9, 9}};
+  std::vector<int> pts;
+  if (handicap < 2 || handicap > 9) return pts;
+  for (int i = 0; i < handicap; ++i) pts.push_back(kRC[i][0] * n + kRC[i][1]);
+  if (handicap >= 5 && handicap % 2 == 1) pts[handicap - 1] = 9 * n + 9;
+  return pts;
+}
+
 void StateInit(HostState* s) {
   std::memset(s->raw, 0, sizeof s->raw);
   s->history.clear();
@@ -354,7 +370,26 @@ void StateInit(HostState* s) {
   WithGame(g, [&](auto tag) {
     using G = decltype(tag);
     G::init(St<G>(*s), g);
-    if constexpr (kIsGo<G>) s->hashes.push_back(St<G>(*s).hash);  // go.cc:218-224
+    if constexpr (kIsGo<G>) {
+      // GoState::ResetBoard (go.cc:211-225): black plays the handicap stones,
+      // then white is to move (for any handicap >= 2, even one above 9 that
+      // places none); the history stays empty and the repetition set holds
+      // only the resulting position.
+      typename G::State& st = St<G>(*s);
+      if (g.handicap >= 2) {
+        for (int p : GoHandicapStones(g.handicap, g.rows)) {
+          HostGoLog buf;
+          GoCtx ctx = HostGoCtx(*s, &buf);
+          st.to_play = 0;
+          G::apply(st, g, ctx, p);
+        }
+        st.to_play = 1;
+        st.moves = 0;
+        st.flags = 0;
+        st.ko = -1;
+      }
+      s->hashes.push_back(st.hash);  // go.cc:218-224
+    }
   });
 }
 

@@ -66,6 +66,10 @@ int64_t DirichletNoise(uint32_t seed, int count, double alpha, double* out);
 // supported by this engine.
 std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported);
 
+// go.cc:56-78 HandicapStones(handicap) as cell indices row * n + col (empty
+// unless 2 <= handicap <= 9).
+std::vector<int> GoHandicapStones(int handicap, int n);
+
 void StateInit(HostState* s);
 bool StateTerminal(const HostState& s);
 int StateCurrentPlayer(const HostState& s);

@@ -194,7 +194,7 @@ struct WaveOcc<Hex> {
 // kPaged: the search may take pages from the pool (os_wave.h kPg*).  The
 // reserved-arena variant is a separate kernel: the cold page-switch path
 // costs the selection loop scalar registers (C2 +1.4% time).
-template <class G, class R, int Policy, bool kPaged>
+template <class G, class R, int Policy, bool kPaged, bool kPuct>
 __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int64_t lr = blockIdx.x;
   if (lr >= a.num_roots) return;
@@ -235,10 +235,10 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   PhaseCycles ph = {};  // paged: the root's page is page lr = blockIdx.x
   SearchResult res = shared
-      ? wave_search<G, R, Policy, kPaged>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
-                                               path, a.path_cap, ph)
-      : wave_search<G, R, Policy, kPaged>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
-                                               path, a.path_cap, ph);
+      ? wave_search<G, R, Policy, kPaged, kPuct>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot,
+                                                 bot, path, a.path_cap, ph)
+      : wave_search<G, R, Policy, kPaged, kPuct>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot,
+                                                 ev, path, a.path_cap, ph);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
   ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);
@@ -646,19 +646,28 @@ int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   constexpr bool kCanPage = Policy == kPolicyCpp;
   const bool paged = kCanPage && a.pages != nullptr;
   if (a.pages && !kCanPage) return Fail(OS_ERR_UNSUPPORTED, "paged arena needs the C++ policy");
-  const void* kfn = paged ? reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, kCanPage>)
-                          : reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, false>);
+  // PUCT searches run on the reserved arena only (SizeArena); their kernel
+  // is a third instantiation, so the UCT kernels keep their registers.
+  const bool puct = a.sp.puct != 0;
+  if (puct && paged) return Fail(OS_ERR_UNSUPPORTED, "paged arena with PUCT");
+  const void* kfn =
+      puct ? reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, false, true>)
+           : (paged ? reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, kCanPage, false>)
+                    : reinterpret_cast<const void*>(&k_wsearch<G, R, Policy, false, false>));
   HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds)));
   for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
     a.root_base = base;
     a.num_roots = n;
-    if (paged)
-      hipLaunchKernelGGL((k_wsearch<G, R, Policy, kCanPage>), dim3(static_cast<unsigned>(n)),
+    if (puct)
+      hipLaunchKernelGGL((k_wsearch<G, R, Policy, false, true>), dim3(static_cast<unsigned>(n)),
                          dim3(64), lds, stream, a);
+    else if (paged)
+      hipLaunchKernelGGL((k_wsearch<G, R, Policy, kCanPage, false>),
+                         dim3(static_cast<unsigned>(n)), dim3(64), lds, stream, a);
     else
-      hipLaunchKernelGGL((k_wsearch<G, R, Policy, false>), dim3(static_cast<unsigned>(n)),
+      hipLaunchKernelGGL((k_wsearch<G, R, Policy, false, false>), dim3(static_cast<unsigned>(n)),
                          dim3(64), lds, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess)
@@ -677,6 +686,15 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   } else {
     if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
   }
+  if constexpr (G::State::kNeedsLog) {
+    // Go searches run one wave per search only.  A lane-per-search go search
+    // keeps its superko log in private memory (4.6 KB of scratch per lane,
+    // ~2700 spilled registers) and hung on MI355X with f64 rewards
+    // (n_rollouts > 1) while the host build of the same code is clean under
+    // ASan/UBSan: it is not built.
+    (void)stream;
+    return Fail(OS_ERR_UNSUPPORTED, "go runs on the wave layout only (OS_LAYOUT_WAVE / AUTO)");
+  } else {
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
   const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
   if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
@@ -697,6 +715,7 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
                                      hipGetErrorString(err));
   }
   return OS_OK;
+  }
 }
 
 template <class G>

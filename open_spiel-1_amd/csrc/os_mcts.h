@@ -54,9 +54,23 @@ struct SearchParams {
   int32_t solve;
   int32_t max_nodes;        // (max_memory_mb << 20) / sizeof(SearchNode) + 1
   int32_t policy;           // kPolicyCpp / kPolicyNumpy
-  int32_t pad;
-  const double* log_lut;    // log(N), N in [0, max_simulations], host libm
+  int32_t puct;             // 0 UCTValue (mcts.cc:89-100), 1 PUCTValue (:102-111)
+  // Parent term of the child value, N in [0, max_simulations], host libm:
+  // log(N) under UCT, sqrt(N) under PUCT.
+  const double* log_lut;
 };
+
+// SearchNode::PUCTValue (mcts.cc:102-111; mcts.py:135-142) of an unsolved
+// child with the uniform prior 1 / nchild of RandomRolloutEvaluator::Prior
+// (mcts.cc:73-86): cprior = uct_c * prior, sqrtN = sqrt(parent explore count).
+// The reference's operation order: Q + ((uct_c * prior) * sqrt(N)) / (n + 1).
+OS_HD double puct_prior_term(double uct_c, int nchild) {
+  return uct_c * (1.0 / static_cast<double>(nchild));
+}
+OS_HD double puct_unsolved(double w, int32_t n, double cprior, double sqrtN) {
+  const double q = n != 0 ? w / static_cast<double>(n) : 0.0;
+  return q + cprior * sqrtN / static_cast<double>(n + 1);
+}
 
 struct SearchResult {
   int32_t status;
@@ -260,7 +274,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         c_w = 0;
       } else {
         const int cp = P0 ^ (depth & 1);  // player choosing at this node
-        const double logN = sp.log_lut[cur_n];
+        const double logN = sp.log_lut[cur_n];  // sqrt(N) under PUCT
+        const double cprior = puct_prior_term(sp.uct_c, cur_nc);
         double best = -inf;
         chosen = 0;
         res.scanned += cur_nc;
@@ -270,6 +285,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
           double v;
           if (c.out != kUnsolved) {
             v = outcome_for(c.out, cp);
+          } else if (sp.puct) {
+            v = puct_unsolved(static_cast<double>(c.w), c.n, cprior, logN);
           } else if (c.n == 0) {
             v = inf;
           } else {

@@ -710,6 +710,15 @@ __device__ __forceinline__ double uct_value_sel(const Node<R>& c, bool in, int c
   v = c.out != kUnsolved ? o : v;
   return in ? v : -__builtin_huge_val();
 }
+// SearchNode::PUCTValue (mcts.cc:102-111) with the uniform prior, likewise
+// selected on every lane.
+template <class R>
+__device__ __forceinline__ double puct_value_sel(const Node<R>& c, bool in, int cp,
+                                                 double sqrtN, double cprior) {
+  double v = puct_unsolved(static_cast<double>(c.w), c.n, cprior, sqrtN);
+  v = c.out != kUnsolved ? outcome_for(c.out, cp) : v;
+  return in ? v : -__builtin_huge_val();
+}
 
 // Inclusive prefix (OR / sum) over the 16 lanes of each DPP row; lanes that
 // would read across the row boundary read 0 (bound_ctrl), the identity.
@@ -1334,8 +1343,9 @@ struct LanePath {
 };
 
 // One search, executed by the whole wave.  `path` (LDS) has path_cap
-// entries.  Same contract as mcts_search.
-template <class G, class R, int Policy, bool kPageable = false, class C>
+// entries.  Same contract as mcts_search; kPuct selects children by
+// PUCTValue (sp.log_lut then holds sqrt(N)).
+template <class G, class R, int Policy, bool kPageable = false, bool kPuct = false, class C>
 __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     const typename G::State& root, C& ctx,
                                     Node<R>* nodes, uint32_t cap, WaveMt& bot,
@@ -1549,6 +1559,15 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             lg1 = sp.log_lut[c1.n];
           }
         }
+        if constexpr (kPuct) {
+          // PUCTValue (mcts.cc:102-111): unvisited children are not +inf, so
+          // every child is scored in f64 (cur_logN holds sqrt(N) here).
+          const double cprior = puct_prior_term(sp.uct_c, cur_nc);
+          const double v0 = puct_value_sel(c0, in0, cp, cur_logN, cprior);
+          const double v1 =
+              WW::kTwoSlots ? puct_value_sel(c1, in1, cp, cur_logN, cprior) : -inf;
+          chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
+        } else {
         // An unvisited unsolved child scores +inf, above every finite UCT
         // value and solver outcome, so the first one in index order wins the
         // strict '>' scan outright: one ballot instead of the f64 UCT values
@@ -1566,7 +1585,8 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                                                   cur_logN, sp.uct_c);
 #endif
         }
-        if (chosen < 0) {
+        }
+        if (!kPuct && chosen < 0) {
           const double v0 = uct_value_sel(c0, in0, cp, cur_logN, sp.uct_c);
           const double v1 = WW::kTwoSlots ? uct_value_sel(c1, in1, cp, cur_logN, sp.uct_c) : -inf;
           chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);

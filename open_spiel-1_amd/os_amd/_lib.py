@@ -22,6 +22,9 @@ OS_ERR_CAPACITY = -4
 POLICY_CPP = 0
 POLICY_NUMPY = 1
 
+SELECT_UCT = 0
+SELECT_PUCT = 1
+
 LAYOUT_WAVE = 0
 LAYOUT_LANE = 1
 LAYOUT_AUTO = 2
@@ -77,7 +80,8 @@ class GameInfo(ctypes.Structure):
 class MctsParams(ctypes.Structure):
   _fields_ = [("uct_c", _dbl), ("max_simulations", _i32), ("n_rollouts", _i32),
               ("max_memory_mb", _i64), ("solve", _i32), ("policy", _i32),
-              ("block_size", _i32), ("layout", _i32), ("arena_nodes", _i64)]
+              ("block_size", _i32), ("layout", _i32), ("arena_nodes", _i64),
+              ("child_selection", _i32), ("reserved", _i32)]
 
 
 def _sig(name, restype, argtypes):

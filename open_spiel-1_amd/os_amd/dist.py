@@ -155,7 +155,11 @@ class HipBackend:
     self.eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
 
   def run_root_parallel(self):
-    """Launches the T searches + the action-indexed reduction (async)."""
+    """Launches the T searches + the action-indexed reduction (async).
+
+    The sums are those of the launched run: if it is a paged batch that runs
+    out of pool pages, `fetch` reruns it on the reserved arena and the sums
+    must be taken again (`root_sums` does; see os_engine_arena_info)."""
     torch = self.torch
     st = self._stream()
     self.eng.run_async(st)
@@ -166,9 +170,22 @@ class HipBackend:
 
   def root_sums(self, history, bot_seeds, eval_seeds, **params):
     self.prepare_root_parallel(history, bot_seeds, eval_seeds, **params)
+    reruns = self._reruns()
     v, w = self.run_root_parallel()
     self.eng.fetch()  # synchronises and raises on any per-tree failure
+    if self._reruns() != reruns:
+      # A paged batch ran out of pool pages: the fetch reran it on the reserved
+      # arena (same seeds, full searches), so the sums queued above belong to
+      # the overflowed run.  Sum the rerun's children instead.
+      st = self._stream()
+      self.eng.root_sums_async(self.num_actions, v.data_ptr(), w.data_ptr(), st)
+      if self.device.type == "cuda":
+        self.torch.cuda.current_stream(self.device).synchronize()
     return v, w
+
+  def _reruns(self):
+    arena_info = getattr(self.eng, "arena_info", None)
+    return arena_info()["reruns"] if arena_info else 0
 
   def prepare_playouts(self, history, seeds, n_rollouts=1):
     self.eng.rollouts_prepare(history, seeds, n_rollouts)

@@ -21,8 +21,10 @@ UNSOLVED = 2
 
 def make_params(uct_c=2.0, max_simulations=1000, n_rollouts=1,
                 max_memory_mb=1000, solve=True, policy=_lib.POLICY_CPP,
-                block_size=0, arena_nodes=0, layout=_lib.LAYOUT_AUTO):
+                block_size=0, arena_nodes=0, layout=_lib.LAYOUT_AUTO,
+                child_selection=_lib.SELECT_UCT):
   p = _lib.MctsParams()
+  p.child_selection = int(child_selection)
   p.layout = int(layout)
   p.uct_c = float(uct_c)
   p.max_simulations = int(max_simulations)
@@ -333,6 +335,8 @@ def root_parallel(engines, root_actions, trees_per_device, seed_base=0, **params
   check(lib.os_root_parallel(ctypes.cast(hs, ctypes.c_void_p), len(engines), ctypes.byref(p),
                              ptr(acts), len(acts), int(trees_per_device), int(seed_base), A,
                              ptr(visits), ptr(rewards), ptr(sims)))
+  for e in engines:  # each engine now holds a prepared batch of T trees (fetchable)
+    e._prep_R = int(trees_per_device)
   return visits, rewards, int(sims[0])
 
 

@@ -4,18 +4,21 @@ Public names and signatures follow the reference module (Evaluator :29-43,
 RandomRolloutEvaluator :46-82, SearchNode :85-196, MCTSBot :199-443).
 
 `MCTSBot.mcts_search` runs on the MI355X whenever the search is the hot path
-the engine implements — a `RandomRolloutEvaluator`, UCT child selection, no
-Dirichlet noise, one of the supported games (the five, and pig with its chance
-nodes) — continuing the bot's and
+the engine implements — a `RandomRolloutEvaluator`, UCT or PUCT child
+selection (`SearchNode.uct_value` / `SearchNode.puct_value`), no Dirichlet
+noise, one of the supported games (the five, and pig with its chance nodes) —
+continuing the bot's and
 the evaluator's `np.random.RandomState` streams in place, bit-exact with the
 reference module (one shared RandomState, as in mcts_test.py:41-54, or two).
 Searches the engine does not implement (user evaluators, custom
 `child_selection_fn`, Dirichlet noise, hex / go boards above 11 x 11) run the
-generic host loop below; pass `backend="hip"` to forbid that and fail loudly
-instead.
+generic host loop below with a RuntimeWarning under `backend="auto"`; pass
+`backend="hip"` to forbid that and fail loudly instead, or `backend="host"` to
+choose it.
 """
 import math
 import time
+import warnings
 
 import numpy as np
 
@@ -194,12 +197,13 @@ class MCTSBot(pyspiel.Bot):
     self._child_selection_fn = child_selection_fn
     self.backend = backend
     if backend == "hip" and not self._gpu_eligible():
-      raise ValueError("backend='hip' needs RandomRolloutEvaluator, UCT child "
-                       "selection, no Dirichlet noise and a supported game")
+      raise ValueError("backend='hip' needs RandomRolloutEvaluator, UCT or PUCT "
+                       "child selection, no Dirichlet noise and a supported game")
+    self._warned_host = False
 
   def _gpu_eligible(self):
     return (type(self.evaluator) is RandomRolloutEvaluator and
-            self._child_selection_fn is SearchNode.uct_value and
+            self._child_selection_fn in (SearchNode.uct_value, SearchNode.puct_value) and
             not self._dirichlet_noise and
             isinstance(self._game, pyspiel.Game) and self._game.on_device())
 
@@ -236,6 +240,14 @@ class MCTSBot(pyspiel.Bot):
                                         self._gpu_eligible())
     if use_gpu:
       return self._search_gpu(state)
+    if self.backend == "auto" and not self._warned_host:
+      # Never a silent CPU search: say once why this bot runs on the host.
+      warnings.warn("MCTSBot(backend='auto') runs this search on the host CPU (the "
+                    "GPU engine needs RandomRolloutEvaluator, UCT or PUCT selection, "
+                    "no Dirichlet noise and a game it runs on the device); pass "
+                    "backend='host' to silence this or backend='hip' to make it an "
+                    "error", RuntimeWarning, stacklevel=2)
+      self._warned_host = True
     return self._search_host(state)
 
   # ---- GPU path -------------------------------------------------------------
@@ -250,7 +262,9 @@ class MCTSBot(pyspiel.Bot):
         state.history(), (b[1], b[2]), None if shared else (e[1], e[2]),
         uct_c=self.uct_c, max_simulations=self.max_simulations,
         n_rollouts=self.evaluator.n_rollouts, solve=self.solve,
-        max_memory_mb=0, policy=_lib.POLICY_NUMPY)
+        max_memory_mb=0, policy=_lib.POLICY_NUMPY,
+        child_selection=(_lib.SELECT_PUCT if self._child_selection_fn is SearchNode.puct_value
+                         else _lib.SELECT_UCT))
     bot_rs.set_state(("MT19937", nb[0], nb[1], b[3], b[4]))
     if not shared:
       ev_rs.set_state(("MT19937", ne[0], ne[1], e[3], e[4]))

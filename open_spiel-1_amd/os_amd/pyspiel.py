@@ -146,7 +146,7 @@ class Game:
 
   def max_chance_outcomes(self):
     # pig.h:88: diceoutcomes (the largest chance branching); 0 for the others
-    return self._info.max_children if self._info.kind == _PIG else 0
+    return self._pig_dice() if self._info.kind == _PIG else 0
 
   def num_players(self):
     return 2
@@ -286,9 +286,12 @@ class State:
   def legal_actions(self, player=None):
     if player is not None and player != self.current_player():
       return []
-    cap = self._game._info.num_distinct_actions
+    cap = max(self._game._info.num_distinct_actions, self._game._info.max_children)
     buf = np.zeros(cap, np.int64)
     n = lib.os_state_legal_actions(self._h, buf.ctypes.data, cap)
+    if n > cap:  # chance outcomes can outnumber the distinct actions (pig)
+      buf = np.zeros(n, np.int64)
+      n = lib.os_state_legal_actions(self._h, buf.ctypes.data, n)
     return [int(a) for a in buf[:n]]
 
   def legal_actions_mask(self, player=None):
@@ -362,10 +365,14 @@ class State:
   def chance_outcomes(self):
     """ChanceOutcomes() (spiel.h:322-327): [(action, probability)] in outcome
     order; [] at a decision node."""
-    cap = self._game._info.num_distinct_actions
+    cap = max(self._game._info.num_distinct_actions, self._game._info.max_children)
     acts = np.zeros(cap, np.int64)
     probs = np.zeros(cap, np.float64)
     n = lib.os_state_chance_outcomes(self._h, acts.ctypes.data, probs.ctypes.data, cap)
+    if n > cap:
+      acts = np.zeros(n, np.int64)
+      probs = np.zeros(n, np.float64)
+      n = lib.os_state_chance_outcomes(self._h, acts.ctypes.data, probs.ctypes.data, n)
     return [(int(acts[i]), float(probs[i])) for i in range(n)]
 
   def num_distinct_actions(self):
@@ -489,8 +496,8 @@ class MCTSBot(Bot):
     if not isinstance(evaluator, RandomRolloutEvaluator):
       raise ValueError("the GPU MCTSBot supports RandomRolloutEvaluator only "
                        "(pyspiel.Evaluator has no Python trampoline either)")
-    if child_selection_policy != ChildSelectionPolicy.UCT:
-      raise ValueError("PUCT child selection is not supported by this engine")
+    if child_selection_policy not in (ChildSelectionPolicy.UCT, ChildSelectionPolicy.PUCT):
+      raise ValueError("unknown child_selection_policy")
     gt = game.get_type()
     if gt.reward_model != GameType.RewardModel.TERMINAL:
       raise SpielError("Game must have terminal rewards.")
@@ -504,6 +511,8 @@ class MCTSBot(Bot):
     self.solve = bool(solve)
     self.verbose = bool(verbose)
     self._state = _mt_key(seed)
+    self._select = (_lib.SELECT_PUCT if child_selection_policy == ChildSelectionPolicy.PUCT
+                    else _lib.SELECT_UCT)
 
   def mcts_search(self, state):
     from .mcts import SearchNode, tree_to_search_nodes
@@ -512,7 +521,7 @@ class MCTSBot(Bot):
         state.history(), self._state, self._evaluator._state,
         uct_c=self.uct_c, max_simulations=self.max_simulations,
         n_rollouts=self._evaluator.n_rollouts, max_memory_mb=self.max_memory_mb,
-        solve=self.solve, policy=_lib.POLICY_CPP)
+        solve=self.solve, policy=_lib.POLICY_CPP, child_selection=self._select)
     del o, SearchNode
     return tree_to_search_nodes(eng.tree(0), state, self._game, root_action=-1)
 

@@ -194,7 +194,8 @@ int oref_rollouts(void* g, const int64_t* actions, int64_t n_actions,
 
 // Batched independent searches (the C++ MCTSBot path, mcts.cc), one bot +
 // one RandomRolloutEvaluator per root, `threads` host threads with static
-// round-robin root assignment.  Writes child-ordered outputs.
+// round-robin root assignment; puct != 0: ChildSelectionPolicy::PUCT.  Writes
+// child-ordered outputs.
 int oref_mcts_batch(void* g, int64_t num_roots, const int64_t* root_actions,
                     const int64_t* root_offsets, double uct_c,
                     int32_t max_simulations, int32_t n_rollouts,
@@ -204,7 +205,7 @@ int oref_mcts_batch(void* g, int64_t num_roots, const int64_t* root_actions,
                     int32_t* child_n, double* child_w, int8_t* child_out,
                     int32_t* nchild, int32_t* root_n, double* root_w,
                     int8_t* root_out, int64_t* best_action, int32_t* nodes,
-                    int32_t threads) {
+                    int32_t threads, int32_t puct) {
   auto* og = static_cast<OGame*>(g);
   RootOut o{child_action, child_n, child_w, child_out, nchild,
             root_n,       root_w,  root_out, best_action, nodes};
@@ -215,7 +216,7 @@ int oref_mcts_batch(void* g, int64_t num_roots, const int64_t* root_actions,
                           root_offsets[r + 1] - root_offsets[r]);
       RandomRolloutEvaluator ev(n_rollouts, eval_seeds[r]);
       MCTSBot bot(*og->game, &ev, uct_c, max_simulations, max_memory_mb,
-                  solve != 0, bot_seeds[r]);
+                  solve != 0, bot_seeds[r], puct != 0);
       SearchStats st;
       auto root = bot.MCTSearch(*state, &st);
       FillOut(*root, max_children, r, st, o);
@@ -231,19 +232,20 @@ int oref_mcts_batch(void* g, int64_t num_roots, const int64_t* root_actions,
   return 0;
 }
 
-// The Python mcts.py path with one shared numpy RandomState(seed).
+// The Python mcts.py path with one shared numpy RandomState(seed);
+// puct != 0: child_selection_fn = SearchNode.puct_value (mcts.py:135-142).
 int oref_mcts_numpy(void* g, const int64_t* actions, int64_t n_actions,
                     double uct_c, int32_t max_simulations, int32_t n_rollouts,
                     int32_t solve, uint32_t seed, int32_t max_children,
                     int32_t* child_action, int32_t* child_n, double* child_w,
                     int8_t* child_out, int32_t* nchild, int32_t* root_n,
                     double* root_w, int8_t* root_out, int64_t* best_action,
-                    int32_t* nodes, uint32_t* rng_state_out) {
+                    int32_t* nodes, uint32_t* rng_state_out, int32_t puct) {
   auto* og = static_cast<OGame*>(g);
   auto state = Replay(*og->game, actions, n_actions);
   std::mt19937 rng(seed);
   NumpyMCTSBot bot(*og->game, &rng, uct_c, max_simulations, n_rollouts,
-                   solve != 0);
+                   solve != 0, puct != 0);
   SearchStats st;
   auto root = bot.Search(*state, &st);
   RootOut o{child_action, child_n, child_w, child_out, nchild,

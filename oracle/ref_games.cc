@@ -891,12 +891,13 @@ class State : public RState {
   void Reset() {
     board_.Clear();
     to_play_ = kBlack;
-    if (handicap_ >= 2 && handicap_ <= 9) {
+    if (handicap_ >= 2) {  // go.cc:211-217 (HandicapStones is empty above 9)
       static const char* kPlace[9] = {"d4", "q16", "d16", "q4", "d10",
                                       "q10", "k4", "k16", "k10"};
       std::vector<uint16_t> pts;
-      for (int i = 0; i < handicap_; ++i) pts.push_back(MakePoint(kPlace[i]));
-      if (handicap_ >= 5 && handicap_ % 2 == 1) pts[handicap_ - 1] = MakePoint("k10");
+      for (int i = 0; i < handicap_ && handicap_ <= 9; ++i) pts.push_back(MakePoint(kPlace[i]));
+      if (handicap_ <= 9 && handicap_ >= 5 && handicap_ % 2 == 1)
+        pts[handicap_ - 1] = MakePoint("k10");
       for (uint16_t p : pts) board_.Play(p, kBlack);
       to_play_ = kWhite;
     }

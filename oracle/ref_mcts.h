@@ -320,9 +320,9 @@ class MCTSBot {
 class NumpyMCTSBot {
  public:
   NumpyMCTSBot(const RGame& game, std::mt19937* rng, double uct_c,
-               int max_simulations, int n_rollouts, bool solve)
+               int max_simulations, int n_rollouts, bool solve, bool puct = false)
       : uct_c_(uct_c), max_simulations_(max_simulations),
-        n_rollouts_(n_rollouts), solve_(solve),
+        n_rollouts_(n_rollouts), solve_(solve), puct_(puct),
         max_utility_(game.MaxUtility()), rng_(rng) {}
 
   std::unique_ptr<SearchNode> Search(const RState& state, SearchStats* st) {
@@ -362,7 +362,10 @@ class NumpyMCTSBot {
         } else {
           double max_value = -std::numeric_limits<double>::infinity();
           for (SearchNode& child : cur->children) {
-            double val = child.UCTValue(cur->explore_count, uct_c_);
+            // mcts.py:312-314: max() over child_selection_fn (uct_value or
+            // puct_value, mcts.py:124-142; the same arithmetic as mcts.cc).
+            double val = puct_ ? child.PUCTValue(cur->explore_count, uct_c_)
+                               : child.UCTValue(cur->explore_count, uct_c_);
             if (chosen == nullptr || val > max_value) {
               max_value = val;
               chosen = &child;
@@ -455,6 +458,7 @@ class NumpyMCTSBot {
   int max_simulations_;
   int n_rollouts_;
   bool solve_;
+  bool puct_;
   double max_utility_;
   std::mt19937* rng_;
 };

@@ -114,8 +114,12 @@ int hc_mcts_batch(const char* game_string, int64_t num_roots,
     g_err = err;
     return -1;
   }
+  // policy bit 8: PUCT child selection (the LUT then holds sqrt(N)).
+  const bool puct = (policy >> 8) & 1;
+  policy &= 0xff;
   std::vector<double> lut(max_simulations + 2);
-  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  for (size_t i = 0; i < lut.size(); ++i)
+    lut[i] = puct ? std::sqrt(static_cast<double>(i)) : std::log(static_cast<double>(i));
   SearchParams sp;
   std::memset(&sp, 0, sizeof sp);
   sp.uct_c = uct_c;
@@ -124,6 +128,7 @@ int hc_mcts_batch(const char* game_string, int64_t num_roots,
   sp.solve = solve;
   sp.max_nodes = static_cast<int32_t>((max_memory_mb << 20) / 80 + 1);
   sp.policy = policy;
+  sp.puct = puct ? 1 : 0;
   sp.log_lut = lut.data();
   const uint32_t cap = 1 + static_cast<uint32_t>(max_simulations) * game.cfg.max_children +
                        static_cast<uint32_t>(GcStackReserve(game.cfg.max_children));

@@ -44,7 +44,7 @@ KEYS = ("child_action", "child_n", "child_w", "child_out", "nchild", "root_n",
 
 def mcts_batch(game_string, acts, offs, bot_seeds, eval_seeds, max_children,
                uct_c=2.0, max_simulations=1000, n_rollouts=1, max_memory_mb=1000,
-               solve=True, policy=0):
+               solve=True, policy=0, puct=False):
   R = len(offs) - 1
   mc = max_children
   o = dict(child_action=np.zeros((R, mc), np.int32),
@@ -63,7 +63,8 @@ def mcts_batch(game_string, acts, offs, bot_seeds, eval_seeds, max_children,
   es = np.ascontiguousarray(eval_seeds, np.uint32)
   rc = lib().hc_mcts_batch(game_string.encode(), R, acts.ctypes.data,
                            offs.ctypes.data, uct_c, max_simulations, n_rollouts,
-                           max_memory_mb, int(solve), policy, bs.ctypes.data,
+                           max_memory_mb, int(solve), policy | (256 if puct else 0),
+                           bs.ctypes.data,
                            es.ctypes.data, mc, *[o[k].ctypes.data for k in KEYS])
   if rc:
     raise RuntimeError(lib().hc_last_error().decode())

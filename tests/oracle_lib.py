@@ -55,11 +55,12 @@ def lib():
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
         _u32p, ctypes.c_int32, _i32p, _i32p, _f64p, _i8p, _i32p, _i32p, _f64p,
-        _i8p, _i64p, _i32p, ctypes.c_int32]
+        _i8p, _i64p, _i32p, ctypes.c_int32, ctypes.c_int32]
     L.oref_mcts_numpy.argtypes = [
         ctypes.c_void_p, _i64p, ctypes.c_int64, ctypes.c_double, ctypes.c_int32,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, _i32p,
-        _i32p, _f64p, _i8p, _i32p, _i32p, _f64p, _i8p, _i64p, _i32p, _u32p]
+        _i32p, _f64p, _i8p, _i32p, _i32p, _f64p, _i8p, _i64p, _i32p, _u32p,
+        ctypes.c_int32]
     L.oref_mt19937.argtypes = [ctypes.c_uint32, ctypes.c_int64, _u32p]
     L.oref_mt19937_64.argtypes = [ctypes.c_uint64, ctypes.c_int64, _u64p]
     L.oref_absl_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint64,
@@ -120,7 +121,8 @@ class Game:
 
   def mcts_batch(self, root_actions, root_offsets, bot_seeds, eval_seeds,
                  uct_c=2.0, max_simulations=1000, n_rollouts=1,
-                 max_memory_mb=1000, solve=True, max_children=None, threads=1):
+                 max_memory_mb=1000, solve=True, max_children=None, threads=1,
+                 puct=False):
     R = len(root_offsets) - 1
     mc = max_children or self.num_distinct_actions
     out = dict(
@@ -142,11 +144,11 @@ class Game:
         np.ascontiguousarray(eval_seeds, dtype=np.uint32), mc,
         out["child_action"], out["child_n"], out["child_w"], out["child_out"],
         out["nchild"], out["root_n"], out["root_w"], out["root_out"],
-        out["best_action"], out["nodes"], threads)
+        out["best_action"], out["nodes"], threads, int(bool(puct)))
     return out
 
   def mcts_numpy(self, history, seed, uct_c=2.0, max_simulations=1000,
-                 n_rollouts=1, solve=True):
+                 n_rollouts=1, solve=True, puct=False):
     mc = self.num_distinct_actions
     out = dict(
         child_action=np.zeros((1, mc), np.int32),
@@ -162,7 +164,8 @@ class Game:
         self._h, a, len(a), uct_c, max_simulations, n_rollouts, int(solve),
         seed, mc, out["child_action"], out["child_n"], out["child_w"],
         out["child_out"], out["nchild"], out["root_n"], out["root_w"],
-        out["root_out"], out["best_action"], out["nodes"], out["next_word"])
+        out["root_out"], out["best_action"], out["nodes"], out["next_word"],
+        int(bool(puct)))
     return out
 
   def time_mcts_batch(self, root_actions, root_offsets, bot_seeds, eval_seeds,

@@ -101,3 +101,44 @@ def test_reserved_is_default_and_small_batches_stay_reserved(E):
   assert _run(eng, small, 200)[1]["paged"] == 0  # < 64 roots
   with pytest.raises(ValueError):
     eng.set_arena_mode("heap")
+
+
+def test_root_sums_after_pool_overflow(E):
+  """a paged root-parallel batch that runs out of pool pages is
+  rerun on the reserved arena inside the fetch; the action-indexed sums that
+  feed the all-reduce (dist.HipBackend.root_sums, C-ABI os_root_parallel) must
+  then be those of the rerun, i.e. of the full searches."""
+  from os_amd import dist
+  gs, T, sims = "connect_four", 128, 400
+  be = dist.HipBackend(gs, 0)
+  be.eng.set_arena_mode("paged")
+  ids = np.arange(T, dtype=np.uint32)
+  es = ids + np.uint32(1 << 20)
+  late = np.array([0, 1, 0, 1, 0, 1], np.int64)  # solved in a few sims: tiny hint
+  be.root_sums(late, ids, es, uct_c=2.0, max_simulations=sims)
+  be.root_sums(late, ids, es, uct_c=2.0, max_simulations=sims)
+  assert be.eng.arena_info()["paged"] == 1
+  v, w = be.root_sums(np.zeros(0, np.int64), ids, es, uct_c=2.0, max_simulations=sims)
+  info = be.eng.arena_info()
+  assert info["reruns"] == 1 and info["overflowed_searches"] > 0
+  out = be.eng.fetch()
+  want = E.action_indexed_visits(out, 7).sum(axis=0)
+  assert np.array_equal(v.cpu().numpy(), want)
+  assert int(want.sum()) == int((out["root_n"] - 1).sum())
+  ref = O.Game(gs).mcts_batch(np.zeros(0, np.int64), np.array([0, 0]), ids[:1], es[:1],
+                              uct_c=2.0, max_simulations=sims, max_children=7)
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(out[k][:1], ref[k], err_msg=k)
+  # The single-process C-ABI driver on a fresh engine: hint from the late
+  # position only, then the opening overflows and is rerun there too.
+  eng = E.Engine(gs)
+  eng.set_arena_mode("paged")
+  for _ in range(2):
+    E.root_parallel([eng], late, T, uct_c=2.0, max_simulations=sims)
+    eng.fetch()  # records the hint (os_root_parallel does not fetch)
+  assert eng.arena_info()["paged"] == 1
+  vis, rew, s = E.root_parallel([eng], np.zeros(0, np.int64), T, uct_c=2.0,
+                                max_simulations=sims)
+  assert eng.arena_info()["reruns"] == 1
+  assert np.array_equal(vis, want) and s == int(out["root_n"].sum())
+  np.testing.assert_array_equal(rew, w.cpu().numpy())

@@ -14,7 +14,10 @@ import pyspiel
 from open_spiel.python.algorithms import mcts
 
 BIG = ["go", "go(board_size=13)", "go(board_size=12,komi=0.5)", "hex(board_size=13)",
-       "hex(board_size=19)", "hex(board_size=12)"]
+       "hex(board_size=19)", "hex(board_size=12)",
+       # handicap stones (go.cc:56-78, 211-225): white moves first, score -= h
+       "go(handicap=2)", "go(handicap=5,komi=0.5)", "go(board_size=16,handicap=9)",
+       "go(handicap=12)"]
 
 
 def test_default_go_is_19x19():
@@ -75,9 +78,35 @@ def test_gpu_search_refuses_big_boards_and_auto_backend_uses_host_loop():
     mcts.MCTSBot(g, 2.0, 10, mcts.RandomRolloutEvaluator(1, rs), random_state=rs,
                  backend="hip")
   bot = mcts.MCTSBot(g, 2.0, 12, mcts.RandomRolloutEvaluator(1, rs), random_state=rs)
-  root = bot.mcts_search(g.new_initial_state())
+  with pytest.warns(RuntimeWarning, match="host CPU"):
+    root = bot.mcts_search(g.new_initial_state())
   assert root.explore_count == 12 and len(root.children) == 170
   cbot = pyspiel.MCTSBot(g, pyspiel.RandomRolloutEvaluator(1, 1), 2.0, 10, 100, True, 1,
                          False)
   with pytest.raises(ValueError):
     cbot.step(g.new_initial_state())
+
+
+@pytest.mark.parametrize("h,stones", [(2, ["d4", "q16"]), (4, ["d4", "q16", "d16", "q4"]),
+                                      (5, ["d4", "q16", "d16", "q4", "k10"]),
+                                      (9, ["d4", "q16", "d16", "q4", "d10", "q10", "k4",
+                                           "k16", "k10"]), (1, []), (10, [])])
+def test_go_handicap_setup(h, stones):
+  """go_test.cc:43-53 HandicapTest, every handicap count."""
+  g = pyspiel.load_game("go(handicap=%d)" % h)
+  st = g.new_initial_state()
+  assert st.current_player() == (1 if h >= 2 else 0)
+  assert st.history() == []
+  cols = "abcdefghjklmnopqrst"
+  black = {cols.index(x[0]) + 19 * (int(x[1:]) - 1) for x in stones}
+  legal = set(st.legal_actions())
+  assert not black & legal and len(legal) == 362 - len(black)
+  assert g.get_parameters()["handicap"] == h
+  ref = O.Game("go(handicap=%d)" % h).state_info([])
+  assert sorted(legal) == ref["legal_actions"] and st.current_player() == ref["current_player"]
+
+
+def test_go_handicap_off_the_board_is_an_error():
+  with pytest.raises(RuntimeError):  # GoBoard::PlayMove's SPIEL_CHECK (go_board.cc:263)
+    pyspiel.load_game("go(board_size=9,handicap=2)")
+  pyspiel.load_game("go(board_size=9,handicap=1)")  # no stones: loads

@@ -143,3 +143,23 @@ def test_go_tromp_taylor_score_matches_oracle(gs):
         assert H.go_score(gs, hist) == og.go_score(hist), hist
         checked += 1
   assert checked > 300
+
+
+# ChildSelectionPolicy::PUCT with the random-rollout evaluator's uniform prior
+# (mcts.cc:102-111, mcts.py:135-142): both RNG policies, pig's chance search.
+@pytest.mark.parametrize("gs", ["tic_tac_toe", "connect_four", "breakthrough(rows=5,columns=5)",
+                                "hex(board_size=5)", "go(board_size=5,komi=0.5)",
+                                "pig(horizon=30,winscore=10)"])
+@pytest.mark.parametrize("uct_c,solve,nr", [(2.0, True, 1), (0.5, False, 2)])
+def test_puct_matches_oracle(gs, uct_c, solve, nr):
+  from os_amd import pyspiel
+  maxc = pyspiel.load_game(gs)._info.max_children
+  acts, offs = _roots(gs, 8, 4)
+  bs = np.arange(8, dtype=np.uint32) * 5 + 2
+  es = bs + np.uint32(1 << 20)
+  kw = dict(uct_c=uct_c, max_simulations=300, n_rollouts=nr, solve=solve)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=maxc, puct=True, **kw)
+  got = H.mcts_batch(gs, acts, offs, bs, es, maxc, puct=True, **kw)
+  _check(got, ref)
+  uct = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=maxc, **kw)
+  assert not all(np.array_equal(uct[k], ref[k]) for k in H.KEYS)  # PUCT is not UCT

@@ -55,6 +55,10 @@ def test_search_bit_exact(E, gs, R, sims, plies, layout, block):
   bs = np.arange(R, dtype=np.uint32)
   es = bs + np.uint32(1 << 20)
   lay = _lib.LAYOUT_WAVE if layout == "wave" else _lib.LAYOUT_LANE
+  if gs.startswith("go") and layout == "lane":  # go runs one wave per search only
+    with pytest.raises(ValueError):
+      eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims, layout=lay)
+    return
   got = eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
                        block_size=block, layout=lay)
   ref = O.Game(gs).mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
@@ -286,3 +290,57 @@ def test_uct_screen_ties_and_near_ties(E, gs, uct_c, solve):
   ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, threads=8,
                               **kw)
   _cmp(E, got, ref)
+
+
+# ChildSelectionPolicy::PUCT with the random-rollout evaluator (mcts.cc:102-111,
+# uniform Prior :73-86): both search kernels, n_rollouts > 1 (f64 rewards),
+# solver on and off.  The numpy policy's PUCT is pinned by the reference-Python
+# fixtures (tests/golden/python_mcts_puct_*.json, test_python_goldens.py).
+@pytest.mark.parametrize("gs,R,sims,plies", [
+    ("tic_tac_toe", 32, 600, 4), ("connect_four", 64, 700, 8),
+    ("breakthrough(rows=6,columns=6)", 16, 300, 4), ("hex(board_size=5)", 24, 400, 6),
+    ("hex", 4, 300, 4), ("go(board_size=7,komi=4.5)", 6, 150, 6)])
+@pytest.mark.parametrize("layout", ["wave", "lane"])
+@pytest.mark.parametrize("nr,solve,uct_c", [(1, True, 2.0), (2, False, 0.7)])
+def test_puct_bit_exact(E, gs, R, sims, plies, layout, nr, solve, uct_c):
+  from os_amd import _lib
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, R, 1000, plies)
+  bs = np.arange(R, dtype=np.uint32) * 3 + 1
+  es = bs + np.uint32(1 << 20)
+  kw = dict(uct_c=uct_c, max_simulations=sims, n_rollouts=nr, solve=solve)
+  lay = _lib.LAYOUT_WAVE if layout == "wave" else _lib.LAYOUT_LANE
+  if gs.startswith("go") and layout == "lane":
+    pytest.skip("go runs one wave per search only")
+  got = eng.mcts_batch(acts, offs, bs, es, layout=lay, child_selection=_lib.SELECT_PUCT, **kw)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, threads=8,
+                              puct=True, **kw)
+  _cmp(E, got, ref)
+
+
+def test_puct_pig_chance_search(E):
+  from os_amd import _lib
+  gs = "pig(horizon=30,winscore=10)"
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, 32, 1000, 6)
+  bs = np.arange(32, dtype=np.uint32) + 9
+  es = bs + np.uint32(1 << 20)
+  kw = dict(uct_c=2.0, max_simulations=400)
+  got = eng.mcts_batch(acts, offs, bs, es, child_selection=_lib.SELECT_PUCT, **kw)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, puct=True,
+                              **kw)
+  _cmp(E, got, ref)
+
+
+def test_cpp_style_puct_bot_matches_oracle(E):
+  """pyspiel.MCTSBot(..., ChildSelectionPolicy.PUCT) (pyspiel.cc:512-524)."""
+  import pyspiel
+  game = pyspiel.load_game("connect_four")
+  bot = pyspiel.MCTSBot(game, pyspiel.RandomRolloutEvaluator(1, 7), 2.0, 400, 1000, True, 3,
+                        False, pyspiel.ChildSelectionPolicy.PUCT)
+  root = bot.mcts_search(game.new_initial_state())
+  ref = O.Game("connect_four").mcts_batch(np.zeros(0, np.int64), np.array([0, 0]), [3], [7],
+                                          uct_c=2.0, max_simulations=400, puct=True)
+  assert [c.action for c in root.children] == list(ref["child_action"][0][:7])
+  assert [c.explore_count for c in root.children] == list(ref["child_n"][0][:7])
+  assert root.best_child().action == ref["best_action"][0]

@@ -85,6 +85,36 @@ def test_hip_backend_rejects_custom_evaluators():
 def test_cpp_style_bot_validates_arguments():
   game = pyspiel.load_game("connect_four")
   ev = pyspiel.RandomRolloutEvaluator(1, 1)
+  pyspiel.MCTSBot(game, ev, 2.0, 10, 100, True, 1, False,
+                  pyspiel.ChildSelectionPolicy.PUCT)  # PUCT is bound (pyspiel.cc:512-524)
   with pytest.raises(ValueError):
-    pyspiel.MCTSBot(game, ev, 2.0, 10, 100, True, 1, False,
-                    pyspiel.ChildSelectionPolicy.PUCT)
+    pyspiel.MCTSBot(game, ev, 2.0, 10, 100, True, 1, False, 7)
+  with pytest.raises(ValueError):
+    pyspiel.MCTSBot(game, object(), 2.0, 10, 100, True, 1, False)
+
+
+def test_auto_backend_warns_before_a_host_search():
+  """A search the GPU engine does not run is never silent under backend='auto'."""
+  class MyEval(mcts.RandomRolloutEvaluator):
+    pass
+  game = pyspiel.load_game("tic_tac_toe")
+  rng = np.random.RandomState(0)
+  bot = mcts.MCTSBot(game, 2.0, 20, MyEval(1, rng), random_state=rng)
+  with pytest.warns(RuntimeWarning, match="host CPU"):
+    bot.mcts_search(game.new_initial_state())
+  quiet = mcts.MCTSBot(game, 2.0, 20, MyEval(1, rng), random_state=rng, backend="host")
+  import warnings
+  with warnings.catch_warnings():
+    warnings.simplefilter("error")
+    quiet.mcts_search(game.new_initial_state())
+
+
+def test_pig_buffers_hold_more_outcomes_than_distinct_actions():
+  game = pyspiel.load_game("pig(diceoutcomes=10)")
+  assert game.max_chance_outcomes() == 10
+  st = game.new_initial_state()
+  st.apply_action(0)  # roll
+  outs = st.chance_outcomes()
+  assert [a for a, _ in outs] == list(range(1, 11))
+  assert st.legal_actions() == list(range(1, 11))
+  assert pyspiel.load_game("pig(diceoutcomes=1)").max_chance_outcomes() == 1

@@ -14,6 +14,8 @@ post-search RandomState position(s).
   * GPU (-m gpu): the product's device path (os_amd.mcts backend="hip", one
     `os_mcts_stateful` call per search) reproduces every case, including the
     RandomState(s) it continues in place.
+  * python_mcts_puct_*.json: the same with child_selection_fn =
+    SearchNode.puct_value (mcts.py:135-142), on every game.
 """
 import glob
 import hashlib
@@ -61,9 +63,11 @@ def _search(game_string, c, backend):
     st.apply_action(a)
   bot_rs = np.random.RandomState(c["seed"])
   ev_rs = bot_rs if c["shared"] else np.random.RandomState(c["seed2"])
+  sel = mcts.SearchNode.puct_value if c.get("selection") == "puct" else mcts.SearchNode.uct_value
   bot = mcts.MCTSBot(game, c["uct_c"], c["max_simulations"],
                      mcts.RandomRolloutEvaluator(c["n_rollouts"], ev_rs),
-                     solve=c["solve"], random_state=bot_rs, backend=backend)
+                     solve=c["solve"], random_state=bot_rs, backend=backend,
+                     child_selection_fn=sel)
   root = bot.mcts_search(st)
   return root, bot_rs, ev_rs
 
@@ -85,6 +89,8 @@ def test_fixture_coverage():
   assert games == {"tic_tac_toe", "connect_four", "breakthrough", "hex", "go", "pig"}
   assert any(not p.values[1]["shared"] for p in CASES)
   assert any(p.values[1]["n_rollouts"] > 1 for p in CASES)
+  puct = {p.values[0].split("(")[0] for p in CASES if p.values[1].get("selection") == "puct"}
+  assert puct == games  # SearchNode.puct_value on every game
 
 
 @pytest.mark.parametrize("game_string,c", [p for p in CASES if p.values[1]["shared"]])
@@ -92,7 +98,7 @@ def test_oracle_numpy_bot_matches_reference_python(game_string, c):
   og = oracle_lib.Game(game_string)
   r = og.mcts_numpy(c["history"], c["seed"], uct_c=c["uct_c"],
                     max_simulations=c["max_simulations"], n_rollouts=c["n_rollouts"],
-                    solve=c["solve"])
+                    solve=c["solve"], puct=c.get("selection") == "puct")
   k = int(r["nchild"][0])
   assert k == len(c["children"])
   assert r["child_action"][0, :k].tolist() == [ch[0] for ch in c["children"]]

@@ -73,16 +73,17 @@ def random_history(game, plies, seed):
   return hist if not st.is_terminal() else hist[:-1]
 
 
-def run_case(mcts, game, history, seed, seed2, uct_c, sims, n_rollouts, solve):
+def run_case(mcts, game, history, seed, seed2, uct_c, sims, n_rollouts, solve, puct=False):
   st = game.new_initial_state()
   for a in history:
     st.apply_action(a)
   bot_rs = np.random.RandomState(seed)
   ev_rs = bot_rs if seed2 is None else np.random.RandomState(seed2)
+  kw = {"child_selection_fn": mcts.SearchNode.puct_value} if puct else {}
   bot = mcts.MCTSBot(game, uct_c, max_simulations=sims, solve=solve,
                      random_state=bot_rs,
                      evaluator=mcts.RandomRolloutEvaluator(n_rollouts=n_rollouts,
-                                                           random_state=ev_rs))
+                                                           random_state=ev_rs), **kw)
   t0 = time.time()
   root = bot.mcts_search(st)
   secs = time.time() - t0
@@ -99,6 +100,8 @@ def run_case(mcts, game, history, seed, seed2, uct_c, sims, n_rollouts, solve):
       "bot_rng_after": rs_fingerprint(bot_rs),
       "eval_rng_after": None if seed2 is None else rs_fingerprint(ev_rs),
   }
+  if puct:
+    rec["selection"] = "puct"  # child_selection_fn = SearchNode.puct_value
   return rec, secs
 
 
@@ -106,6 +109,9 @@ def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--reference", default="/root/reference")
   ap.add_argument("--only", default="")
+  ap.add_argument("--puct", action="store_true",
+                  help="write python_mcts_puct_<game>.json: the same plan with "
+                       "child_selection_fn = SearchNode.puct_value (mcts.py:135-142)")
   args = ap.parse_args()
   sys.path.insert(0, PKG)
   import pyspiel  # noqa: F401  (the drop-in; the reference module imports it)
@@ -132,8 +138,19 @@ def main():
       "pig": dict(positions=[[], [0, 4, 0, 3], [1, 0, 5, 1]], seeds=[0, 42], sims=300),
       "pig(horizon=30,winscore=8)": dict(positions=[[], [0, 5]], seeds=[0, 42], sims=1000),
   }
+  if args.puct:
+    plan = {
+        "tic_tac_toe": dict(positions=[[], [4, 0]], seeds=[0, 42], sims=600),
+        "connect_four": dict(positions=[[], ("random", 8, 7)], seeds=[0, 42], sims=500),
+        "breakthrough(rows=6,columns=6)": dict(positions=[[]], seeds=[3], sims=300),
+        "hex(board_size=5)": dict(positions=[[], ("random", 6, 5)], seeds=[0], sims=500),
+        "go(board_size=7,komi=4.5)": dict(positions=[[]], seeds=[42], sims=150),
+        "pig(horizon=30,winscore=8)": dict(positions=[[], [0, 5]], seeds=[0], sims=500),
+    }
   for gs, p in plan.items():
     base = gs.split("(")[0] + ("" if "(" not in gs else "_" + gs.split("=")[-1].rstrip(")"))
+    if args.puct:
+      base = "puct_" + gs.split("(")[0]
     if args.only and args.only not in gs:
       continue
     game = pyspiel.load_game(gs)
@@ -141,20 +158,22 @@ def main():
     total = 0.0
     for pos in p["positions"]:
       hist = pos if isinstance(pos, list) else random_history(game, pos[1], pos[2])
+      pu = args.puct
       for seed in p["seeds"]:
-        rec, secs = run_case(mcts, game, hist, seed, None, C, p["sims"], 1, True)
+        rec, secs = run_case(mcts, game, hist, seed, None, C, p["sims"], 1, True, pu)
         cases.append(rec)
         total += secs
       # one case with two RandomStates, and one with n_rollouts=2 / solve off
-      rec, secs = run_case(mcts, game, hist, 7, 1007, C, p["sims"], 1, True)
+      rec, secs = run_case(mcts, game, hist, 7, 1007, C, p["sims"], 1, True, pu)
       cases.append(rec)
       total += secs
-      rec, secs = run_case(mcts, game, hist, 11, None, 1.4, max(10, p["sims"] // 2), 2, False)
+      rec, secs = run_case(mcts, game, hist, 11, None, 1.4, max(10, p["sims"] // 2), 2, False,
+                           pu)
       cases.append(rec)
       total += secs
     if gs == "tic_tac_toe":
       # mcts_test.py:41-54 / :115-153 solver positions (10000 sims, 20 rollouts).
-      for hist in ([4, 0, 8], [4, 0, 8, 1, 2], [1, 8]):
+      for hist in ([] if args.puct else ([4, 0, 8], [4, 0, 8, 1, 2], [1, 8])):
         rec, secs = run_case(mcts, game, hist, 42, None, 2 ** 0.5, 10000, 20, True)
         cases.append(rec)
         total += secs
@@ -162,7 +181,8 @@ def main():
       pg = pyttt.TicTacToeGame()
       for rec in cases:
         got, _ = run_case(mcts, pg, rec["history"], rec["seed"], rec["seed2"], rec["uct_c"],
-                          rec["max_simulations"], rec["n_rollouts"], rec["solve"])
+                          rec["max_simulations"], rec["n_rollouts"], rec["solve"],
+                          args.puct)
         assert got == rec, "python_tic_tac_toe differs on %s" % rec["history"]
     doc = {
         "_source": "tools/gen_python_mcts_goldens.py: unmodified reference "
