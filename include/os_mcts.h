@@ -22,7 +22,9 @@
  *   - Child outputs are in the tree's child order (the shuffled expansion
  *     order of mcts.cc:275), stride max_children per root.
  *   - Outcomes are int8: the value for the node's own player (the reference's
- *     `outcome[player]`), or 2 when the node is unsolved (empty vector).
+ *     `outcome[player]`), or 2 when the node is unsolved (empty vector).  With
+ *     more than two players (pig) it is the value's sign: +1 a win (1), -1 a
+ *     loss (-1 / (n - 1)), 0 nobody won (0).
  */
 #ifndef OS_MCTS_C_ABI_H_
 #define OS_MCTS_C_ABI_H_
@@ -56,7 +58,7 @@ typedef struct {
   int32_t kind;               /* 0 ttt, 1 connect_four, 2 breakthrough, 3 hex, 4 go, 5 pig */
   int32_t num_distinct_actions;  /* Game::NumDistinctActions (spiel.h:601-750) */
   int32_t max_game_length;    /* Game::MaxGameLength */
-  int32_t num_players;        /* 2 */
+  int32_t num_players;        /* Game::NumPlayers: 2 (pig: `players`, 2..10) */
   int32_t max_children;       /* upper bound on |LegalActions()| */
   int32_t rows, cols;         /* board geometry */
   double min_utility, max_utility, utility_sum;
@@ -75,7 +77,8 @@ void os_state_free(os_state* s);
 int os_state_apply(os_state* s, int64_t action);            /* ApplyAction (spiel.h:205) */
 int32_t os_state_current_player(const os_state* s);         /* CurrentPlayer (-4 terminal) */
 int32_t os_state_is_terminal(const os_state* s);            /* IsTerminal (spiel.h:283) */
-int os_state_returns(const os_state* s, double* out2);      /* Returns (spiel.h:309) */
+/* Returns (spiel.h:309): writes num_players values (os_game_info). */
+int os_state_returns(const os_state* s, double* out2);
 /* IsChanceNode (spiel.h:331; CurrentPlayer() is then -1, kChancePlayerId). */
 int32_t os_state_is_chance_node(const os_state* s);
 /* ChanceOutcomes (spiel.h:322-327): (action, probability) pairs in outcome
@@ -360,6 +363,13 @@ int32_t os_engine_state_bytes(os_engine* e);
  * total action count, or < 0 on error.  actions may be NULL to size. */
 int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base,
                       int32_t max_plies, int64_t* actions, int64_t* offsets);
+
+/* SampleAction(outcomes, rng) (spiel.cc:337-366), as EvaluateBots
+ * (evaluate_bots.cc:24-61) samples chance nodes: z = absl::Uniform(rng, 0.0,
+ * 1.0) from a std::mt19937 held in numpy's legacy (key[624], pos) form
+ * (advanced in place); returns the index of the first outcome whose
+ * [sum, sum + probs[k]) holds z, or < 0 on error. */
+int32_t os_sample_action(const double* probs, int32_t n, uint32_t* key, int32_t* pos);
 
 /* Library/kernel build info string (arch, build flags). */
 const char* os_build_info(void);

@@ -34,7 +34,8 @@ OS_HD int sample_chance(const GameCfg& g, Rng& rng) {
   return NpChoiceEquiprobable(rng, n, p);
 }
 
-// RandomRolloutEvaluator::Evaluate's playout with chance nodes.
+// RandomRolloutEvaluator::Evaluate's playout with chance nodes; returns the
+// terminal's outcome code (G::ret0).
 template <class G, int Policy, class Rng>
 OS_HD int rollout_ret0_chance(typename G::State s, const GameCfg& g, typename G::Ctx& ctx,
                               Rng& ev) {
@@ -54,6 +55,33 @@ OS_HD int rollout_ret0_chance(typename G::State s, const GameCfg& g, typename G:
 }
 
 OS_HD int reward_player(int p, int root_player) { return p < 0 ? root_player : p; }
+
+// Evaluate()'s return vector (mcts.cc:42-71) for up to G::kMaxPlayers
+// players, indexed through unrolled selects only (registers, no scratch).
+template <class G>
+struct Returns {
+  double v[G::kMaxPlayers];
+  // Returns() of a terminal with outcome code `code`.
+  OS_HD void set(int code, const GameCfg& g) {
+#pragma unroll
+    for (int i = 0; i < G::kMaxPlayers; ++i) v[i] = OutValue<G>::value(code, i, g);
+  }
+  // result[k] += r[k] (the reference sums rollouts in order, then divides).
+  OS_HD void add(int code, const GameCfg& g) {
+#pragma unroll
+    for (int i = 0; i < G::kMaxPlayers; ++i) v[i] += OutValue<G>::value(code, i, g);
+  }
+  OS_HD void div(int n) {
+#pragma unroll
+    for (int i = 0; i < G::kMaxPlayers; ++i) v[i] /= n;
+  }
+  OS_HD double of(int p) const {
+    double x = 0.0;
+#pragma unroll
+    for (int i = 0; i < G::kMaxPlayers; ++i) x = i == p ? v[i] : x;
+    return x;
+  }
+};
 
 // Same contract as mcts_search; path_cap <= kChancePathCap.
 template <class G, class R, int Policy, class Rng>
@@ -135,7 +163,7 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
         for (int k = 0; k < nc; ++k) {
           const Node<R> c = nodes[first + k];
           double v;
-          if (c.out != kUnsolved) v = outcome_for(c.out, cp);
+          if (c.out != kUnsolved) v = OutValue<G>::value(c.out, cp, g);
           else if (sp.puct) v = puct_unsolved(static_cast<double>(c.w), c.n, cprior, logN);
           else if (c.n == 0) v = inf;
           else v = static_cast<double>(c.w) / c.n + sp.uct_c * __builtin_sqrt(logN / c.n);
@@ -154,33 +182,30 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
     }
     if (depth > res.max_depth) res.max_depth = depth;
     {
-      // ---- evaluation ----
+      // ---- evaluation: the n-player return vector ----
       bool solved;
-      R rv0;
+      Returns<G> ret;
       if (G::terminal(s, g)) {
-        const int r0 = G::ret0(s, g, ctx);
-        nodes[path[depth].idx].out = static_cast<int8_t>(r0);
+        const int code = G::ret0(s, g, ctx);
+        nodes[path[depth].idx].out = static_cast<int8_t>(code);
         solved = sp.solve != 0;
-        rv0 = static_cast<R>(r0);
+        ret.set(code, g);
       } else {
         solved = false;
-        if (sp.n_rollouts == 1) {
-          rv0 = static_cast<R>(rollout_ret0_chance<G, Policy>(s, g, ctx, ev));
-        } else {
-          const int leaf_mark = ctx.mark();
-          double s0 = 0.0;
-          for (int k = 0; k < sp.n_rollouts; ++k) {
-            if (k) ctx.rewind(leaf_mark);
-            s0 += static_cast<double>(rollout_ret0_chance<G, Policy>(s, g, ctx, ev));
-          }
-          rv0 = static_cast<R>(s0 / sp.n_rollouts);
+        const int leaf_mark = ctx.mark();
+        for (int k = 0; k < sp.n_rollouts; ++k) {
+          if (k) ctx.rewind(leaf_mark);
+          const int code = rollout_ret0_chance<G, Policy>(s, g, ctx, ev);
+          if (k) ret.add(code, g);
+          else ret.set(code, g);
         }
+        ret.div(sp.n_rollouts);  // x / 1 == x: the single-rollout case too
       }
       // ---- backup + MCTS-Solver (mcts.cc:351-396) ----
       for (int d = depth; d >= 0; --d) {
         Node<R>& nd = nodes[path[d].idx];
         const int pl = d == 0 ? P0 : reward_player(chooser[d - 1], P0);
-        nd.w += pl == 0 ? rv0 : static_cast<R>(-rv0);
+        nd.w += static_cast<R>(ret.of(pl));
         nd.n += 1;
         res.backed += 1;
         if (solved && nd.nchild > 0) {
@@ -202,7 +227,7 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
               if (co == kUnsolved) {
                 all_solved = false;
               } else {
-                const double v = outcome_for(co, cpl);
+                const double v = OutValue<G>::value(co, cpl, g);
                 if (best < 0 || v > bestv) {
                   best = k;
                   bestv = v;

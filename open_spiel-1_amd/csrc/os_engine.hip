@@ -364,8 +364,11 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   e->num_roots = R;
   const GameCfg& cfg = e->game.cfg;
   e->max_children = cfg.max_children;
-  e->node_bytes = p->n_rollouts == 1 ? static_cast<int>(sizeof(Node<int32_t>))
-                                      : static_cast<int>(sizeof(Node<double>));
+  // f64 node rewards when they are not integers: rollout means, or pig's
+  // -1 / (n - 1) losses with more than two players (pig.cc:94-111).
+  e->node_bytes = p->n_rollouts == 1 && cfg.pig_players <= 2
+                      ? static_cast<int>(sizeof(Node<int32_t>))
+                      : static_cast<int>(sizeof(Node<double>));
   if ((rc = SizeArena(e, true))) return rc;
 
   // Root states (+ go hash sets) on the host.
@@ -872,7 +875,7 @@ int os_game_get_info(const os_game* game, os_game_info* o) {
   o->kind = c.kind;
   o->num_distinct_actions = c.num_actions;
   o->max_game_length = c.max_game_length;
-  o->num_players = 2;
+  o->num_players = NumPlayers(c);
   o->max_children = c.max_children;
   o->rows = c.rows;
   o->cols = c.cols;
@@ -947,7 +950,8 @@ int64_t os_game_observation_shape(const os_game* game, int32_t* shape3) {
 int64_t os_state_observation_tensor(const os_state* s, int32_t player, float* out,
                                     int64_t cap) {
   if (!s) return Fail(OS_ERR_INVALID, "null state");
-  if (player < 0 || player > 1) return Fail(OS_ERR_INVALID, "player must be 0 or 1");
+  if (player < 0 || player >= NumPlayers(s->s.game->cfg))
+    return Fail(OS_ERR_INVALID, "player out of range");
   const int64_t n = ObservationShape(*s->s.game, nullptr);
   if (out && cap >= n) StateObservation(s->s, player, out);
   return n;
@@ -1508,6 +1512,22 @@ int os_root_parallel(os_engine* const* engines, int32_t ndev, const os_mcts_para
   HIP_TRY(hipMemcpy(out_rewards, out_w, A * 8, hipMemcpyDeviceToHost));
   if (out_sims) *out_sims = sims;
   return OS_OK;
+}
+
+int32_t os_sample_action(const double* probs, int32_t n, uint32_t* key, int32_t* pos) {
+  if (!probs || n < 1 || !key || !pos || *pos < 0 || *pos > kMtN)
+    return Fail(OS_ERR_INVALID, "bad argument");
+  MtStream g{key, *pos, 1, 0};
+  const double z = AbslUniformDouble01(g);
+  g.finalize();
+  *pos = g.idx;
+  // spiel.cc:341-366: the first outcome whose [sum, sum + p) holds z.
+  double sum = 0.0;
+  for (int32_t k = 0; k < n; ++k) {
+    if (sum <= z && z < sum + probs[k]) return k;
+    sum += probs[k];
+  }
+  return Fail(OS_ERR_INVALID, "SampleAction: probabilities do not cover z");
 }
 
 int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base,

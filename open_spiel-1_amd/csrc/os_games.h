@@ -18,7 +18,7 @@
 //   breakthrough  open_spiel/games/breakthrough.cc:119-320
 //   hex           open_spiel/games/hex.cc:55-255
 //   go            open_spiel/games/go.cc:124-216, go/go_board.cc:217-597
-//   pig           open_spiel/games/pig.cc:81-244 (two players; chance nodes)
+//   pig           open_spiel/games/pig.cc:81-244 (2..10 players; chance nodes)
 // Games with chance nodes (G::kHasChance) also provide
 //   chance(const S&)                    IsChanceNode()
 //   chance_count(cfg), chance_prob(cfg) ChanceOutcomes(): actions kth(0..count)
@@ -51,6 +51,7 @@ struct GameCfg {
   float komi;
   int32_t handicap;
   int32_t pig_dice, pig_horizon, pig_win;         // pig diceoutcomes / horizon / winscore
+  int32_t pig_players;                            // pig players (2..10)
   uint64_t board64, notcol0_64, notcollast_64;   // breakthrough (<= 64 cells)
   B128 board, notcol0, notcollast;               // hex / go (<= 128 cells)
   // Hex side-neighbour masks.  Equal to notcol0 / notcollast except on n = 2,
@@ -810,17 +811,25 @@ using Go = GoT<B128>;
 using GoBig = GoT<B384>;  // board_size 12..19 (host State API)
 
 // ----------------------------------------------------------------------------
-// pig (pig.cc:81-244), two players.  A decision node offers roll (0) and stop
-// (1) -- only stop once the turn total would reach winscore (:225-229).  Roll
-// moves to a chance node whose outcomes are 1..diceoutcomes, each with
-// probability 1 / diceoutcomes (:233-244): outcome 1 loses the turn total and
-// passes the turn, outcome k > 1 adds k + 1 (:204-213, as written).  Stop
-// banks the turn total and passes.  total_moves counts decisions only;
-// terminal at total_moves >= horizon or a score >= winscore (:81-92); the
-// winner gets +1 and the other -1, nobody 0 (:94-111).
+// pig (pig.cc:81-244), 2..10 players.  A decision node offers roll (0) and
+// stop (1) -- only stop once the turn total would reach winscore
+// (:225-229).  Roll moves to a chance node whose outcomes are
+// 1..diceoutcomes, each with probability 1 / diceoutcomes (:233-244):
+// outcome 1 loses the turn total and passes the turn, outcome k > 1 adds
+// k + 1 (:204-213, as written).  Stop banks the turn total and passes
+// (round robin).  total_moves counts decisions only; terminal at total_moves
+// >= horizon or a score >= winscore (:81-92).  Returns (:94-111): the first
+// player (in player order) at winscore gets +1, every other -1 / (n - 1);
+// nobody: all 0.  The scores live in a fixed array indexed only through
+// unrolled selects, so a state held in registers never goes to scratch.
+//
+// Outcome codes (ret0 / Node::out): two players keep the player-0 value
+// {-1, 0, +1}; with n > 2 players a win by player w is 3 + w and "nobody" 0
+// (the reference's outcome vectors are determined by them; out_value()).
 struct Pig {
+  static constexpr int kMaxPlayers = 10;
   struct State {
-    int32_t score0, score1;
+    int32_t score[kMaxPlayers];
     int32_t turn_total;
     int32_t cur;          // player to move, -1 at a chance node
     int32_t turn_player;
@@ -834,15 +843,30 @@ struct Pig {
     int count;
     OS_HD int kth(int k) const { return select64(mask, k); }
   };
+  OS_HD static int32_t score_of(const State& s, int p) {
+    int32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxPlayers; ++i) v = i == p ? s.score[i] : v;
+    return v;
+  }
   OS_HD static void init(State& s, const GameCfg&) {
-    s.score0 = s.score1 = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxPlayers; ++i) s.score[i] = 0;
     s.turn_total = 0;
     s.cur = 0;
     s.turn_player = 0;
     s.moves = 0;
   }
+  // The first player (in player order) whose score reaches winscore, or -1.
+  OS_HD static int winner(const State& s, const GameCfg& g) {
+    int w = -1;
+#pragma unroll
+    for (int i = kMaxPlayers - 1; i >= 0; --i)
+      w = (i < g.pig_players && s.score[i] >= g.pig_win) ? i : w;
+    return w;
+  }
   OS_HD static bool terminal(const State& s, const GameCfg& g) {
-    return s.moves >= g.pig_horizon || s.score0 >= g.pig_win || s.score1 >= g.pig_win;
+    return s.moves >= g.pig_horizon || winner(s, g) >= 0;
   }
   OS_HD static int to_move(const State& s) { return s.cur; }
   OS_HD static bool chance(const State& s) { return s.cur < 0; }
@@ -854,27 +878,29 @@ struct Pig {
       l.mask = ((1u << g.pig_dice) - 1u) << 1;  // outcomes 1..dice
       l.count = g.pig_dice;
     } else {
-      const int mine = s.cur ? s.score1 : s.score0;
-      l.mask = mine + s.turn_total >= g.pig_win ? 2u : 3u;
+      l.mask = score_of(s, s.cur) + s.turn_total >= g.pig_win ? 2u : 3u;
       l.count = popc64(l.mask);
     }
     return l;
   }
-  OS_HD static void apply(State& s, const GameCfg&, Ctx&, int a) {
+  OS_HD static int next_player(int p, const GameCfg& g) {  // NextPlayerRoundRobin
+    return p + 1 < g.pig_players ? p + 1 : 0;
+  }
+  OS_HD static void apply(State& s, const GameCfg& g, Ctx&, int a) {
     if (s.cur >= 0) {
       s.moves++;
       if (a == 0) {
         s.cur = -1;
         return;
       }
-      if (s.turn_player) s.score1 += s.turn_total;
-      else s.score0 += s.turn_total;
+#pragma unroll
+      for (int i = 0; i < kMaxPlayers; ++i) s.score[i] += i == s.turn_player ? s.turn_total : 0;
       s.turn_total = 0;
-      s.turn_player ^= 1;
+      s.turn_player = next_player(s.turn_player, g);
       s.cur = s.turn_player;
     } else if (a == 1) {
       s.turn_total = 0;
-      s.turn_player ^= 1;
+      s.turn_player = next_player(s.turn_player, g);
       s.cur = s.turn_player;
     } else {
       s.turn_total += a + 1;
@@ -882,19 +908,38 @@ struct Pig {
     }
   }
   OS_HD static int ret0(const State& s, const GameCfg& g, Ctx&) {
-    if (s.score0 >= g.pig_win) return 1;
-    if (s.score1 >= g.pig_win) return -1;
-    return 0;
+    const int w = winner(s, g);
+    if (g.pig_players == 2) return w == 0 ? 1 : (w == 1 ? -1 : 0);
+    return w < 0 ? 0 : 3 + w;
   }
-  // ObservationTensor (pig.cc:119-168): [1 + 2][winscore + 1] one-hot bins of
-  // the turn total, then each player's score (the last bin holds >= winscore);
-  // as a [3][1][winscore + 1] CHW image (rows = 1, cols = winscore + 1).
-  static constexpr int kObsPlanes = 3;
+  // Returns()[p] of a terminal whose outcome code is `code` (pig.cc:94-111).
+  OS_HD static double value(int code, int p, const GameCfg& g) {
+    if (code >= 3) return p == code - 3 ? 1.0 : -1.0 / (g.pig_players - 1);
+    return static_cast<double>(p == 0 ? code : -code);
+  }
+  // ObservationTensor (pig.cc:119-168): [1 + players][winscore + 1] one-hot
+  // bins of the turn total, then each player's score (the last bin holds >=
+  // winscore); as a [1 + players][1][winscore + 1] CHW image.
+  static constexpr int kObsPlanes = 1 + kMaxPlayers;  // planes used: 1 + players
   OS_HD static float obs(const State& s, const GameCfg& g, int, int plane, int cell) {
-    const int v = plane == 0 ? s.turn_total : (plane == 1 ? s.score0 : s.score1);
+    const int v = plane == 0 ? s.turn_total : score_of(s, plane - 1);
     const int bin = v < g.pig_win ? v : g.pig_win;
     return cell == bin ? 1.0f : 0.0f;
   }
+};
+
+// Returns()[p] of a solved node whose outcome code is `out` (os_mcts.h
+// Node::out): the player-0 value of two-player zero-sum games, or the game's
+// own decoding (pig with more than two players).
+template <class G, class = void>
+struct OutValue {
+  OS_HD static double value(int out, int p, const GameCfg&) {
+    return static_cast<double>(p == 0 ? out : -out);
+  }
+};
+template <class G>
+struct OutValue<G, decltype(void(&G::value))> {
+  OS_HD static double value(int out, int p, const GameCfg& g) { return G::value(out, p, g); }
 };
 
 // Chance-node traits (games without them never reach the chance branches).

@@ -302,10 +302,6 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
       return "bad pig parameter";
     if (players < 2 || players > 10 || horizon < 1 || win < 1 || dice < 1)
       return "bad pig parameter";
-    if (players != 2) {
-      *unsupported = true;
-      return "pig with more than two players is not supported by this engine";
-    }
     if (dice > 30 || win > 4096) {
       *unsupported = true;
       return "pig diceoutcomes must be <= 30 and winscore <= 4096 for this engine";
@@ -319,6 +315,7 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
     c.pig_dice = dice;
     c.pig_horizon = horizon;
     c.pig_win = win;
+    c.pig_players = players;
     std::string canon = "pig(";
     bool first = true;
     for (auto& it : kv) {  // sorted by key, as GameParametersToString
@@ -480,10 +477,13 @@ void StateChanceOutcomes(const HostState& s, std::vector<std::pair<int64_t, doub
   });
 }
 
+int NumPlayers(const GameCfg& g) { return g.kind == kPig ? g.pig_players : 2; }
+
 void StateReturns(const HostState& s, double* r) {
-  r[0] = r[1] = 0.0;
-  if (!StateTerminal(s)) return;
   const GameCfg& g = s.game->cfg;
+  const int np = NumPlayers(g);
+  for (int p = 0; p < np; ++p) r[p] = 0.0;
+  if (!StateTerminal(s)) return;
   const int r0 = WithGame(g, [&](auto tag) {
     using G = decltype(tag);
     if constexpr (kIsGo<G>) {
@@ -495,6 +495,10 @@ void StateReturns(const HostState& s, double* r) {
       return G::ret0(St<G>(s), g, nc);
     }
   });
+  if (g.kind == kPig) {  // outcome code -> Returns() (pig.cc:94-111)
+    for (int p = 0; p < np; ++p) r[p] = Pig::value(r0, p, g);
+    return;
+  }
   r[0] = static_cast<double>(r0);
   r[1] = static_cast<double>(-r0);
 }
@@ -506,13 +510,16 @@ template <class G>
 void ObsFill(const HostState& s, int player, float* out) {
   const GameCfg& g = s.game->cfg;
   const int cells = g.rows * g.cols;
-  for (int c = 0; c < G::kObsPlanes; ++c)
+  const int planes = g.kind == kPig ? 1 + g.pig_players : G::kObsPlanes;
+  for (int c = 0; c < planes; ++c)
     for (int i = 0; i < cells; ++i) out[c * cells + i] = G::obs(St<G>(s), g, player, c, i);
 }
 }  // namespace
 
 int ObservationShape(const HostGame& g, int32_t* shape3) {
-  const int c = WithGame(g.cfg, [&](auto tag) { return ObsPlanes<decltype(tag)>(); });
+  const int c = g.cfg.kind == kPig  // pig.cc:118-121: 1 + players planes
+                    ? 1 + g.cfg.pig_players
+                    : WithGame(g.cfg, [&](auto tag) { return ObsPlanes<decltype(tag)>(); });
   if (shape3) {
     shape3[0] = c;
     shape3[1] = g.cfg.rows;
@@ -636,11 +643,13 @@ std::string StateToString(const HostState& s) {
     case kGo:
       return g.rows > kB128Side ? GoString(St<GoBig>(s), g, s.history.size())
                                 : GoString(St<Go>(s), g, s.history.size());
-    case kPig: {  // pig.cc:246-251
+    case kPig: {  // pig.cc:246-251 (StrJoin(scores_, " "))
       const Pig::State& p = St<Pig>(s);
-      return "Scores: " + std::to_string(p.score0) + " " + std::to_string(p.score1) +
-             ", Turn total: " + std::to_string(p.turn_total) + "\nCurrent player: " +
-             std::to_string(p.turn_player) + (p.cur < 0 ? " (rolling)\n" : "\n");
+      std::string sc;
+      for (int i = 0; i < g.pig_players; ++i) sc += (i ? " " : "") + std::to_string(p.score[i]);
+      return "Scores: " + sc + ", Turn total: " + std::to_string(p.turn_total) +
+             "\nCurrent player: " + std::to_string(p.turn_player) +
+             (p.cur < 0 ? " (rolling)\n" : "\n");
     }
   }
   return "";

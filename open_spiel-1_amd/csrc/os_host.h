@@ -70,6 +70,9 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported);
 // unless 2 <= handicap <= 9).
 std::vector<int> GoHandicapStones(int handicap, int n);
 
+// Game::NumPlayers (2, or pig's `players`).
+int NumPlayers(const GameCfg& g);
+
 void StateInit(HostState* s);
 bool StateTerminal(const HostState& s);
 int StateCurrentPlayer(const HostState& s);

@@ -125,18 +125,16 @@ __global__ void k_mcts(DevArgs a) {
   a.nchild[gr] = nc;
   a.root_n[gr] = rn.n;
   a.root_w[gr] = static_cast<double>(rn.w);
-  a.root_out[gr] = rn.out == kUnsolved ? kUnsolved
-                                       : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+  a.root_out[gr] = out_sign<G>(rn.out, P0, a.cfg);
   const int64_t ob = gr * a.max_children;
   for (int k = 0; k < nc && k < a.max_children; ++k) {
     const Node<R>& c = nodes[rn.first + k];
     a.child_action[ob + k] = c.action;
     a.child_n[ob + k] = c.n;
     a.child_w[ob + k] = static_cast<double>(c.w);
-    a.child_out[ob + k] =
-        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+    a.child_out[ob + k] = out_sign<G>(c.out, P0, a.cfg);
   }
-  const int b = best_child(nodes, P0);
+  const int b = best_child_g<G>(nodes, P0, a.cfg);
   a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
   if (a.import_state) {
     bot.finalize();
@@ -720,7 +718,7 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
 
 template <class G>
 int LaunchForGame(os_engine* e, const DevArgs& a, hipStream_t stream) {
-  const bool dbl = e->params.n_rollouts != 1;
+  const bool dbl = e->node_bytes != static_cast<int>(sizeof(Node<int32_t>));
   if (e->params.policy == OS_POLICY_NUMPY) {
     return dbl ? LaunchSearch<G, double, kPolicyNumpy>(e, a, stream)
                : LaunchSearch<G, int32_t, kPolicyNumpy>(e, a, stream);
@@ -858,6 +856,8 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
   a.n_root_hashes = e->roll_nhash;
   const int64_t n = e->roll_n;
+  if (e->game.cfg.pig_players > 2)
+    return Fail(OS_ERR_UNSUPPORTED, "rollout batches return two players' values");
   if constexpr (!HasChance<G>::value) {
     if (e->rollout_layout == OS_LAYOUT_WAVE) {
       hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream,

@@ -102,6 +102,36 @@ OS_HD bool final_less(const Node<R>& a, int pa, const Node<R>& b, int pb) {
   return static_cast<double>(a.w) < static_cast<double>(b.w);
 }
 
+// CompareFinal / BestChild with the game's outcome decoding (OutValue: pig
+// with more than two players).
+template <class G, class R>
+OS_HD bool final_less_g(const Node<R>& a, const Node<R>& b, int p, const GameCfg& g) {
+  const double oa = a.out == kUnsolved ? 0.0 : OutValue<G>::value(a.out, p, g);
+  const double ob = b.out == kUnsolved ? 0.0 : OutValue<G>::value(b.out, p, g);
+  if (oa != ob) return oa < ob;
+  if (a.n != b.n) return a.n < b.n;
+  return static_cast<double>(a.w) < static_cast<double>(b.w);
+}
+template <class G, class R>
+OS_HD int best_child_g(const Node<R>* nodes, int child_player, const GameCfg& g) {
+  const Node<R>& root = nodes[0];
+  if (root.nchild == 0) return -1;
+  int best = 0;
+  for (int k = 1; k < root.nchild; ++k)
+    if (final_less_g<G>(nodes[root.first + best], nodes[root.first + k], child_player, g))
+      best = k;
+  return best;
+}
+// The C-ABI's int8 outcome of a solved node for player p: the sign of its
+// Returns()[p] (== the value in two-player games; with n players +1 / -1 / 0
+// stand for 1, -1 / (n - 1) and 0, which the game fixes).
+template <class G>
+OS_HD int8_t out_sign(int8_t out, int p, const GameCfg& g) {
+  if (out == kUnsolved) return kUnsolved;
+  const double v = OutValue<G>::value(out, p, g);
+  return static_cast<int8_t>(v > 0.0 ? 1 : (v < 0.0 ? -1 : 0));
+}
+
 // Index (within the root's children) of BestChild(): std::max_element keeps
 // the first maximum (mcts.cc:125-141; mcts.py:160-162 max() likewise).
 template <class R>

@@ -160,6 +160,7 @@ _sig("os_az_fetch", ctypes.c_int, [_vp, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P
 _sig("os_engine_node_bytes", _i32, [_vp])
 _sig("os_engine_state_bytes", _i32, [_vp])
 _sig("os_make_roots", _i64, [_vp, _i64, _u32, _i32, _P, _P])
+_sig("os_sample_action", _i32, [_P, _i32, _P, _P])
 
 
 class SpielError(RuntimeError):

@@ -131,6 +131,18 @@ class SearchNode(object):
     return self.to_str(None)
 
 
+def _outcome_vector(code, nplayers):
+  """Returns() of a solved node from the engine's outcome code (os_games.h):
+  the player-0 value v of a two-player game ([v, -v]); with more players
+  (pig) 3 + w for a win by w (1 for w, -1 / (n - 1) for the others,
+  pig.cc:94-111) and 0 for nobody (all 0)."""
+  if nplayers == 2:
+    return [float(code), float(-code)]
+  if code >= 3:
+    return [1.0 if p == code - 3 else -1.0 / (nplayers - 1) for p in range(nplayers)]
+  return [0.0] * nplayers
+
+
 def tree_to_search_nodes(flat, state, game, root_action=None):
   """Materialises the engine's flat arena (os_engine_tree) as SearchNodes.
 
@@ -140,6 +152,7 @@ def tree_to_search_nodes(flat, state, game, root_action=None):
   Other priors are the uniform 1/|legal| of RandomRolloutEvaluator.prior;
   outcomes are [v, -v] vectors as the reference stores Returns().
   """
+  nplayers = game.num_players()
   first, n, w = flat["first"], flat["n"], flat["w"]
   action, nchild, out0 = flat["action"], flat["nchild"], flat["out0"]
   p0 = state.current_player()
@@ -152,8 +165,7 @@ def tree_to_search_nodes(flat, state, game, root_action=None):
     node.explore_count = int(n[idx])
     node.total_reward = float(w[idx])
     if out0[idx] != 2:
-      v = float(out0[idx])
-      node.outcome = [v, -v]
+      node.outcome = _outcome_vector(int(out0[idx]), nplayers)
     nc = int(nchild[idx])
     if nc:
       base = int(first[idx])

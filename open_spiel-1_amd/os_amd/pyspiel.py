@@ -103,7 +103,7 @@ _TYPES = {
                         info_string=False),
     3: _two_player_type("hex", "Hex", {"board_size": 11}),
     4: _two_player_type("go", "Go", {"komi": 7.5, "board_size": 19, "handicap": 0}),
-    # pig.cc:42-62 (this engine: two players)
+    # pig.cc:42-62 (2..10 players)
     5: GameType("pig", "Pig", GameType.Dynamics.SEQUENTIAL,
                 GameType.ChanceMode.EXPLICIT_STOCHASTIC,
                 GameType.Information.PERFECT_INFORMATION, GameType.Utility.ZERO_SUM,
@@ -149,7 +149,7 @@ class Game:
     return self._pig_dice() if self._info.kind == _PIG else 0
 
   def num_players(self):
-    return 2
+    return self._info.num_players
 
   def min_utility(self):
     return self._info.min_utility
@@ -198,7 +198,7 @@ class Game:
               "komi": self._info.komi}
     if k == _PIG:
       return {"diceoutcomes": self._pig_dice(), "horizon": self._info.max_game_length,
-              "players": 2, "winscore": self._info.cols - 1}
+              "players": self._info.num_players, "winscore": self._info.cols - 1}
     return {}
 
   def _pig_dice(self):
@@ -319,12 +319,12 @@ class State:
     raise SpielError("Illegal move: %s" % s)
 
   def returns(self):
-    r = np.zeros(2, np.float64)
+    r = np.zeros(self._game._info.num_players, np.float64)
     lib.os_state_returns(self._h, r.ctypes.data)
-    return [float(r[0]), float(r[1])]
+    return [float(x) for x in r]
 
   def rewards(self):
-    return self.returns() if self.is_terminal() else [0.0, 0.0]
+    return self.returns() if self.is_terminal() else [0.0] * self.num_players()
 
   def player_return(self, player):
     return self.returns()[player]
@@ -379,7 +379,7 @@ class State:
     return self._game.num_distinct_actions()
 
   def num_players(self):
-    return 2
+    return self._game.num_players()
 
   def get_game(self):
     return self._game
@@ -466,6 +466,41 @@ class RandomRolloutEvaluator(Evaluator):
   def __init__(self, n_rollouts, seed):
     self.n_rollouts = int(n_rollouts)
     self._state = _mt_key(seed)
+
+
+def evaluate_bots(state, bots, seed):
+  """pyspiel.evaluate_bots(state, bots, seed) (pyspiel.cc:724; EvaluateBots,
+  evaluate_bots.cc:24-61): plays to the end from `state`, chance nodes sampled
+  by SampleAction with a std::mt19937(seed) (absl::Uniform(rng, 0.0, 1.0),
+  os_sample_action); every other bot is informed of each move.  Returns
+  state.returns()."""
+  key, pos = _mt_key(seed)
+  pos_a = np.array([pos], np.int32)
+  if state.history():
+    for b in bots:
+      b.restart_at(state)
+  else:
+    for b in bots:
+      b.restart()
+  while not state.is_terminal():
+    if state.is_chance_node():
+      outs = state.chance_outcomes()
+      probs = np.array([p for _, p in outs], np.float64)
+      k = lib.os_sample_action(probs.ctypes.data, len(outs), key.ctypes.data,
+                               pos_a.ctypes.data)
+      if k < 0:
+        check(int(k))
+      action = outs[k][0]
+      for b in bots:
+        b.inform_action(state, PlayerId.CHANCE, action)
+    else:
+      mover = state.current_player()
+      action = bots[mover].step(state)
+      for p, b in enumerate(bots):
+        if p != mover:
+          b.inform_action(state, mover, action)
+    state.apply_action(action)
+  return state.returns()
 
 
 _ENGINES = {}

@@ -54,6 +54,10 @@ struct RootOut {
   int32_t* nodes;
 };
 
+// The int8 outcome of the C-ABI: the value (two players), or its sign (pig
+// with more players: 1, -1 / (n - 1), 0).
+int8_t Sign(double v) { return static_cast<int8_t>(v > 0 ? 1 : (v < 0 ? -1 : 0)); }
+
 void FillOut(const SearchNode& root, int max_children, int64_t r,
              const SearchStats& st, const RootOut& o) {
   int nc = static_cast<int>(root.children.size());
@@ -69,13 +73,11 @@ void FillOut(const SearchNode& root, int max_children, int64_t r,
     o.child_action[r * max_children + k] = static_cast<int32_t>(c.action);
     o.child_n[r * max_children + k] = c.explore_count;
     o.child_w[r * max_children + k] = c.total_reward;
-    o.child_out[r * max_children + k] =
-        c.outcome.empty() ? 2 : static_cast<int8_t>(c.outcome[c.player]);
+    o.child_out[r * max_children + k] = c.outcome.empty() ? 2 : Sign(c.outcome[c.player]);
   }
   o.root_n[r] = root.explore_count;
   o.root_w[r] = root.total_reward;
-  o.root_out[r] = root.outcome.empty() ? 2
-                                        : static_cast<int8_t>(root.outcome[root.player]);
+  o.root_out[r] = root.outcome.empty() ? 2 : Sign(root.outcome[root.player]);
   o.best_action[r] = nc > 0 ? root.BestChild().action : -1;
   o.nodes[r] = st.nodes;
 }
@@ -432,6 +434,44 @@ int oref_selfplay(void* g, int64_t num_games, const int64_t* start_actions,
     for (auto& t : ts) t.join();
   }
   return err.load() ? -1 : 0;
+}
+
+// mcts_test.cc:24-36 InitBot bots driven by EvaluateBots (evaluate_bots.cc:
+// 24-61): num_bots MCTSBots (seeds bot_seeds[i]) sharing ONE
+// RandomRolloutEvaluator(n_rollouts, eval_seed); chance nodes sampled by
+// SampleAction(outcomes, absl::Uniform(mt19937(seed), 0.0, 1.0)).  Writes the
+// game's actions (history[cap]) and Returns() (returns[num_players]); returns
+// the history length, or -1 when it exceeds cap.
+int64_t oref_evaluate_mcts_bots(void* g, int32_t num_bots, const uint32_t* bot_seeds,
+                                int32_t n_rollouts, uint32_t eval_seed, double uct_c,
+                                int32_t max_simulations, int64_t max_memory_mb, int32_t solve,
+                                uint32_t seed, int64_t* history, int64_t cap,
+                                double* returns) {
+  auto* og = static_cast<OGame*>(g);
+  RandomRolloutEvaluator ev(n_rollouts, eval_seed);
+  std::vector<std::unique_ptr<MCTSBot>> bots;
+  for (int i = 0; i < num_bots; ++i)
+    bots.push_back(std::make_unique<MCTSBot>(*og->game, &ev, uct_c, max_simulations,
+                                             max_memory_mb, solve != 0, bot_seeds[i]));
+  std::mt19937 rng(seed);
+  auto state = og->game->NewInitialState();
+  int64_t m = 0;
+  while (!state->IsTerminal()) {
+    Action a;
+    if (state->IsChanceNode()) {
+      a = SampleAction(state->ChanceOutcomes(), AbslUniformDouble01(rng));
+    } else {
+      SearchStats st;
+      auto root = bots[state->CurrentPlayer()]->MCTSearch(*state, &st);
+      a = root->BestChild().action;  // MCTSBot::Step (mcts.cc:219-226)
+    }
+    if (m >= cap) return -1;
+    history[m++] = a;
+    state->ApplyAction(a);
+  }
+  const auto r = state->Returns();
+  for (size_t i = 0; i < r.size(); ++i) returns[i] = r[i];
+  return m;
 }
 
 }  // extern "C"

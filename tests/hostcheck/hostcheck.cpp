@@ -62,12 +62,12 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
     child_action[k] = c.action;
     child_n[k] = c.n;
     child_w[k] = static_cast<double>(c.w);
-    child_out[k] = c.out == kUnsolved ? kUnsolved : (P0 == 0 ? c.out : -c.out);
+    child_out[k] = out_sign<G>(c.out, P0, game.cfg);
   }
   *root_n = rn.n;
   *root_w = static_cast<double>(rn.w);
-  *root_out = rn.out == kUnsolved ? kUnsolved : (P0 == 0 ? rn.out : -rn.out);
-  const int b = best_child(nodes.data(), P0);
+  *root_out = out_sign<G>(rn.out, P0, game.cfg);
+  const int b = best_child_g<G>(nodes.data(), P0, game.cfg);
   *best_action = b < 0 ? -1 : nodes[rn.first + b].action;
   *nodes_out = res.nodes;
   return 0;
@@ -78,7 +78,7 @@ int Dispatch(const HostGame& game, const HostState& root, const SearchParams& sp
              int policy, uint32_t bs, uint32_t es, uint32_t cap, int32_t mc, int32_t* ca,
              int32_t* cn, double* cw, int8_t* co, int32_t* nch, int32_t* rn,
              double* rw, int8_t* ro, int64_t* ba, int32_t* nd) {
-  if (sp.n_rollouts == 1) {
+  if (sp.n_rollouts == 1 && game.cfg.pig_players <= 2) {  // else f64 node rewards
     if (policy == kPolicyCpp)
       return RunOne<G, int32_t, kPolicyCpp>(game, root, sp, bs, es, cap, mc, ca, cn, cw,
                                             co, nch, rn, rw, ro, ba, nd);

@@ -80,6 +80,11 @@ def lib():
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
         _u32p, ctypes.c_int32, _i64p, _i32p, _f64p, ctypes.c_void_p, ctypes.c_int32]
+    L.oref_evaluate_mcts_bots.restype = ctypes.c_int64
+    L.oref_evaluate_mcts_bots.argtypes = [
+        ctypes.c_void_p, ctypes.c_int32, _u32p, ctypes.c_int32, ctypes.c_uint32,
+        ctypes.c_double, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32,
+        _i64p, ctypes.c_int64, _f64p]
     _lib = L
   return _lib
 
@@ -241,6 +246,20 @@ class Game:
     if rc:
       raise RuntimeError("oref_selfplay: game longer than max_len")
     return out
+
+
+def evaluate_mcts_bots(game_string, bot_seeds, n_rollouts, eval_seed, seed, uct_c=2.0,
+                       max_simulations=100, max_memory_mb=5, solve=True, num_players=2):
+  """EvaluateBots over MCTSBots sharing one RandomRolloutEvaluator
+  (mcts_test.cc:24-36 InitBot): (history, returns)."""
+  g = Game(game_string)
+  hist = np.zeros(100000, np.int64)
+  ret = np.zeros(num_players, np.float64)
+  n = lib().oref_evaluate_mcts_bots(
+      g._h, len(bot_seeds), np.ascontiguousarray(bot_seeds, dtype=np.uint32), n_rollouts,
+      eval_seed, uct_c, max_simulations, max_memory_mb, int(solve), seed, hist, len(hist), ret)
+  assert n >= 0
+  return [int(a) for a in hist[:n]], [float(x) for x in ret]
 
 
 def mt19937(seed, n):

@@ -3,7 +3,7 @@ the oracle, which the reference's own pig playthroughs pin (test_oracle.py)
 and the unmodified reference mcts.py pins on the numpy path
 (test_python_goldens.py, python_mcts_pig*.json).
 
-  * CPU: the product's host State API (two-player pig) equals the oracle's on
+  * CPU: the product's host State API (pig, 2..5 players) equals the oracle's on
     random games; the search engine compiled for the host (csrc/os_chance.h)
     equals the oracle's MCTSBot / numpy bot; product rollouts equal the
     oracle's RandomRolloutEvaluator.
@@ -18,7 +18,12 @@ import oracle_lib as O
 from os_amd import engine as E
 from os_amd import pyspiel
 
-PIGS = ["pig", "pig(horizon=30,winscore=8)", "pig(diceoutcomes=4,winscore=25)"]
+PIGS = ["pig", "pig(horizon=30,winscore=8)", "pig(diceoutcomes=4,winscore=25)",
+        # more than two players (pig.cc:94-111 returns, round-robin turns)
+        "pig(horizon=30,players=3,winscore=20)", "pig(horizon=40,players=4,winscore=12)",
+        "pig(diceoutcomes=4,horizon=50,players=5,winscore=10)"]
+NP = {"pig(horizon=30,players=3,winscore=20)": 3, "pig(horizon=40,players=4,winscore=12)": 4,
+      "pig(diceoutcomes=4,horizon=50,players=5,winscore=10)": 5}
 
 
 def _random_games(gs, n, seed):
@@ -95,6 +100,8 @@ def test_engine_cpp_policy_matches_oracle(gs, n_rollouts, solve):
 
 @pytest.mark.parametrize("gs", PIGS)
 def test_engine_rollouts_match_oracle(gs):
+  if gs in NP:
+    pytest.skip("rollout batches return two players' values")
   seeds = np.arange(200, dtype=np.uint32)
   for hist in ([], [0], [0, 3], [1, 0, 4]):
     np.testing.assert_array_equal(H.rollouts(gs, hist, seeds),
@@ -112,6 +119,24 @@ def test_solver_proves_short_games():
   for k in H.KEYS:
     np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
   assert (ref["root_out"] == 0).all()  # proven through chance nodes
+
+
+@pytest.mark.parametrize("gs", sorted(NP))
+def test_n_player_api(gs):
+  n = NP[gs]
+  g = pyspiel.load_game(gs)
+  assert g.num_players() == n and g.get_parameters()["players"] == n
+  assert g.observation_tensor_shape()[0] == 1 + n
+  for hist, st in _random_games(gs, 3, 11):
+    r = st.returns()
+    assert len(r) == n
+    if st.is_terminal():
+      assert abs(sum(r)) < 1e-12
+      if max(r) > 0:
+        assert sorted(r)[:-1] == [-1.0 / (n - 1)] * (n - 1)
+    else:
+      assert st.current_player() in list(range(n)) + [pyspiel.PlayerId.CHANCE]
+      assert len(st.observation_tensor(n - 1)) == (1 + n) * (g.get_parameters()["winscore"] + 1)
 
 
 def test_chance_node_api():
@@ -183,3 +208,47 @@ def test_gpu_cpp_bot_plays_pig(require_gpu):
     else:
       st.apply_action(bots[st.current_player()].step(st))
   assert st.returns() in ([1.0, -1.0], [-1.0, 1.0])
+
+
+def test_sample_action_follows_absl_uniform_double():
+  """os_sample_action = SampleAction(outcomes, absl::Uniform(rng, 0.0, 1.0))
+  (spiel.cc:337-366) on a caller-held std::mt19937, as EvaluateBots samples
+  chance nodes (evaluate_bots.cc:32-37)."""
+  import ctypes
+  from os_amd import _lib
+  zs = H.absl_double(42, 300)
+  key, pos = pyspiel._mt_key(42)
+  pos_a = np.array([pos], np.int32)
+  rs = np.random.RandomState(9)
+  for i in range(300):
+    n = int(rs.randint(1, 7))
+    p = rs.dirichlet([1.0] * n)
+    p[-1] = 1.0 - p[:-1].sum() if n > 1 else 1.0
+    k = _lib.lib.os_sample_action(p.ctypes.data, n, key.ctypes.data, pos_a.ctypes.data)
+    acc, want = 0.0, None
+    for j in range(n):
+      if acc <= zs[i] < acc + p[j]:
+        want = j
+        break
+      acc += p[j]
+    assert k == (want if want is not None else -1), i
+
+
+@pytest.mark.gpu
+def test_gpu_three_player_pig_as_mcts_test(require_gpu):
+  """mcts_test.cc:73-84 MCTSTest_CanPlayThreePlayerStochasticGames on the
+  drop-in: three pyspiel.MCTSBot(uct_c 2, 1000 sims, max_memory_mb 5, solve,
+  seed 42) sharing RandomRolloutEvaluator(20, 42), pyspiel.evaluate_bots(...,
+  42).  The whole game (every chance draw and every bot move) equals the
+  oracle's EvaluateBots, and the returns sum to 0 as the reference asserts."""
+  gs = "pig(players=3,winscore=20,horizon=30)"
+  g = pyspiel.load_game(gs)
+  ev = pyspiel.RandomRolloutEvaluator(20, 42)
+  bots = [pyspiel.MCTSBot(g, ev, 2.0, 1000, 5, True, 42, False) for _ in range(3)]
+  st = g.new_initial_state()
+  ret = pyspiel.evaluate_bots(st, bots, 42)
+  assert abs(sum(ret)) < 1e-12
+  hist, ref = O.evaluate_mcts_bots(gs, [42, 42, 42], 20, 42, 42, uct_c=2.0,
+                                   max_simulations=1000, max_memory_mb=5, num_players=3)
+  assert st.history() == hist
+  assert ret == ref

@@ -46,8 +46,9 @@ CASES = _cases()
 
 
 def _child_out(o, player):
-  """Batch outputs hold a child's outcome from its own player's view."""
-  return 2 if o is None else int(o[player])
+  """Batch outputs hold a child's outcome from its own player's view (its
+  sign with more than two players: 1, -1 / (n - 1), 0)."""
+  return 2 if o is None else int(np.sign(o[player]))
 
 
 def _fingerprint(rs):

@@ -137,6 +137,9 @@ def main():
       # trees reach terminal states (solver, chance-node proof rule)
       "pig": dict(positions=[[], [0, 4, 0, 3], [1, 0, 5, 1]], seeds=[0, 42], sims=300),
       "pig(horizon=30,winscore=8)": dict(positions=[[], [0, 5]], seeds=[0, 42], sims=1000),
+      # three players (mcts_test.cc:73's game; Returns -1 / (n - 1) for losers)
+      "pig(horizon=30,players=3,winscore=20)": dict(positions=[[], [0, 6, 1]], seeds=[0, 42],
+                                                    sims=500),
   }
   if args.puct:
     plan = {
