@@ -693,8 +693,21 @@ def _oracle(game):
   return oracle_lib.Game(game)
 
 
-CALIBRATION = ("uncalibrated restatement: the reference mcts.cc cannot be built "
-               "here (abseil absent), so no reference/restatement speed ratio exists")
+def calibration(game):
+  """Restatement/reference CPU speed ratio for `game`, measured in the build
+  container by tools/calibrate_cpu.py against SURVEY.md §6's single-core
+  probes of the (shim-built) reference mcts.cc on the same CPU."""
+  path = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+  key = game if game.startswith("go") else game.split("(")[0]
+  try:
+    with open(path) as f:
+      g = json.load(f)["games"][key]
+  except (OSError, KeyError, ValueError):
+    return "uncalibrated: no profiles/cpu_calibration.json entry for %s" % game
+  return {"oracle_over_reference": g["ratio"], "oracle_sims_per_s_1core": g["oracle_sims_per_s"],
+          "reference_sims_per_s_1core": g["reference_sims_per_s"], "sims": g["sims"],
+          "conditions": "initial position, seeds 1-3, one thread, build container",
+          "source": "profiles/cpu_calibration.json (tools/calibrate_cpu.py; SURVEY.md §6)"}
 
 
 def host_cores():
@@ -733,8 +746,10 @@ def cpu_baseline_search(game, acts, offs, bot_seeds, eval_seeds, sims, seconds):
     secs, n = og.time_mcts_batch(acts[:offs[want]], offs[:want + 1], bot_seeds[:want],
                                  eval_seeds[:want], max_simulations=sims, threads=threads)
     total_s, total_n, passes = total_s + secs, total_n + n, passes + 1
+  cal = calibration(game)
+  ref_eq = (total_n / total_s / cal["oracle_over_reference"]) if isinstance(cal, dict) else None
   return {"value": total_n / total_s, "unit": "sims/s", "cores": threads, "kind": "port",
-          "calibration": CALIBRATION,
+          "calibration": cal, "reference_equivalent": ref_eq,
           "sample": "%d pass(es) over %d of the %d roots x %d sims (%d sims, %.1f s), "
                     "oracle restatement of mcts.cc; %s" %
                     (passes, want, R, sims, total_n, total_s, cores_desc)}
@@ -760,7 +775,7 @@ def cpu_baseline_playouts(game, seconds):
     t.join()
   secs = time.perf_counter() - t0
   return {"value": threads * n_per / secs, "unit": "playouts/s", "cores": threads,
-          "kind": "port", "calibration": CALIBRATION,
+          "kind": "port", "calibration": calibration(game),
           "sample": "%d playouts (seeds 0..%d), %.1f s, oracle restatement of "
                     "RandomRolloutEvaluator; %s" % (threads * n_per, threads * n_per - 1,
                                                     secs, cores_desc)}

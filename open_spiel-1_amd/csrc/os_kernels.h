@@ -169,11 +169,18 @@ struct WaveCtxMaker<Go> {
   }
 };
 
+// Arena nodes of each search kept in LDS by the wave kernel (os_wave.h
+// NodeCache): the first OS_NODE_CACHE nodes, i.e. the tree's top levels.
+#ifndef OS_NODE_CACHE
+#define OS_NODE_CACHE 0  // A/B: 128 / 256 / 512 were no faster
+#endif
+
 template <class G, class R>
 __host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
   return static_cast<size_t>(2 * kMtN * 4) + kPageDescLds +
          static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
-         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
+         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0) +
+         static_cast<size_t>(OS_NODE_CACHE) * sizeof(Node<R>) + 16;
 }
 
 // Minimum waves per SIMD requested from the register allocator (A/B knob).
@@ -202,8 +209,12 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
   // [MT bot | MT evaluator | page descriptor address | path | go log]
   PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4 + kPageDescLds);
-  uint64_t* glog = reinterpret_cast<uint64_t*>(
-      smem + ((2 * kMtN * 4 + kPageDescLds + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  const size_t glog_off =
+      (2 * kMtN * 4 + kPageDescLds + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7);
+  uint64_t* glog = reinterpret_cast<uint64_t*>(smem + glog_off);
+  // [... | node cache], 16-byte aligned
+  Node<R>* lcache = reinterpret_cast<Node<R>*>(
+      smem + ((glog_off + (G::State::kNeedsLog ? kGoLogCap * 8 + 8 : 0) + 15) & ~size_t(15)));
   if (l == 0)
     *reinterpret_cast<uint64_t*>(smem + 2 * kMtN * 4) = reinterpret_cast<uintptr_t>(a.pages);
   const bool shared = Policy == kPolicyNumpy && a.shared_stream;
@@ -233,10 +244,10 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   PhaseCycles ph = {};  // paged: the root's page is page lr = blockIdx.x
   SearchResult res = shared
-      ? wave_search<G, R, Policy, kPaged, kPuct>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot,
-                                                 bot, path, a.path_cap, ph)
-      : wave_search<G, R, Policy, kPaged, kPuct>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot,
-                                                 ev, path, a.path_cap, ph);
+      ? wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE>(
+            a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path, a.path_cap, ph, lcache)
+      : wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE>(
+            a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path, a.path_cap, ph, lcache);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
   ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);

@@ -1342,16 +1342,33 @@ struct LanePath {
   }
 };
 
+// LDS copy of the search's first kCache arena nodes (os_kernels.h
+// OS_NODE_CACHE).  Nodes are allocated in expansion order, so these are the
+// tree's top levels, which every simulation walks: selection reads a child
+// block that lies wholly below kCache from LDS instead of HBM / MALL.  Every
+// store to such a node is written through to both copies.
+template <class R, int K>
+struct NodeCache {
+  Node<R>* c;
+  __device__ __forceinline__ bool has(uint32_t i) const { return K > 0 && i < static_cast<uint32_t>(K); }
+  __device__ __forceinline__ bool block(uint32_t first, int n) const {
+    return K > 0 && first + static_cast<uint32_t>(n) <= static_cast<uint32_t>(K);
+  }
+};
+
 // One search, executed by the whole wave.  `path` (LDS) has path_cap
 // entries.  Same contract as mcts_search; kPuct selects children by
-// PUCTValue (sp.log_lut then holds sqrt(N)).
-template <class G, class R, int Policy, bool kPageable = false, bool kPuct = false, class C>
+// PUCTValue (sp.log_lut then holds sqrt(N)); kCache > 0: `lcache` (LDS)
+// holds the first kCache nodes (NodeCache).
+template <class G, class R, int Policy, bool kPageable = false, bool kPuct = false,
+          int kCache = 0, class C>
 __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     const typename G::State& root, C& ctx,
                                     Node<R>* nodes, uint32_t cap, WaveMt& bot,
                                     WaveMt& ev, PathEnt<R>* path, int path_cap,
-                                    PhaseCycles& ph) {
+                                    PhaseCycles& ph, Node<R>* lcache = nullptr) {
   const int l = lane_id();
+  const NodeCache<R, kCache> nc_ = {lcache};
   const uint64_t t_begin = OS_PH_NOW();
   SearchResult res;
   res.status = kOk;
@@ -1373,6 +1390,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     nodes[0].action = 0;
     nodes[0].nchild = 0;
     nodes[0].out = kUnsolved;
+    if (kCache > 0) nc_.c[0] = nodes[0];
   }
   // Root statistics persist in registers across simulations.
   uint32_t root_first = 0;
@@ -1485,11 +1503,16 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             c.action = static_cast<uint16_t>(h == 0 ? acts.a0 : acts.a1);
             c.nchild = 0;
             c.out = kUnsolved;
+            if (nc_.has(first + k)) nc_.c[first + k] = c;
           }
         }
         if (l == 0) {
           nodes[cur_idx].first = first;
           nodes[cur_idx].nchild = static_cast<uint8_t>(nc);
+          if (nc_.has(cur_idx)) {
+            nc_.c[cur_idx].first = first;
+            nc_.c[cur_idx].nchild = static_cast<uint8_t>(nc);
+          }
         }
         if (depth == 0) {
           root_first = first;
@@ -1552,10 +1575,13 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         } else {
           // Every lane loads (lanes past the last child re-read child 0, so
           // no exec-mask branch); their values are masked by in0 / in1.
-          c0 = load_node(nodes + cur_first + (in0 ? l : 0));
+          // A block of the cached top levels comes from LDS (wave-uniform).
+          const Node<R>* src = nc_.block(cur_first, cur_nc) ? nc_.c : nodes;
+          if (nc_.block(cur_first, cur_nc)) c0 = load_node(nc_.c + cur_first + (in0 ? l : 0));
+          else c0 = load_node(nodes + cur_first + (in0 ? l : 0));
           lg0 = sp.log_lut[c0.n];
           if (in1) {
-            c1 = load_node(nodes + cur_first + l + 64);
+            c1 = load_node(src + cur_first + l + 64);
             lg1 = sp.log_lut[c1.n];
           }
         }
@@ -1643,7 +1669,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       if (G::terminal(s, g)) {
         const int r0 = G::ret0(s, g, ctx);
         leaf_out = static_cast<int8_t>(r0);
-        if (l == 0) nodes[cur_idx].out = leaf_out;
+        if (l == 0) {
+          nodes[cur_idx].out = leaf_out;
+          if (nc_.has(cur_idx)) nc_.c[cur_idx].out = leaf_out;
+        }
         if (depth == 1 && l == (root_k & 63)) {
           if (root_k < 64) rc0.out = leaf_out;
           else rc1.out = leaf_out;
@@ -1680,9 +1709,16 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         if (l <= depth) {  // lane 0 stores the root
           const bool rt = l == 0;
           const int pl = rt ? P0 : (P0 ^ ((l - 1) & 1));
-          Node<R>& nd = nodes[rt ? 0u : lp.idx];
-          nd.n = (rt ? root_n : lp.n) + 1;
-          nd.w = (rt ? root_w : lp.w) + (pl == 0 ? rv0 : rv1);
+          const uint32_t ix = rt ? 0u : lp.idx;
+          Node<R>& nd = nodes[ix];
+          const int32_t nn = (rt ? root_n : lp.n) + 1;
+          const R nw = (rt ? root_w : lp.w) + (pl == 0 ? rv0 : rv1);
+          nd.n = nn;
+          nd.w = nw;
+          if (nc_.has(ix)) {
+            nc_.c[ix].n = nn;
+            nc_.c[ix].w = nw;
+          }
         }
       } else for (int d0 = 1; d0 <= depth; d0 += 64) {
         const int d = d0 + l;
@@ -1692,6 +1728,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           Node<R>& nd = nodes[pe.idx];
           nd.n = pe.n + 1;
           nd.w = pe.w + (pl == 0 ? rv0 : rv1);
+          if (nc_.has(pe.idx)) {
+            nc_.c[pe.idx].n = pe.n + 1;
+            nc_.c[pe.idx].w = pe.w + (pl == 0 ? rv0 : rv1);
+          }
         }
       }
       root_n += 1;
@@ -1719,6 +1759,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       if (!kLP && l == 0) {
         nodes[0].n = root_n;
         nodes[0].w = root_w;
+        if (kCache > 0) {
+          nc_.c[0].n = root_n;
+          nc_.c[0].w = root_w;
+        }
       }
       OS_PH_ADD(ph.c[kPhBackup], t_ph);
       t_ph = OS_PH_NOW();
@@ -1754,7 +1798,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
             if (k < nnc) {
               co = (nfirst + k == prev_idx)
                        ? prev_out
-                       : (d == 0 ? (h == 0 ? rc0.out : rc1.out) : nodes[nfirst + k].out);
+                       : (d == 0 ? (h == 0 ? rc0.out : rc1.out)
+                                 : (nc_.block(nfirst, nnc) ? nc_.c[nfirst + k].out
+                                                           : nodes[nfirst + k].out));
             }
             const bool uns = k < nnc && co == kUnsolved;
             if (ballot(uns)) any_unsolved = true;
@@ -1765,7 +1811,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           }
           if (best_v > -128 && (!any_unsolved || best_v == 1)) {
             const int8_t no = static_cast<int8_t>(cpl == 0 ? best_v : -best_v);
-            if (l == 0) nodes[nidx].out = no;
+            if (l == 0) {
+              nodes[nidx].out = no;
+              if (nc_.has(nidx)) nc_.c[nidx].out = no;
+            }
             if (d == 0) root_out = no;
             if (d == 1 && l == (root_k & 63)) {
               if (root_k < 64) rc0.out = no;
@@ -1800,6 +1849,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     (nodes_count > sp.max_nodes / 2 ? 1.25 : 0.9));
         if (gc_limit < 5) gc_limit = 5;
         __threadfence_block();
+        if (kCache > 0) {  // GC rewrote nchild fields: refresh the LDS copy
+          for (int i = l; i < kCache && i < static_cast<int>(used); i += 64) nc_.c[i] = nodes[i];
+          __builtin_amdgcn_wave_barrier();
+        }
         root_nc = nodes[0].nchild;
         root_first = nodes[0].first;
         // GC may have detached root children's subtrees: reload the mirror.
