@@ -273,6 +273,34 @@ int os_selfplay(os_engine* e, const os_mcts_params* p, int64_t num_games,
  * fetch then requires (NULL skips the copy). */
 #define OS_RECORD_VISITS 1
 #define OS_RECORD_OBSERVATIONS 2
+#define OS_RECORD_POLICY 4       /* f64 [G][max_len][A]: the normalised move policy */
+#define OS_RECORD_ROOT_VALUES 8  /* f64 [G][max_len]: root total_reward / explore_count */
+
+/* AlphaZero's PlayGame move choice (alpha_zero.cc:64-118) for the next
+ * os_selfplay_prepare on this engine.  Each move's policy over the root's
+ * children is pow(explore_count, 1 / temperature), normalised
+ * (NormalizePolicy, spiel.cc:327-335); while fewer than temperature_drop
+ * moves have been played in the game the action is SampleAction(policy,
+ * actor rng) (absl::Uniform(rng, 0.0, 1.0), spiel.cc:337-366), then BestChild.
+ * The root value is root total_reward / explore_count.  With resign != 0,
+ * the game's cutoff is drawn at its start from the same actor rng
+ * (alpha_zero.cc:154-157: u < cutoff_probability ? cutoff_value :
+ * MaxUtility + 1) and the game stops after a move whose |root value| exceeds
+ * it, returns[mover] = root value, returns[other] = -root value (:105-110).
+ * actor_seeds[g] seeds game g's std::mt19937 actor rng.  temperature <= 0
+ * restores the default (BestChild every move, mcts_example.cc); the policy
+ * and root values are then still recorded, with exponent 1. */
+typedef struct {
+  double temperature;
+  int32_t temperature_drop;
+  int32_t resign;
+  double cutoff_value;
+  double cutoff_probability;
+} os_selfplay_options;
+int os_selfplay_set_options(os_engine* e, const os_selfplay_options* options,
+                            int64_t num_games, const uint32_t* actor_seeds);
+/* The recorded targets of the last fetched self-play run (NULL skips). */
+int os_selfplay_fetch_targets(os_engine* e, double* policy, double* root_values);
 int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games,
                         const int64_t* start_actions, const int64_t* start_offsets,
                         const uint32_t* bot_seeds, const uint32_t* eval_seeds,

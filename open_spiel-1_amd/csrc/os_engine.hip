@@ -563,12 +563,14 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
               const uint32_t* eval_seeds, int32_t max_len, int32_t record) {
   const bool with_visits = (record & OS_RECORD_VISITS) != 0;
   const bool with_obs = (record & OS_RECORD_OBSERVATIONS) != 0;
+  const bool with_policy = (record & OS_RECORD_POLICY) != 0;
+  const bool with_values = (record & OS_RECORD_ROOT_VALUES) != 0;
+  if (!e->sp_actor_seeds.empty() && static_cast<int64_t>(e->sp_actor_seeds.size()) != G)
+    return Fail(OS_ERR_INVALID, "os_selfplay_set_options was given a different game count");
   int rc = CheckParams(e, p);
   if (rc) return rc;
   if (p->policy != OS_POLICY_CPP)
     return Fail(OS_ERR_UNSUPPORTED, "self-play implements the C++ MCTSBot policy only");
-  if (p->child_selection != OS_SELECT_UCT)
-    return Fail(OS_ERR_UNSUPPORTED, "self-play with the random-rollout evaluator runs UCT");
   if (G < 0 || max_len < 0) return Fail(OS_ERR_INVALID, "negative size");
   if (G > 0 && (!bot_seeds || !eval_seeds || !start_offsets))
     return Fail(OS_ERR_INVALID, "null argument");
@@ -624,9 +626,25 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
                       hipMemcpyHostToDevice));
   }
   std::vector<double> lut(static_cast<size_t>(p->max_simulations) + 2);
-  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  const bool puct = p->child_selection == OS_SELECT_PUCT;
+  for (size_t i = 0; i < lut.size(); ++i)
+    lut[i] = puct ? std::sqrt(static_cast<double>(i)) : std::log(static_cast<double>(i));
   if ((rc = e->d_lut.ensure(lut.size() * 8))) return rc;
   HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice));
+  // AlphaZero move choice: pow(explore_count, 1 / T) from the host libm
+  // (alpha_zero.cc:82-83), and the actor rng seeds.
+  if (e->sp_opts.temperature > 0.0) {
+    std::vector<double> pw(lut.size());
+    const double ex = 1.0 / e->sp_opts.temperature;
+    for (size_t i = 0; i < pw.size(); ++i) pw[i] = std::pow(static_cast<double>(i), ex);
+    if ((rc = e->d_sp_pow.ensure(pw.size() * 8))) return rc;
+    HIP_TRY(hipMemcpy(e->d_sp_pow.p, pw.data(), pw.size() * 8, hipMemcpyHostToDevice));
+  }
+  if (!e->sp_actor_seeds.empty()) {
+    if ((rc = e->d_sp_actor.ensure(e->sp_actor_seeds.size() * 4))) return rc;
+    HIP_TRY(hipMemcpy(e->d_sp_actor.p, e->sp_actor_seeds.data(), e->sp_actor_seeds.size() * 4,
+                      hipMemcpyHostToDevice));
+  }
   const size_t L = static_cast<size_t>(std::max(max_len, 1));
   const size_t A = static_cast<size_t>(cfg.num_actions);
   if ((rc = e->d_arena.ensure(static_cast<size_t>(e->chunk_roots) * per_game)) ||
@@ -634,12 +652,16 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
       (rc = e->d_sp_act.ensure(Gz * L * 4)) || (rc = e->d_sp_len.ensure(Gz * 4)) ||
       (rc = e->d_sp_ret.ensure(Gz * 16)) ||
       (with_visits && (rc = e->d_sp_vis.ensure(Gz * L * A * 4))) ||
-      (with_obs && (rc = e->d_sp_obs.ensure(Gz * L * ObservationShape(e->game, nullptr) * 4))))
+      (with_obs && (rc = e->d_sp_obs.ensure(Gz * L * ObservationShape(e->game, nullptr) * 4))) ||
+      (with_policy && (rc = e->d_sp_pol.ensure(Gz * L * A * 8))) ||
+      (with_values && (rc = e->d_sp_val.ensure(Gz * L * 8))))
     return rc;
   e->sp_games = G;
   e->sp_max_len = max_len;
   e->sp_visits = with_visits;
   e->sp_obs = with_obs;
+  e->sp_policy = with_policy;
+  e->sp_values = with_values;
   e->sp_ready = true;
   e->num_roots = 0;       // the search buffers now hold no prepared batch
   e->roll_ready = false;
@@ -1287,6 +1309,39 @@ int os_selfplay_prepare(os_engine* e, const os_mcts_params* p, int64_t num_games
   if (!e) return Fail(OS_ERR_INVALID, "null engine");
   return SpPrepare(e, p, num_games, start_actions, start_offsets, bot_seeds, eval_seeds,
                    max_len, record);
+}
+
+int os_selfplay_set_options(os_engine* e, const os_selfplay_options* o, int64_t num_games,
+                            const uint32_t* actor_seeds) {
+  if (!e || !o) return Fail(OS_ERR_INVALID, "null argument");
+  if (o->temperature > 0.0 && !(o->temperature < 1e300))
+    return Fail(OS_ERR_INVALID, "temperature must be finite");
+  if (o->resign && (!(o->cutoff_probability >= 0.0) || o->cutoff_probability > 1.0))
+    return Fail(OS_ERR_INVALID, "cutoff_probability must be in [0, 1]");
+  if (num_games < 0 || (num_games > 0 && !actor_seeds))
+    return Fail(OS_ERR_INVALID, "actor seeds needed for every game");
+  e->sp_opts = *o;
+  e->sp_actor_seeds.assign(actor_seeds, actor_seeds + num_games);
+  e->sp_ready = false;  // takes effect at the next os_selfplay_prepare
+  return OS_OK;
+}
+
+int os_selfplay_fetch_targets(os_engine* e, double* policy, double* root_values) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (!e->sp_ready) return Fail(OS_ERR_INVALID, "os_selfplay_prepare was not called");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t GL = static_cast<size_t>(e->sp_games) * e->sp_max_len;
+  if (policy) {
+    if (!e->sp_policy) return Fail(OS_ERR_INVALID, "prepared without OS_RECORD_POLICY");
+    HIP_TRY(hipMemcpy(policy, e->d_sp_pol.p, GL * e->game.cfg.num_actions * 8,
+                      hipMemcpyDeviceToHost));
+  }
+  if (root_values) {
+    if (!e->sp_values) return Fail(OS_ERR_INVALID, "prepared without OS_RECORD_ROOT_VALUES");
+    HIP_TRY(hipMemcpy(root_values, e->d_sp_val.p, GL * 8, hipMemcpyDeviceToHost));
+  }
+  return OS_OK;
 }
 
 int os_selfplay_run_async(os_engine* e, void* hip_stream) {

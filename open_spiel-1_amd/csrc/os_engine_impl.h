@@ -110,6 +110,18 @@ struct SpArgs {
   float* obs;             // [total][max_len][obs_size] or null
   int32_t obs_size;       // C * H * W
   SearchResult* results;  // [total], summed over the game's searches
+  // AlphaZero PlayGame move choice (alpha_zero.cc:64-118; os_selfplay_set_
+  // options): policy = pow(explore_count, 1 / T) over the root's children,
+  // normalised; SampleAction from the game's actor rng before
+  // temperature_drop moves, BestChild after; resign when |root value| >
+  // the game's cutoff.  actor_seeds == null: BestChild every move.
+  const uint32_t* actor_seeds;  // [total]
+  const double* pow_lut;        // pow(n, 1 / T), n in [0, max_simulations]
+  int32_t temperature_drop;
+  int32_t resign;               // draw the cutoff at game start, apply it
+  double cutoff_value, cutoff_probability, max_utility;
+  double* policy;               // [total][max_len][num_actions] or null
+  double* root_value;           // [total][max_len] or null
 };
 
 // ---------------------------------------------------------------------------
@@ -227,6 +239,10 @@ struct os_engine {
   bool sp_visits = false;
   bool sp_obs = false;
   bool sp_ready = false;
+  bool sp_policy = false;   // OS_RECORD_POLICY
+  bool sp_values = false;   // OS_RECORD_ROOT_VALUES
+  os_selfplay_options sp_opts{};  // os_selfplay_set_options
+  std::vector<uint32_t> sp_actor_seeds;
   // prepared external-evaluator batch (os_az_*): caller-owned device buffers
   bool az_ready = false;
   int32_t az_puct = 0;
@@ -242,7 +258,8 @@ struct os_engine {
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
-      d_sp_obs, d_glog, d_glink, d_roll_cnt, d_rp_sum, d_rp_all;
+      d_sp_obs, d_glog, d_glink, d_roll_cnt, d_rp_sum, d_rp_all, d_sp_pol, d_sp_val,
+      d_sp_actor, d_sp_pow;
   std::vector<osm::SearchResult> last_results;
   int64_t last_sims = 0;
   // Paged arena (os_engine_set_arena_mode).  arena_mode is the
@@ -268,7 +285,8 @@ struct os_engine {
                      &d_rout,  &d_best,  &d_rollout_out, &d_dense_n, &d_dense_w,
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
-                     &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next};
+                     &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
+                     &d_sp_actor, &d_sp_pow};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

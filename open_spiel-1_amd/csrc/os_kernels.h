@@ -323,11 +323,53 @@ struct SpCtx<Go> {
 
 template <class G, class R>
 __host__ __device__ constexpr size_t SelfPlayLdsBytes(int path_cap) {
-  return static_cast<size_t>(3 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+  return static_cast<size_t>(4 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
          (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
 }
 
-template <class G, class R>
+// AlphaZero's move choice (alpha_zero.cc:77-95) from the root's children
+// (lane k holds child k in slot 0, k + 64 in slot 1): the action index in the
+// child block, with the normalised policy (lane-distributed) and the root
+// value.  Sums run serially in child order, as NormalizePolicy and
+// SampleAction add them (spiel.cc:327-366).
+struct AzChoice {
+  int child;
+  double p0, p1;
+};
+template <class R>
+__device__ AzChoice az_choose(const SpArgs& a, const Node<R>* kids, int rnc, bool sample,
+                              WaveMt& act, int best) {
+  const int l = lane_id();
+  const int32_t n0 = l < rnc ? kids[l].n : 0;
+  const int32_t n1 = l + 64 < rnc ? kids[l + 64].n : 0;
+  const double* lut = a.pow_lut;
+  double p0 = l < rnc ? (lut ? lut[n0] : static_cast<double>(n0)) : 0.0;
+  double p1 = l + 64 < rnc ? (lut ? lut[n1] : static_cast<double>(n1)) : 0.0;
+  double sum = 0.0;
+  for (int k = 0; k < rnc; ++k) sum += k < 64 ? rld(p0, k) : rld(p1, k - 64);
+  p0 /= sum;
+  p1 /= sum;
+  AzChoice c;
+  c.p0 = p0;
+  c.p1 = p1;
+  c.child = best;
+  if (sample) {
+    const double z = AbslUniformDouble01(act);
+    double acc = 0.0;
+    c.child = -1;
+    for (int k = 0; k < rnc; ++k) {
+      const double pk = k < 64 ? rld(p0, k) : rld(p1, k - 64);
+      if (c.child < 0 && acc <= z && z < acc + pk) c.child = k;
+      acc += pk;
+    }
+    // SampleAction's SpielFatalError (z beyond the rounded total) cannot
+    // stop a kernel: take the last child, as the oracle restatement does.
+    if (c.child < 0) c.child = rnc - 1;
+  }
+  return c;
+}
+
+template <class G, class R, bool kPuct>
 __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
   const int64_t lg = blockIdx.x;
   if (lg >= a.num_games) return;
@@ -335,24 +377,34 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
   const int l = lane_id();
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
-  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 3 * kMtN * 4);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 4 * kMtN * 4);
   uint64_t* glog = reinterpret_cast<uint64_t*>(
-      smem + ((3 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
-  WaveMt b0, b1, ev;
+      smem + ((4 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
+  WaveMt b0, b1, ev, act;
   b0.s = mt;
   b1.s = mt + kMtN;
   ev.s = mt + 2 * kMtN;
-  b0.use7 = b1.use7 = 0;
+  act.s = mt + 3 * kMtN;
+  b0.use7 = b1.use7 = act.use7 = 0;
   ev.use7 = SmallAbsl<G>::value ? 1 : 0;
+  const bool actor = a.actor_seeds != nullptr;
   if (l == 0) {
     mt_seed(b0.s, a.bot_seeds[2 * gg]);
     mt_seed(b1.s, a.bot_seeds[2 * gg + 1]);
     mt_seed(ev.s, a.eval_seeds[gg]);
+    if (actor) mt_seed(act.s, a.actor_seeds[gg]);
   }
   __syncthreads();
   b0.init_seeded();
   b1.init_seeded();
   ev.init_seeded();
+  act.init_seeded();
+  // The game's resign cutoff (alpha_zero.cc:154-157), drawn first.
+  double cutoff = a.max_utility + 1.0;
+  if (actor && a.resign) {
+    const double u = AbslUniformDouble01(act);
+    if (u < a.cutoff_probability) cutoff = a.cutoff_value;
+  }
   typename G::State s = make_uniform(static_cast<const typename G::State*>(a.starts)[gg]);
   typename WaveCtxOf<G>::type ctx = SpCtx<G>::make(a, gg, glog);
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lg * static_cast<int64_t>(a.cap);
@@ -363,6 +415,9 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
   tot.used = tot.scanned = tot.backed = tot.expanded = tot.solver_scanned = 0;
   tot.rng_words = tot.pad = 0;
   int m = 0;
+  bool resigned = false;
+  double res_value = 0.0;
+  int res_player = 0;
   while (!G::terminal(s, a.cfg)) {
     if (m >= a.max_len) {
       tot.status = kGameOverflow;
@@ -371,8 +426,8 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
     const int p = G::to_move(s);
     WaveMt bot = p == 0 ? b0 : b1;
     const SearchResult r =
-        wave_search<G, R, kPolicyCpp>(a.cfg, a.sp, s, ctx, nodes, a.cap, bot, ev, path,
-                                      a.path_cap, ph);
+        wave_search<G, R, kPolicyCpp, false, kPuct>(a.cfg, a.sp, s, ctx, nodes, a.cap, bot, ev,
+                                                    path, a.path_cap, ph);
     if (p == 0) b0 = bot;
     else b1 = bot;
     tot.sims += r.sims;
@@ -395,7 +450,17 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
     bi = rli(bi, 0);
     const uint32_t rfirst = static_cast<uint32_t>(rli(static_cast<int>(nodes[0].first), 0));
     const int rnc = rli(nodes[0].nchild, 0);
-    const int act = rli(nodes[rfirst + bi].action, 0);
+    // AlphaZero's choice when an actor rng is given (alpha_zero.cc:77-95).
+    const bool want_policy = a.policy != nullptr || actor;
+    AzChoice ch;
+    ch.child = bi;
+    ch.p0 = ch.p1 = 0.0;
+    if (want_policy)
+      ch = az_choose(a, nodes + rfirst, rnc, actor && m < a.temperature_drop, act, bi);
+    const int act_i = rli(nodes[rfirst + ch.child].action, 0);
+    // root->total_reward / root->explore_count (alpha_zero.cc:92)
+    const double rw = rld(static_cast<double>(nodes[0].w), 0);
+    const double rv = rw / static_cast<double>(rli(nodes[0].n, 0));
     if (a.visits) {
       int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
       for (int i = l; i < a.num_actions; i += 64) v[i] = 0;
@@ -405,35 +470,62 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
         v[c.action] = c.n;
       }
     }
+    if (a.policy) {
+      double* pv = a.policy + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+      for (int i = l; i < a.num_actions; i += 64) pv[i] = 0.0;
+      __threadfence_block();
+      if (l < rnc) pv[nodes[rfirst + l].action] = ch.p0;
+      if (l + 64 < rnc) pv[nodes[rfirst + l + 64].action] = ch.p1;
+    }
+    if (a.root_value && l == 0) a.root_value[gg * a.max_len + m] = rv;
     if (a.obs) {  // ObservationTensor(player to move) of the position searched
       float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
       const int cells = a.cfg.rows * a.cfg.cols;
       for (int i = l; i < a.obs_size; i += 64) o[i] = G::obs(s, a.cfg, p, i / cells, i % cells);
     }
-    if (l == 0) a.actions[gg * a.max_len + m] = act;
+    if (l == 0) a.actions[gg * a.max_len + m] = act_i;
     ctx.reset();
-    G::apply(s, a.cfg, ctx, act);
+    G::apply(s, a.cfg, ctx, act_i);
     SpCtx<G>::commit(ctx, a, gg);
     s = make_uniform(s);
     ++m;
+    // alpha_zero.cc:105-110: a decided position ends the game early.
+    if (!G::terminal(s, a.cfg) && fabs(rv) > cutoff) {
+      resigned = true;
+      res_value = rv;
+      res_player = p;
+      break;
+    }
   }
-  tot.rng_words = b0.words.get() + b1.words.get() + ev.words.get();
+  tot.rng_words = b0.words.get() + b1.words.get() + ev.words.get() + act.words.get();
   for (int k = m + l; k < a.max_len; k += 64) a.actions[gg * a.max_len + k] = -1;
   if (a.visits) {  // rows after the last move are all-zero policy targets
     int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
     const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.num_actions;
     for (int64_t i = l; i < nz; i += 64) v[i] = 0;
   }
+  if (a.policy) {
+    double* pv = a.policy + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+    const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.num_actions;
+    for (int64_t i = l; i < nz; i += 64) pv[i] = 0.0;
+  }
+  if (a.root_value)
+    for (int k = m + l; k < a.max_len; k += 64) a.root_value[gg * a.max_len + k] = 0.0;
   if (a.obs) {
     float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
     const int64_t nz = static_cast<int64_t>(a.max_len - m) * a.obs_size;
     for (int64_t i = l; i < nz; i += 64) o[i] = 0.0f;
   }
   if (l == 0) {
-    const int r0 = G::terminal(s, a.cfg) ? G::ret0(s, a.cfg, ctx) : 0;
     a.length[gg] = m;
-    a.returns[2 * gg] = static_cast<double>(r0);
-    a.returns[2 * gg + 1] = static_cast<double>(-r0);
+    if (resigned) {
+      a.returns[2 * gg + res_player] = res_value;
+      a.returns[2 * gg + 1 - res_player] = -res_value;
+    } else {
+      const int r0 = G::terminal(s, a.cfg) ? G::ret0(s, a.cfg, ctx) : 0;
+      a.returns[2 * gg] = static_cast<double>(r0);
+      a.returns[2 * gg + 1] = static_cast<double>(-r0);
+    }
     a.results[gg] = tot;
   }
 }
@@ -738,7 +830,7 @@ int LaunchForGame(os_engine* e, const DevArgs& a, hipStream_t stream) {
              : LaunchSearch<G, int32_t, kPolicyCpp>(e, a, stream);
 }
 
-template <class G, class R>
+template <class G, class R, bool kPuct>
 int SpLaunch(os_engine* e, hipStream_t stream) {
   SpArgs a;
   std::memset(&a, 0, sizeof a);
@@ -749,6 +841,7 @@ int SpLaunch(os_engine* e, hipStream_t stream) {
   a.sp.solve = e->params.solve;
   a.sp.max_nodes = static_cast<int32_t>((e->params.max_memory_mb << 20) / 80 + 1);
   a.sp.policy = kPolicyCpp;
+  a.sp.puct = kPuct ? 1 : 0;
   a.sp.log_lut = static_cast<const double*>(e->d_lut.p);
   a.starts = e->d_roots.p;
   a.bot_seeds = static_cast<const uint32_t*>(e->d_bseed.p);
@@ -769,17 +862,27 @@ int SpLaunch(os_engine* e, hipStream_t stream) {
   a.obs = e->sp_obs ? static_cast<float*>(e->d_sp_obs.p) : nullptr;
   a.obs_size = ObservationShape(e->game, nullptr);
   a.results = static_cast<SearchResult*>(e->d_res.p);
+  const bool actor = !e->sp_actor_seeds.empty();
+  a.actor_seeds = actor ? static_cast<const uint32_t*>(e->d_sp_actor.p) : nullptr;
+  a.pow_lut = e->sp_opts.temperature > 0.0 ? static_cast<const double*>(e->d_sp_pow.p) : nullptr;
+  a.temperature_drop = e->sp_opts.temperature > 0.0 ? e->sp_opts.temperature_drop : 0;
+  a.resign = actor && e->sp_opts.resign ? 1 : 0;
+  a.cutoff_value = e->sp_opts.cutoff_value;
+  a.cutoff_probability = e->sp_opts.cutoff_probability;
+  a.max_utility = 1.0;  // every self-play game: Game::MaxUtility() == 1
+  a.policy = e->sp_policy ? static_cast<double*>(e->d_sp_pol.p) : nullptr;
+  a.root_value = e->sp_values ? static_cast<double*>(e->d_sp_val.p) : nullptr;
   const size_t lds = SelfPlayLdsBytes<G, R>(a.path_cap);
   if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "self-play LDS slice exceeds the CU's LDS");
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay<G, R>),
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay<G, R, kPuct>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds)));
   for (int64_t base = 0; base < e->sp_games; base += e->chunk_roots) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->sp_games - base);
     a.game_base = base;
     a.num_games = n;
-    hipLaunchKernelGGL((k_wselfplay<G, R>), dim3(static_cast<unsigned>(n)), dim3(64), lds,
-                       stream, a);
+    hipLaunchKernelGGL((k_wselfplay<G, R, kPuct>), dim3(static_cast<unsigned>(n)), dim3(64),
+                       lds, stream, a);
     HIP_TRY(hipGetLastError());
   }
   return OS_OK;
@@ -908,8 +1011,12 @@ int SelfPlayEntry(os_engine* e, hipStream_t stream) {
   if constexpr (HasChance<G>::value)
     return Fail(OS_ERR_UNSUPPORTED, "self-play of games with chance nodes");
   else
-    return e->params.n_rollouts != 1 ? SpLaunch<G, double>(e, stream)
-                                     : SpLaunch<G, int32_t>(e, stream);
+  {
+    const bool puct = e->params.child_selection == OS_SELECT_PUCT;
+    if (e->params.n_rollouts != 1)
+      return puct ? SpLaunch<G, double, true>(e, stream) : SpLaunch<G, double, false>(e, stream);
+    return puct ? SpLaunch<G, int32_t, true>(e, stream) : SpLaunch<G, int32_t, false>(e, stream);
+  }
 }
 
 }  // namespace osx

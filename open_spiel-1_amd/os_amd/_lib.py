@@ -151,6 +151,18 @@ _sig("os_selfplay_run_async", ctypes.c_int, [_vp, _vp])
 _sig("os_selfplay_fetch", ctypes.c_int, [_vp, _P, _P, _P, _P, _P])
 RECORD_VISITS = 1
 RECORD_OBSERVATIONS = 2
+RECORD_POLICY = 4
+RECORD_ROOT_VALUES = 8
+
+
+class SelfPlayOptions(ctypes.Structure):
+  _fields_ = [("temperature", _dbl), ("temperature_drop", _i32), ("resign", _i32),
+              ("cutoff_value", _dbl), ("cutoff_probability", _dbl)]
+
+
+_sig("os_selfplay_set_options", ctypes.c_int,
+     [_vp, ctypes.POINTER(SelfPlayOptions), _i64, _P])
+_sig("os_selfplay_fetch_targets", ctypes.c_int, [_vp, _P, _P])
 _sig("os_az_prepare", ctypes.c_int,
      [_vp, ctypes.POINTER(MctsParams), _i32, _i64, _P, _P, _P, ctypes.c_double,
       ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp])

@@ -206,9 +206,25 @@ class Engine:
                                         dev_rewards_ptr, stream))
 
   # ---- self-play (two MCTSBots + one shared RandomRolloutEvaluator) ----
+  def selfplay_set_options(self, actor_seeds=None, temperature=0.0, temperature_drop=0,
+                           resign=False, cutoff_value=0.9, cutoff_probability=0.8):
+    """AlphaZero's PlayGame move choice for the next self-play batch
+    (include/os_mcts.h os_selfplay_set_options; alpha_zero.cc:64-118):
+    visit-count^(1/temperature) policy sampled from each game's actor rng
+    (actor_seeds[g]) before temperature_drop moves, resignation at
+    |root value| > cutoff.  No actor seeds: BestChild every move."""
+    o = _lib.SelfPlayOptions()
+    o.temperature = float(temperature)
+    o.temperature_drop = int(temperature_drop)
+    o.resign = 1 if resign else 0
+    o.cutoff_value = float(cutoff_value)
+    o.cutoff_probability = float(cutoff_probability)
+    seeds = _lib.u32(actor_seeds if actor_seeds is not None else [])
+    check(lib.os_selfplay_set_options(self._h, ctypes.byref(o), len(seeds), ptr(seeds)))
+
   def selfplay_prepare(self, start_actions, start_offsets, bot_seeds, eval_seeds,
                        max_len=None, record_visits=True, record_observations=False,
-                       **params):
+                       record_policy=False, record_root_values=False, **params):
     """Device self-play batch (os_selfplay_prepare).  bot_seeds: [G][2]."""
     self._sp_params = make_params(**params)
     offs = _lib.i64(start_offsets)
@@ -221,9 +237,13 @@ class Engine:
     self._sp_len = int(max_len if max_len is not None else self.max_game_length)
     self._sp_vis = bool(record_visits)
     self._sp_obs = bool(record_observations)
+    self._sp_pol = bool(record_policy)
+    self._sp_val = bool(record_root_values)
     acts = self._sp[0]
     record = ((_lib.RECORD_VISITS if record_visits else 0) |
-              (_lib.RECORD_OBSERVATIONS if record_observations else 0))
+              (_lib.RECORD_OBSERVATIONS if record_observations else 0) |
+              (_lib.RECORD_POLICY if record_policy else 0) |
+              (_lib.RECORD_ROOT_VALUES if record_root_values else 0))
     check(lib.os_selfplay_prepare(self._h, ctypes.byref(self._sp_params), G, ptr(acts),
                                   ptr(offs), ptr(bs), ptr(es), self._sp_len, record))
 
@@ -240,13 +260,19 @@ class Engine:
     check(lib.os_selfplay_fetch(self._h, ptr(o["actions"]), ptr(o["length"]),
                                 ptr(o["returns"]), ptr(o["visits"]),
                                 ptr(o["observations"])))
+    o["policy"] = np.zeros((G, L, A), np.float64) if self._sp_pol else None
+    o["root_value"] = np.zeros((G, L), np.float64) if self._sp_val else None
+    if self._sp_pol or self._sp_val:
+      check(lib.os_selfplay_fetch_targets(self._h, ptr(o["policy"]), ptr(o["root_value"])))
     return o
 
   def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len=None,
-               record_visits=True, record_observations=False, **params):
+               record_visits=True, record_observations=False, record_policy=False,
+               record_root_values=False, **params):
     """Plays G games on the device; see include/os_mcts.h os_selfplay."""
     self.selfplay_prepare(start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
-                          record_visits, record_observations, **params)
+                          record_visits, record_observations, record_policy,
+                          record_root_values, **params)
     self.selfplay_run_async()
     return self.selfplay_fetch()
 

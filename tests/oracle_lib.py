@@ -80,6 +80,11 @@ def lib():
         ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double,
         ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, _u32p,
         _u32p, ctypes.c_int32, _i64p, _i32p, _f64p, ctypes.c_void_p, ctypes.c_int32]
+    L.oref_selfplay_az.argtypes = [
+        ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double, ctypes.c_int32,
+        ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _u32p, _u32p, _u32p,
+        ctypes.c_double, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+        ctypes.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
     L.oref_evaluate_mcts_bots.restype = ctypes.c_int64
     L.oref_evaluate_mcts_bots.argtypes = [
         ctypes.c_void_p, ctypes.c_int32, _u32p, ctypes.c_int32, ctypes.c_uint32,
@@ -260,6 +265,31 @@ def evaluate_mcts_bots(game_string, bot_seeds, n_rollouts, eval_seed, seed, uct_
       eval_seed, uct_c, max_simulations, max_memory_mb, int(solve), seed, hist, len(hist), ret)
   assert n >= 0
   return [int(a) for a in hist[:n]], [float(x) for x in ret]
+
+
+def selfplay_az(game_string, start_actions, start_offsets, bot_seeds, eval_seeds, actor_seeds,
+                max_len, uct_c=2.0, max_simulations=100, n_rollouts=1, max_memory_mb=1000,
+                solve=True, puct=False, temperature=1.0, temperature_drop=10, resign=False,
+                cutoff_value=0.9, cutoff_probability=0.8):
+  """AlphaZero PlayGame move choice over self-play MCTSBots (oref_selfplay_az)."""
+  g = Game(game_string)
+  G = len(start_offsets) - 1
+  A = g.num_distinct_actions
+  out = dict(actions=np.zeros((G, max_len), np.int64), length=np.zeros(G, np.int32),
+             returns=np.zeros((G, 2), np.float64), policy=np.zeros((G, max_len, A), np.float64),
+             root_value=np.zeros((G, max_len), np.float64))
+  rc = lib().oref_selfplay_az(
+      g._h, G, np.ascontiguousarray(start_actions, dtype=np.int64),
+      np.ascontiguousarray(start_offsets, dtype=np.int64), uct_c, max_simulations, n_rollouts,
+      max_memory_mb, int(solve), int(puct),
+      np.ascontiguousarray(bot_seeds, dtype=np.uint32).reshape(-1),
+      np.ascontiguousarray(eval_seeds, dtype=np.uint32),
+      np.ascontiguousarray(actor_seeds, dtype=np.uint32), float(temperature),
+      int(temperature_drop), int(bool(resign)), float(cutoff_value), float(cutoff_probability),
+      max_len, out["actions"], out["length"], out["returns"], out["policy"], out["root_value"])
+  if rc:
+    raise RuntimeError("oref_selfplay_az: game longer than max_len")
+  return out
 
 
 def mt19937(seed, n):

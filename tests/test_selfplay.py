@@ -137,3 +137,90 @@ def test_gpu_selfplay_errors(require_gpu):
     eng.selfplay(acts, offs, [[1, 2]], [3], policy=_lib.POLICY_NUMPY, max_simulations=10)
   with pytest.raises(_lib.SpielError):
     eng.selfplay(acts, offs, [[1, 2]], [3], max_len=2, max_simulations=10)
+
+
+# ---- AlphaZero's PlayGame move choice (alpha_zero.cc:64-118) -------------
+AZ_CASES = [  # (game, temperature, drop, resign, puct)
+    ("tic_tac_toe", 1.0, 4, False, False),
+    ("connect_four", 0.5, 6, False, False),
+    ("connect_four", 1.0, 10, True, False),
+    ("hex(board_size=5)", 1.0, 8, True, True),
+    ("breakthrough(rows=6,columns=6)", 0.7, 5, False, True),
+    ("go(board_size=5,komi=0.5)", 1.0, 6, True, False),
+]
+
+
+def _az_kw(game, t, drop, resign, puct):
+  return dict(uct_c=2.0, max_simulations=SIMS[game], puct=puct, temperature=t,
+              temperature_drop=drop, resign=resign, cutoff_value=0.5, cutoff_probability=0.7)
+
+
+def test_oracle_az_selfplay_without_sampling_is_plain_selfplay():
+  """temperature <= 0 (or drop 0) and no resignation: the moves are BestChild,
+  i.e. oref_selfplay's games; policies are normalised visit counts."""
+  game = "connect_four"
+  og = oracle_lib.Game(game)
+  acts, offs, bot, ev = _batch(game)
+  actor = np.arange(len(offs) - 1, dtype=np.uint32) + 77
+  ref = og.selfplay(acts, offs, bot, ev, 42, max_simulations=SIMS[game])
+  for t, drop in ((0.0, 10), (1.0, 0)):
+    o = oracle_lib.selfplay_az(game, acts, offs, bot, ev, actor, 42, max_simulations=SIMS[game],
+                               temperature=t, temperature_drop=drop)
+    for k in ("actions", "length", "returns"):
+      assert np.array_equal(o[k], ref[k]), (t, k)
+    vis = ref["visits"].astype(np.float64)
+    n = vis.sum(axis=2, keepdims=True)
+    want = np.divide(vis, n, out=np.zeros_like(vis), where=n > 0)
+    np.testing.assert_allclose(o["policy"], want, rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("game,t,drop,resign,puct", AZ_CASES)
+def test_oracle_az_selfplay_is_consistent(game, t, drop, resign, puct):
+  og = oracle_lib.Game(game)
+  acts, offs, bot, ev = _batch(game)
+  G = len(offs) - 1
+  actor = np.arange(G, dtype=np.uint32) * 13 + 5
+  o = oracle_lib.selfplay_az(game, acts, offs, bot, ev, actor, og.max_game_length,
+                             **_az_kw(game, t, drop, resign, puct))
+  for g in range(G):
+    hist = list(acts[offs[g]:offs[g + 1]])
+    n = int(o["length"][g])
+    for m in range(n):
+      info = og.state_info(hist)
+      a = int(o["actions"][g, m])
+      assert a in info["legal_actions"] and o["policy"][g, m, a] > 0
+      assert abs(o["policy"][g, m].sum() - 1) < 1e-12
+      assert -1 <= o["root_value"][g, m] <= 1
+      hist.append(a)
+    info = og.state_info(hist)
+    if not info["is_terminal"]:  # resigned: returns are the last root value
+      v = o["root_value"][g, n - 1]
+      assert resign and abs(v) > 0.5
+      mover = og.state_info(hist[:-1])["current_player"]
+      assert o["returns"][g, mover] == v and o["returns"][g, 1 - mover] == -v
+    else:
+      assert list(o["returns"][g]) == list(info["returns"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("game,t,drop,resign,puct", AZ_CASES)
+def test_gpu_az_selfplay_matches_oracle(require_gpu, game, t, drop, resign, puct):
+  """k_wselfplay with AlphaZero's move choice: every action, length, return,
+  policy target and root value bit-exact with the oracle's PlayGame."""
+  from os_amd import _lib
+  og = oracle_lib.Game(game)
+  acts, offs, bot, ev = _batch(game)
+  G = len(offs) - 1
+  actor = np.arange(G, dtype=np.uint32) * 13 + 5
+  kw = _az_kw(game, t, drop, resign, puct)
+  ref = oracle_lib.selfplay_az(game, acts, offs, bot, ev, actor, og.max_game_length, **kw)
+  eng = E.Engine(game)
+  eng.selfplay_set_options(actor, temperature=t, temperature_drop=drop, resign=resign,
+                           cutoff_value=kw["cutoff_value"],
+                           cutoff_probability=kw["cutoff_probability"])
+  got = eng.selfplay(acts, offs, bot, ev, og.max_game_length, record_visits=False,
+                     record_policy=True, record_root_values=True, uct_c=2.0,
+                     max_simulations=SIMS[game],
+                     child_selection=_lib.SELECT_PUCT if puct else _lib.SELECT_UCT)
+  for k in ("actions", "length", "returns", "policy", "root_value"):
+    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
