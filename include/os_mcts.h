@@ -235,6 +235,20 @@ int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t n
                   double dirichlet_epsilon, int32_t* dev_kind, float* dev_obs,
                   uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
                   int32_t* dev_pending);
+/* os_az_prepare for bots whose rng_ has advanced over earlier searches (an
+ * AlphaZero actor's MCTSBots keep one rng_ across a game, mcts.cc:209,
+ * 325-333): search r continues the std::mt19937 held in numpy's legacy
+ * (bot_keys[r][624], bot_pos[r]) form; the Dirichlet noise is drawn from that
+ * stream.  After the searches finish, os_az_export_rng writes the advanced
+ * streams back in the same form. */
+int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,
+                           int64_t num_roots, const int64_t* root_actions,
+                           const int64_t* root_offsets, const uint32_t* bot_keys,
+                           const int32_t* bot_pos, double dirichlet_alpha,
+                           double dirichlet_epsilon, int32_t* dev_kind, float* dev_obs,
+                           uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
+                           int32_t* dev_pending);
+int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos);
 /* The Dirichlet noise os_az_prepare draws for one fresh MCTSBot(seed) at a
  * root with `count` legal actions: out[count] (normalised, legal-action
  * order); returns the MT19937 words consumed (< 0 on error).  Exposed so the

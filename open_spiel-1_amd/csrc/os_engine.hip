@@ -723,11 +723,23 @@ int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
 }
 
 
+// bot_keys / bot_pos (both or neither): each search continues a bot rng_
+// held in numpy's (key[624], pos) form instead of seeding one.
 int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
               const int64_t* root_actions, const int64_t* root_offsets,
               const uint32_t* bot_seeds, double alpha, double eps, int32_t* kind, float* obs,
-              uint8_t* legal, const double* prior, const double* value, int32_t* pending) {
+              uint8_t* legal, const double* prior, const double* value, int32_t* pending,
+              const uint32_t* bot_keys = nullptr, const int32_t* bot_pos = nullptr) {
   if (!p) return Fail(OS_ERR_INVALID, "null params");
+  const bool import = bot_keys != nullptr;
+  std::vector<uint32_t> zero_seeds;
+  if (import) {
+    if (!bot_pos) return Fail(OS_ERR_INVALID, "bot_keys need bot_pos");
+    for (int64_t r = 0; r < R; ++r)
+      if (bot_pos[r] < 0 || bot_pos[r] > kMtN) return Fail(OS_ERR_INVALID, "bad rng position");
+    zero_seeds.assign(static_cast<size_t>(std::max<int64_t>(R, 1)), 0u);
+    bot_seeds = zero_seeds.data();
+  }
   if (!(alpha >= 0.0) || !(eps >= 0.0) || eps > 1.0)
     return Fail(OS_ERR_INVALID, "dirichlet_alpha must be >= 0 and epsilon in [0, 1]");
   if (p->policy != OS_POLICY_CPP)
@@ -771,8 +783,11 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
       ReplayRoot(e->game, root_actions + root_offsets[r], root_offsets[r + 1] - root_offsets[r],
                  &hs, &err);
       StateLegal(hs, &acts);
-      const int64_t w = DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
-                                       noise.data() + r * mc);
+      const int64_t w =
+          import ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r],
+                                       static_cast<int>(acts.size()), alpha, noise.data() + r * mc)
+                 : DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
+                                  noise.data() + r * mc);
       if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
       skip[r] = static_cast<int32_t>(w);
     }
@@ -780,6 +795,13 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
       return rc;
     HIP_TRY(hipMemcpy(e->d_az_noise.p, noise.data(), noise.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_az_skip.p, skip.data(), Rz * 4, hipMemcpyHostToDevice));
+  }
+  e->az_import = import;
+  if (import && R > 0) {  // keys into the bot rng rows, positions in / out
+    HIP_TRY(hipMemcpy(e->d_mt.p, bot_keys, static_cast<size_t>(R) * kMtN * 4,
+                      hipMemcpyHostToDevice));
+    if ((rc = e->d_az_pos.ensure(static_cast<size_t>(R) * 8))) return rc;
+    HIP_TRY(hipMemcpy(e->d_az_pos.p, bot_pos, static_cast<size_t>(R) * 4, hipMemcpyHostToDevice));
   }
   e->az_puct = puct ? 1 : 0;
   e->az_kind = kind;
@@ -1273,6 +1295,38 @@ int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t n
   return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, bot_seeds,
                    dirichlet_alpha, dirichlet_epsilon, dev_kind, dev_obs, dev_legal, dev_prior,
                    dev_value, dev_pending);
+}
+
+int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,
+                           int64_t num_roots, const int64_t* root_actions,
+                           const int64_t* root_offsets, const uint32_t* bot_keys,
+                           const int32_t* bot_pos, double dirichlet_alpha,
+                           double dirichlet_epsilon, int32_t* dev_kind, float* dev_obs,
+                           uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
+                           int32_t* dev_pending) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (num_roots > 0 && (!bot_keys || !bot_pos)) return Fail(OS_ERR_INVALID, "null rng state");
+  return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, nullptr, dirichlet_alpha,
+                   dirichlet_epsilon, dev_kind, dev_obs, dev_legal, dev_prior, dev_value,
+                   dev_pending, bot_keys ? bot_keys : nullptr, bot_pos);
+}
+
+int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos) {
+  if (!e || !bot_keys || !bot_pos) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->az_ready || !e->az_import)
+    return Fail(OS_ERR_INVALID, "no os_az_prepare_stateful batch");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  int32_t pending = 0;
+  HIP_TRY(hipMemcpy(&pending, e->az_pending, 4, hipMemcpyDeviceToHost));
+  if (pending != 0) return Fail(OS_ERR_INVALID, "searches still wait for the evaluator");
+  const int64_t R = e->num_roots;
+  if (R == 0) return OS_OK;
+  HIP_TRY(hipMemcpy(bot_keys, e->d_mt.p, static_cast<size_t>(R) * kMtN * 4,
+                    hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(bot_pos, static_cast<int32_t*>(e->d_az_pos.p) + R,
+                    static_cast<size_t>(R) * 4, hipMemcpyDeviceToHost));
+  return OS_OK;
 }
 
 int64_t os_dirichlet_noise(uint32_t seed, int32_t count, double alpha, double* out) {

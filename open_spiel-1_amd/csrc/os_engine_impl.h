@@ -146,6 +146,12 @@ struct AzArgs {
   const double* prior_in;   // [R][A]
   const double* value_in;   // [R]
   int32_t* pending;         // requests written by this step
+  // Bot rng continuing a caller-held stream (os_az_prepare_stateful): rows of
+  // `mt` hold numpy-form keys, mt_pos_in the positions; a finished search
+  // writes its stream back in the same form (key row + mt_pos_out).
+  int32_t import_mt;
+  const int32_t* mt_pos_in;  // [R]
+  int32_t* mt_pos_out;       // [R]
   // Dirichlet root noise (alpha > 0): [R][noise_stride] normalised draws in
   // legal-action order + MT words they consumed (host-drawn, os_az.h)
   const double* noise;      // null: no noise
@@ -254,7 +260,8 @@ struct os_engine {
   int32_t* az_pending = nullptr;
   double az_eps = 0.0;
   bool az_noise = false;
-  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip;
+  bool az_import = false;  // os_az_prepare_stateful
+  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos;
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -286,7 +293,7 @@ struct os_engine {
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
-                     &d_sp_actor, &d_sp_pow};
+                     &d_sp_actor, &d_sp_pow, &d_az_pos};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

@@ -7,6 +7,8 @@
 //   go.cc:133-144 + go_board.cc:478-506.
 #include "os_host.h"
 
+#include "os_rng.h"
+
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -31,16 +33,44 @@ struct CountingMt {
     return static_cast<result_type>(g());
   }
 };
-}  // namespace
 
-int64_t DirichletNoise(uint32_t seed, int count, double alpha, double* out) {
-  CountingMt rng(seed);
+// The same URBG over a caller-held stream in numpy's (key, pos) form (the
+// engine's MtStream import semantics), on a copy of the key.
+struct StateMt {
+  using result_type = uint32_t;
+  std::vector<uint32_t> key;
+  MtStream g;
+  int64_t words = 0;
+  StateMt(const uint32_t* k, int pos) : key(k, k + kMtN), g{nullptr, pos, 1, 0} {
+    g.s = key.data();
+  }
+  static constexpr result_type min() { return 0; }
+  static constexpr result_type max() { return 0xFFFFFFFFu; }
+  result_type operator()() {
+    ++words;
+    return g.next();
+  }
+};
+
+template <class Rng>
+int64_t DirichletFrom(Rng& rng, int count, double alpha, double* out) {
   std::gamma_distribution<double> gamma(alpha, 1.0);
   for (int i = 0; i < count; ++i) out[i] = gamma(rng);
   double sum = 0.0;
   for (int i = 0; i < count; ++i) sum += out[i];  // absl::c_accumulate(noise, 0.0)
   for (int i = 0; i < count; ++i) out[i] /= sum;
   return rng.words;
+}
+}  // namespace
+
+int64_t DirichletNoiseState(const uint32_t* key, int pos, int count, double alpha, double* out) {
+  StateMt rng(key, pos);
+  return DirichletFrom(rng, count, alpha, out);
+}
+
+int64_t DirichletNoise(uint32_t seed, int count, double alpha, double* out) {
+  CountingMt rng(seed);
+  return DirichletFrom(rng, count, alpha, out);
 }
 
 namespace {

@@ -60,6 +60,9 @@ GoCtx HostGoCtx(const HostState& s, HostGoLog* buf);
 // (its Marsaglia-Tsang sampler and libm calls make the bits), normalised by
 // the left-fold sum; writes out[count] and returns the MT words consumed.
 int64_t DirichletNoise(uint32_t seed, int count, double alpha, double* out);
+// The same draw from a bot rng_ held in numpy's (key[624], pos) form (a bot
+// whose stream has advanced over earlier searches).
+int64_t DirichletNoiseState(const uint32_t* key, int pos, int count, double alpha, double* out);
 
 // Parses and validates a game string; returns "" on success, else a message.
 // `unsupported` is set when the game/parameters are valid OpenSpiel but not

@@ -561,9 +561,14 @@ __global__ void k_az_step(AzArgs a) {
   }
   uint32_t* mt = a.mt + r * kMtN;
   if (stage0 == kAzStart) {
-    mt_seed(mt, a.bot_seeds[r]);
-    sl.mt_idx = kMtN;
-    sl.mt_pre = 0;
+    if (a.import_mt) {  // the row already holds the caller's key
+      sl.mt_idx = a.mt_pos_in[r];
+      sl.mt_pre = 1;
+    } else {
+      mt_seed(mt, a.bot_seeds[r]);
+      sl.mt_idx = kMtN;
+      sl.mt_pre = 0;
+    }
     sl.depth = 0;
     sl.s = static_cast<const typename G::State*>(a.roots)[r];
   }
@@ -589,6 +594,10 @@ __global__ void k_az_step(AzArgs a) {
   if (*io.kind != kAzNone) {
     atomicAdd(a.pending, 1);
     return;
+  }
+  if (a.import_mt) {  // the bot's rng_ back in numpy (key, pos) form
+    bot.finalize();
+    a.mt_pos_out[r] = bot.idx;
   }
   // Finished in this step: publish the root's children like the search kernels.
   const int P0 = G::to_move(root);
@@ -921,6 +930,9 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.prior_in = e->az_prior;
   a.value_in = e->az_value;
   a.pending = e->az_pending;
+  a.import_mt = e->az_import ? 1 : 0;
+  a.mt_pos_in = static_cast<const int32_t*>(e->d_az_pos.p);
+  a.mt_pos_out = static_cast<int32_t*>(e->d_az_pos.p) + (e->az_import ? e->num_roots : 0);
   if (e->az_noise) {
     a.noise = static_cast<const double*>(e->d_az_noise.p);
     a.noise_skip = static_cast<const int32_t*>(e->d_az_skip.p);

@@ -167,6 +167,10 @@ _sig("os_az_prepare", ctypes.c_int,
      [_vp, ctypes.POINTER(MctsParams), _i32, _i64, _P, _P, _P, ctypes.c_double,
       ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp])
 _sig("os_dirichlet_noise", _i64, [_u32, _i32, ctypes.c_double, _P])
+_sig("os_az_prepare_stateful", ctypes.c_int,
+     [_vp, ctypes.POINTER(MctsParams), _i32, _i64, _P, _P, _P, _P, ctypes.c_double,
+      ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp])
+_sig("os_az_export_rng", ctypes.c_int, [_vp, _P, _P])
 _sig("os_az_step_async", ctypes.c_int, [_vp, _vp])
 _sig("os_az_fetch", ctypes.c_int, [_vp, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P])
 _sig("os_engine_node_bytes", _i32, [_vp])

@@ -47,8 +47,15 @@ class ExternalEvaluatorSearch:
 
   def run(self, root_actions, root_offsets, bot_seeds, evaluator, puct=True,
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
-          dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False):
+          dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False,
+          bot_rng=None):
     """Runs every search to completion; returns the os_mcts_batch outputs.
+
+    The evaluator may be called once more after the last step, with every
+    kind 0 (idle): its answers are then ignored.  bot_rng = (keys uint32
+    [R][624], pos int32 [R]): each search continues that bot rng_ (numpy
+    legacy form) instead of seeding one from bot_seeds; the advanced streams
+    are left in `self.bot_rng_out` (os_az_prepare_stateful / os_az_export_rng).
 
     dirichlet_alpha / dirichlet_epsilon are the MCTSBot constructor's
     (mcts.h:152-159): root priors become (1 - eps) * p + eps * Dir(alpha)
@@ -70,12 +77,21 @@ class ExternalEvaluatorSearch:
     p = E.make_params(uct_c=uct_c, max_simulations=max_simulations,
                       max_memory_mb=max_memory_mb, solve=solve)
     acts = _lib.i64(root_actions)
-    bs = _lib.u32(bot_seeds)
-    check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
-                            ptr(offs), ptr(bs), float(dirichlet_alpha),
-                            float(dirichlet_epsilon), kind.data_ptr(), obs.data_ptr(),
-                            legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
-                            pending.data_ptr()))
+    if bot_rng is None:
+      bs = _lib.u32(bot_seeds)
+      check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
+                              ptr(offs), ptr(bs), float(dirichlet_alpha),
+                              float(dirichlet_epsilon), kind.data_ptr(), obs.data_ptr(),
+                              legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
+                              pending.data_ptr()))
+    else:
+      keys = np.ascontiguousarray(bot_rng[0], dtype=np.uint32).reshape(R, 624)
+      pos = np.ascontiguousarray(bot_rng[1], dtype=np.int32).reshape(R)
+      check(lib.os_az_prepare_stateful(
+          self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts), ptr(offs), ptr(keys),
+          ptr(pos), float(dirichlet_alpha), float(dirichlet_epsilon), kind.data_ptr(),
+          obs.data_ptr(), legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
+          pending.data_ptr()))
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     self.steps = 0
     self.requests = 0
@@ -109,8 +125,130 @@ class ExternalEvaluatorSearch:
       self.requests += n
     o = E._alloc_outputs(R, self.eng.max_children)
     check(lib.os_az_fetch(self.eng._h, self.eng.max_children, *E._out_ptrs(o)))
+    if bot_rng is not None:
+      keys = np.zeros((R, 624), np.uint32)
+      pos = np.zeros(R, np.int32)
+      check(lib.os_az_export_rng(self.eng._h, ptr(keys), ptr(pos)))
+      self.bot_rng_out = (keys, pos)
     return o
 
   def step_ms(self):
     """Summed k_az_step time of the last run(time_steps=True), ms."""
     return sum(a.elapsed_time(b) for a, b in self.events)
+
+
+class AlphaZeroActor:
+  """AlphaZero's actor games (alpha_zero.cc:64-118 PlayGame; bots as InitAZBot,
+  :120-135: MCTSBot with PUCT, Dirichlet root noise and the network
+  evaluator) for many games at once.
+
+  Every move is ONE batched external-evaluator search over all unfinished
+  games (`ExternalEvaluatorSearch`, one kernel step per evaluator round), each
+  game's two bots continuing their own rng_ across the game; then, per game,
+  the policy pow(explore_count, 1 / temperature) over the root's children,
+  normalised (NormalizePolicy); the move is SampleAction(policy, actor rng)
+  while fewer than `temperature_drop` moves were played (std::mt19937 per
+  game, absl::Uniform(rng, 0.0, 1.0), os_sample_action), BestChild after; the
+  root value total_reward / explore_count; with `resign`, the game's cutoff
+  (drawn from the actor rng first: u < cutoff_probability ? cutoff_value :
+  MaxUtility + 1) ends it early with returns (value, -value).  Results equal
+  the reference PlayGame run with the same evaluator and seeds.
+  """
+
+  def __init__(self, game_string, device=0):
+    from . import pyspiel
+    self.pyspiel = pyspiel
+    self.game = pyspiel.load_game(game_string)
+    self.search = ExternalEvaluatorSearch(game_string, device)
+
+  def play(self, start_actions, start_offsets, bot_seeds, actor_seeds, evaluator, max_len=None,
+           uct_c=2.0, max_simulations=50, temperature=1.0, temperature_drop=10, resign=False,
+           cutoff_value=0.9, cutoff_probability=0.8, dirichlet_alpha=0.0,
+           dirichlet_epsilon=0.0, solve=False, max_memory_mb=10, puct=True):
+    """Plays G games; bot_seeds [G][2], actor_seeds [G].  Returns dict(actions
+    [G][L] (-1 padded), length [G], returns [G][2], policy [G][L][A] (action-
+    indexed), root_value [G][L])."""
+    import math
+    pyspiel = self.pyspiel
+    offs = np.asarray(start_offsets, np.int64)
+    G = len(offs) - 1
+    L = int(max_len or self.game.max_game_length())
+    A = self.game.num_distinct_actions()
+    acts0 = np.asarray(start_actions, np.int64)
+    states = []
+    for g in range(G):
+      st = self.game.new_initial_state()
+      for a in acts0[offs[g]:offs[g + 1]]:
+        st.apply_action(int(a))
+      states.append(st)
+    bseeds = np.asarray(bot_seeds, np.uint32).reshape(G, 2)
+    keys = np.zeros((G, 2, 624), np.uint32)
+    pos = np.zeros((G, 2), np.int32)
+    for g in range(G):
+      for p in range(2):
+        k, q = pyspiel._mt_key(int(bseeds[g, p]))
+        keys[g, p], pos[g, p] = k, q
+    actor = []
+    for s in np.asarray(actor_seeds, np.uint32):
+      k, q = pyspiel._mt_key(int(s))
+      actor.append((k.copy(), np.array([q], np.int32)))
+
+    def sample(g, probs):
+      pr = np.ascontiguousarray(probs, np.float64)
+      k = lib.os_sample_action(pr.ctypes.data, len(pr), actor[g][0].ctypes.data,
+                               actor[g][1].ctypes.data)
+      if k < 0:
+        check(int(k))
+      return k
+
+    cutoff = [self.game.max_utility() + 1.0] * G
+    if resign:
+      for g in range(G):  # SampleAction over [(u < p), (u >= p)] is the draw u < p
+        if sample(g, [cutoff_probability, 1.0 - cutoff_probability]) == 0:
+          cutoff[g] = cutoff_value
+    out = dict(actions=np.full((G, L), -1, np.int64), length=np.zeros(G, np.int32),
+               returns=np.zeros((G, 2), np.float64), policy=np.zeros((G, L, A), np.float64),
+               root_value=np.zeros((G, L), np.float64))
+    live = [g for g in range(G) if not states[g].is_terminal()]
+    moves = [0] * G
+    self.searches = 0
+    while live:
+      players = [states[g].current_player() for g in live]
+      ra, ro = E.roots_from_histories([states[g].history() for g in live])
+      rk = np.stack([keys[g, p] for g, p in zip(live, players)])
+      rp = np.array([pos[g, p] for g, p in zip(live, players)], np.int32)
+      o = self.search.run(ra, ro, None, evaluator, puct=puct, max_simulations=max_simulations,
+                          uct_c=uct_c, solve=solve, max_memory_mb=max_memory_mb,
+                          dirichlet_alpha=dirichlet_alpha,
+                          dirichlet_epsilon=dirichlet_epsilon, bot_rng=(rk, rp))
+      self.searches += len(live)
+      nk, npos = self.search.bot_rng_out
+      still = []
+      for i, (g, p) in enumerate(zip(live, players)):
+        keys[g, p], pos[g, p] = nk[i], npos[i]
+        m = moves[g]
+        if m >= L:
+          raise RuntimeError("game %d longer than max_len" % g)
+        nc = int(o["nchild"][i])
+        kids = [int(a) for a in o["child_action"][i, :nc]]
+        pol = [math.pow(float(n), 1.0 / temperature) for n in o["child_n"][i, :nc]]
+        tot = 0.0
+        for x in pol:  # NormalizePolicy: left-to-right sum in child order
+          tot += x
+        pol = [x / tot for x in pol]
+        a = kids[sample(g, pol)] if m < temperature_drop else int(o["best_action"][i])
+        rv = float(o["root_w"][i]) / int(o["root_n"][i])
+        out["policy"][g, m, kids] = pol
+        out["root_value"][g, m] = rv
+        out["actions"][g, m] = a
+        states[g].apply_action(a)
+        moves[g] = m + 1
+        if states[g].is_terminal():
+          out["returns"][g] = states[g].returns()
+        elif abs(rv) > cutoff[g]:
+          out["returns"][g, p], out["returns"][g, 1 - p] = rv, -rv
+        else:
+          still.append(g)
+      live = still
+    out["length"][:] = moves
+    return out

@@ -514,6 +514,77 @@ int oref_selfplay_az(void* g, int64_t num_games, const int64_t* start_actions,
   return 0;
 }
 
+// AlphaZero's actor games (alpha_zero.cc:64-118 PlayGame, :120-135 InitAZBot):
+// per game two MCTSBots (seeds bot_seeds[2g], [2g+1]; PUCT or UCT; Dirichlet
+// root noise alpha / epsilon) sharing the external evaluator `cb`, one actor
+// std::mt19937(actor_seeds[g]): resign cutoff drawn first when `resign`;
+// pow(count, 1/T) policy, SampleAction before temperature_drop moves,
+// BestChild after; root value; early stop at |value| > cutoff.  Same outputs
+// as oref_selfplay_az.
+int oref_az_actor(void* g, int64_t num_games, const int64_t* start_actions,
+                  const int64_t* start_offsets, double uct_c, int32_t max_simulations,
+                  int64_t max_memory_mb, int32_t solve, int32_t puct, double dirichlet_alpha,
+                  double dirichlet_epsilon, const uint32_t* bot_seeds,
+                  const uint32_t* actor_seeds, double temperature, int32_t temperature_drop,
+                  int32_t resign, double cutoff_value, double cutoff_probability,
+                  oref_eval_cb cb, int32_t max_len, int64_t* actions, int32_t* len,
+                  double* returns, double* policy, double* root_value) {
+  auto* og = static_cast<OGame*>(g);
+  const int A = og->game->NumDistinctActions();
+  CallbackEvaluator ev(cb, A);
+  for (int64_t r = 0; r < num_games; ++r) {
+    auto state = Replay(*og->game, start_actions + start_offsets[r],
+                        start_offsets[r + 1] - start_offsets[r]);
+    MCTSBot b0(*og->game, &ev, uct_c, max_simulations, max_memory_mb, solve != 0,
+               bot_seeds[2 * r], puct != 0, dirichlet_alpha, dirichlet_epsilon);
+    MCTSBot b1(*og->game, &ev, uct_c, max_simulations, max_memory_mb, solve != 0,
+               bot_seeds[2 * r + 1], puct != 0, dirichlet_alpha, dirichlet_epsilon);
+    MCTSBot* bots[2] = {&b0, &b1};
+    std::mt19937 rng(actor_seeds[r]);
+    double cutoff = og->game->MaxUtility() + 1;
+    if (resign && AbslUniformDouble01(rng) < cutoff_probability) cutoff = cutoff_value;
+    std::fill(policy + r * max_len * static_cast<int64_t>(A),
+              policy + (r + 1) * max_len * static_cast<int64_t>(A), 0.0);
+    std::fill(root_value + r * max_len, root_value + (r + 1) * max_len, 0.0);
+    int m = 0;
+    bool stopped = false;
+    while (!state->IsTerminal()) {
+      if (m >= max_len) return -1;
+      const Player player = state->CurrentPlayer();
+      SearchStats st;
+      auto root = bots[player]->MCTSearch(*state, &st);
+      std::vector<std::pair<Action, double>> pol;
+      for (const SearchNode& c : root->children)
+        pol.emplace_back(c.action, std::pow(c.explore_count, 1.0 / temperature));
+      double sum = 0;
+      for (const auto& x : pol) sum += x.second;
+      for (auto& x : pol) x.second /= sum;
+      const Action a = m < temperature_drop ? SampleAction(pol, AbslUniformDouble01(rng))
+                                            : root->BestChild().action;
+      const double rv = root->total_reward / root->explore_count;
+      for (const auto& x : pol) policy[(r * max_len + m) * static_cast<int64_t>(A) + x.first] = x.second;
+      root_value[r * max_len + m] = rv;
+      actions[r * max_len + m] = a;
+      state->ApplyAction(a);
+      ++m;
+      if (!state->IsTerminal() && std::abs(rv) > cutoff) {
+        returns[2 * r + player] = rv;
+        returns[2 * r + 1 - player] = -rv;
+        stopped = true;
+        break;
+      }
+    }
+    for (int k = m; k < max_len; ++k) actions[r * max_len + k] = -1;
+    len[r] = m;
+    if (!stopped) {
+      const std::vector<double> ret = state->Returns();
+      returns[2 * r] = ret[0];
+      returns[2 * r + 1] = ret[1];
+    }
+  }
+  return 0;
+}
+
 // mcts_test.cc:24-36 InitBot bots driven by EvaluateBots (evaluate_bots.cc:
 // 24-61): num_bots MCTSBots (seeds bot_seeds[i]) sharing ONE
 // RandomRolloutEvaluator(n_rollouts, eval_seed); chance nodes sampled by

@@ -85,6 +85,11 @@ def lib():
         ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _u32p, _u32p, _u32p,
         ctypes.c_double, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
         ctypes.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
+    L.oref_az_actor.argtypes = [
+        ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double, ctypes.c_int32,
+        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+        _u32p, _u32p, ctypes.c_double, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
+        ctypes.c_double, EVAL_CB, ctypes.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
     L.oref_evaluate_mcts_bots.restype = ctypes.c_int64
     L.oref_evaluate_mcts_bots.argtypes = [
         ctypes.c_void_p, ctypes.c_int32, _u32p, ctypes.c_int32, ctypes.c_uint32,
@@ -225,6 +230,40 @@ class Game:
         np.ascontiguousarray(bot_seeds, dtype=np.uint32), fn, mc, out["child_action"],
         out["child_n"], out["child_w"], out["child_out"], out["nchild"], out["root_n"],
         out["root_w"], out["root_out"], out["best_action"], out["nodes"])
+    return out
+
+  def az_actor(self, start_actions, start_offsets, bot_seeds, actor_seeds, eval_fn, max_len,
+               uct_c=2.0, max_simulations=50, max_memory_mb=10, solve=False, puct=True,
+               dirichlet_alpha=0.0, dirichlet_epsilon=0.0, temperature=1.0,
+               temperature_drop=10, resign=False, cutoff_value=0.9, cutoff_probability=0.8):
+    """AlphaZero actor games (oref_az_actor): MCTSBots with the external
+    evaluator eval_fn(history, kind) -> (prior [A], player-0 value)."""
+    G = len(start_offsets) - 1
+    A = self.num_distinct_actions
+    out = dict(actions=np.zeros((G, max_len), np.int64), length=np.zeros(G, np.int32),
+               returns=np.zeros((G, 2), np.float64),
+               policy=np.zeros((G, max_len, A), np.float64),
+               root_value=np.zeros((G, max_len), np.float64))
+
+    def cb(hist, n, kind, prior_out, value_out):
+      pr, v = eval_fn([int(hist[i]) for i in range(n)], int(kind))
+      for a in range(A):
+        prior_out[a] = float(pr[a])
+      value_out[0] = float(v)
+      return 0
+
+    fn = EVAL_CB(cb)
+    rc = lib().oref_az_actor(
+        self._h, G, np.ascontiguousarray(start_actions, dtype=np.int64),
+        np.ascontiguousarray(start_offsets, dtype=np.int64), uct_c, max_simulations,
+        max_memory_mb, int(solve), int(puct), float(dirichlet_alpha), float(dirichlet_epsilon),
+        np.ascontiguousarray(bot_seeds, dtype=np.uint32).reshape(-1),
+        np.ascontiguousarray(actor_seeds, dtype=np.uint32), float(temperature),
+        int(temperature_drop), int(bool(resign)), float(cutoff_value),
+        float(cutoff_probability), fn, max_len, out["actions"], out["length"], out["returns"],
+        out["policy"], out["root_value"])
+    if rc:
+      raise RuntimeError("oref_az_actor: game longer than max_len")
     return out
 
   def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
