@@ -85,6 +85,12 @@ def parse():
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
                   help="target CPU-baseline sample duration")
   ap.add_argument("--parity-roots", type=int, default=32)
+  ap.add_argument("--az-graph", type=int, default=1,
+                  help="az: replay each evaluator round as one captured HIP graph (1) "
+                       "or launch it op by op (0)")
+  ap.add_argument("--az-requests", default="fused", choices=("fused", "separate"),
+                  help="az: one evaluator round per simulation (pure evaluator) or "
+                       "the reference's separate Prior / Evaluate rounds")
   ap.add_argument("--rehearse-host", action="store_true",
                   help="CPU test-suite rehearsal of the rank plumbing (gloo, host "
                        "engine from tests/); not a measurement")
@@ -322,7 +328,7 @@ def bench_search(args, ctx, layout):
   stats = eng.stats()
 
   parity = None
-  if ctx.rank == 0:
+  if ctx.rank == 0 and args.parity_roots > 0:
     og = _oracle(game)
     pr = min(args.parity_roots, R)
     ref = og.mcts_batch(acts[:offs[pr]], offs[:pr + 1], bot_seeds[:pr], eval_seeds[:pr],
@@ -412,7 +418,7 @@ def bench_root_parallel(args, ctx, layout):
     ctx.dist.all_reduce(lv)
   reduce_ok = bool(torch.equal(lv, v))
   parity = None
-  if ctx.rank == 0:
+  if ctx.rank == 0 and args.parity_roots > 0:
     og = _oracle(game)
     pr = min(args.parity_roots, 4, T)
     acts = np.zeros(0, np.int64)
@@ -538,7 +544,7 @@ def bench_selfplay(args, ctx, layout):
   moves = int(out["length"].sum())
   sims_step = eng.last_sims()
   parity = None
-  if ctx.rank == 0:
+  if ctx.rank == 0 and args.parity_roots > 0:
     pg = min(args.parity_roots, 8, G)
     ref = _oracle(game).selfplay(acts[:offs[pg]], offs[:pg + 1], bot[:pg], ev[:pg], L,
                                  max_simulations=sims)
@@ -548,6 +554,17 @@ def bench_selfplay(args, ctx, layout):
   elapsed, kernel_ms = ctx.timed(lambda: eng.selfplay_run_async(handle), args.steps)
   total_moves = ctx.total(moves * args.steps)
   total_sims = ctx.total(sims_step * args.steps)
+  out = eng.selfplay_fetch()
+  st = eng.stats()  # summed over the games of the last timed launch
+  # Algorithmic bytes of one k_wselfplay launch: every move is
+  # one search with the tree traffic of algorithmic_bytes (one root state per
+  # move), plus the move's outputs -- its action (8 B) and the root's visit
+  # row (4 B x num_distinct_actions, zeroed then filled).
+  A = eng.num_distinct_actions
+  alg = eng.algorithmic_bytes(moves) + moves * (8 + 4 * A)
+  cpu = None
+  if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+    cpu = cpu_baseline_selfplay(game, acts, offs, bot, ev, L, sims, args.cpu_seconds)
   if ctx.rank != 0:
     return None
   line = _base_line(args, ctx, "self-play MCTS moves/sec on %s (%d sims per move)"
@@ -557,11 +574,13 @@ def bench_selfplay(args, ctx, layout):
                                     % (game, G, sims),
                         "game": game, "games_per_gpu": G, "sims_per_move": sims,
                         "parallelism": "dp%d (independent games)" % ctx.world,
-                        "layout": "wave", "moves_per_step_per_gpu": moves})
+                        "layout": "wave", "moves_per_step_per_gpu": moves,
+                        "sims_per_step_per_gpu": sims_step})
   line["sims_per_s"] = total_sims / elapsed
   line["kernel_ms_per_launch"] = kernel_ms
-  line["roofline"] = None
-  line["cpu_baseline"] = None
+  line["roofline"] = _roofline("k_wselfplay", game, alg, kernel_ms, sims_step, "sim")
+  line["cpu_baseline"] = cpu
+  line["tree_stats"] = st
   line["parity"] = parity
   line["outcomes"] = {"p0_wins": int((out["returns"][:, 0] > 0).sum()),
                       "p1_wins": int((out["returns"][:, 0] < 0).sum()),
@@ -622,9 +641,9 @@ def bench_az(args, ctx, layout):
   obs_size = int(np.prod(search.obs_shape))
   net = _az_network(obs_size, A, torch, ctx.dev)
   kw = dict(puct=True, max_simulations=sims, uct_c=c, dirichlet_alpha=alpha,
-            dirichlet_epsilon=eps, stream=ctx.stream)
+            dirichlet_epsilon=eps, stream=ctx.stream, requests=args.az_requests)
   parity = None
-  if ctx.rank == 0:  # exact toy evaluator on a prefix vs the oracle
+  if ctx.rank == 0 and args.parity_roots > 0:  # exact toy evaluator on a prefix vs the oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_az
     pr = min(args.parity_roots, R)
@@ -639,7 +658,7 @@ def bench_az(args, ctx, layout):
               "bit_exact": not bad, "mismatch_fields": bad}
 
   def step():
-    search.run(acts, offs, seeds, net, **kw)
+    search.run(acts, offs, seeds, net, graph=args.az_graph, **kw)
 
   for _ in range(args.warmup):
     step()
@@ -658,11 +677,15 @@ def bench_az(args, ctx, layout):
   # (DESIGN.md §7): tree traffic as in the search kernels with 24-B f64 nodes
   # plus an 8-B prior per child read by PUCT; per request, the observation,
   # legal mask and kind written and the response read; per launch per live
-  # search, its continuation header + working state read and written.
+  # search, its continuation header + working state read and written; fused
+  # requests also park each leaf's priors (8 B per legal action, written once,
+  # read at the expansion).
   sb = st["state_bytes"]
   nb = 24
   tree = (st["scanned"] * (nb + 8) + st["backed"] * 2 * nb + st["expanded"] * (nb + 8) +
           st["solver_scanned"] * nb + st["rng_words"] * 8)
+  if args.az_requests == "fused":
+    tree += (st["used"] - R) * 8 + st["expanded"] * 8
   io = requests * (obs_size * 4 + A + 4 + A * 8 + 8)
   cont = requests * 2 * (sb + 64)
   alg = tree + io + cont
@@ -674,13 +697,20 @@ def bench_az(args, ctx, layout):
                                     "hidden) on the same GPU" % (game, R, sims, c, alpha, eps, 256),
                         "game": game, "searches_per_gpu": R, "sims_per_search": sims,
                         "parallelism": "dp%d (independent searches)" % ctx.world,
-                        "layout": "lane (continuation in HBM)"})
+                        "layout": "lane (continuation in HBM)",
+                        "evaluator_requests": args.az_requests,
+                        "rounds": "hip graph replay" if args.az_graph else "eager",
+                        "sims_per_step_per_gpu": sims_step,
+                        "units_per_launch": requests / max(launches, 1)})
   line["az"] = {"launches_per_step": launches, "requests_per_step": requests,
                 "k_az_step_ms_total": step_ms,
                 "k_az_step_share_of_step": step_ms / (elapsed / max(args.steps, 1) * 1e3)}
   line["roofline"] = _roofline("k_az_step", game, alg / max(launches, 1), kernel_ms,
                                requests / max(launches, 1), "request")
-  line["cpu_baseline"] = None
+  cpu = None
+  if ctx.world == 1 and not args.no_cpu_baseline:
+    cpu = cpu_baseline_az(game, acts, offs, seeds, sims, c, alpha, eps, args.cpu_seconds)
+  line["cpu_baseline"] = cpu
   line["parity"] = parity
   line["tree_stats"] = st
   return line
@@ -753,6 +783,58 @@ def cpu_baseline_search(game, acts, offs, bot_seeds, eval_seeds, sims, seconds):
           "sample": "%d pass(es) over %d of the %d roots x %d sims (%d sims, %.1f s), "
                     "oracle restatement of mcts.cc; %s" %
                     (passes, want, R, sims, total_n, total_s, cores_desc)}
+
+
+def cpu_baseline_selfplay(game, acts, offs, bot, ev, max_len, sims, seconds):
+  """Oracle self-play (two MCTSBots + shared RandomRolloutEvaluator per game,
+  oracle/ref_capi.cc oref_selfplay) on every usable host core over a prefix
+  of the same games, grown until one pass takes >= `seconds`."""
+  og = _oracle(game)
+  threads, cores_desc = host_cores()
+  G = len(offs) - 1
+  n = min(G, threads)
+  secs = moves = passes = 0
+  while secs < seconds:
+    t0 = time.perf_counter()
+    r = og.selfplay(acts[:offs[n]], offs[:n + 1], bot[:n], ev[:n], max_len,
+                    max_simulations=sims, with_visits=False, threads=threads)
+    dt = time.perf_counter() - t0
+    if n < G and dt < seconds:  # grow the prefix; time only full-size passes
+      n = min(G, max(n + threads, int(n * min(8.0, 1.2 * seconds / max(dt, 1e-3)))))
+      continue
+    secs, moves, passes = secs + dt, moves + int(r["length"].sum()), passes + 1
+  cal = calibration(game)
+  ref_eq = (moves / secs / cal["oracle_over_reference"]) if isinstance(cal, dict) else None
+  return {"value": moves / secs, "unit": "moves/s", "cores": threads, "kind": "port",
+          "calibration": cal, "reference_equivalent": ref_eq,
+          "sample": "%d pass(es) over %d of the %d games (%d moves x %d sims, %.1f s), oracle "
+                    "restatement of two MCTSBots sharing one RandomRolloutEvaluator; %s" %
+                    (passes, n, G, moves, sims, secs, cores_desc)}
+
+
+def cpu_baseline_az(game, acts, offs, seeds, sims, uct_c, alpha, eps, seconds):
+  """Oracle MCTSBot PUCT searches with Dirichlet root noise and a native
+  evaluator that costs nothing (uniform prior, zero value;
+  oref_time_mcts_zero_eval): the host's search speed with the network's time
+  excluded, on every usable host core."""
+  og = _oracle(game)
+  threads, cores_desc = host_cores()
+  R = len(offs) - 1
+  n = min(R, 2 * threads)
+  secs = done = passes = 0
+  while secs < seconds:
+    dt, k = og.time_mcts_zero_eval(acts[:offs[n]], offs[:n + 1], seeds[:n], uct_c=uct_c,
+                                   max_simulations=sims, puct=True, dirichlet_alpha=alpha,
+                                   dirichlet_epsilon=eps, threads=threads)
+    if n < R and dt < seconds:
+      n = min(R, max(n + threads, int(n * min(8.0, 1.2 * seconds / max(dt, 1e-3)))))
+      continue
+    secs, done, passes = secs + dt, done + k, passes + 1
+  return {"value": done / secs, "unit": "sims/s", "cores": threads, "kind": "port",
+          "sample": "%d pass(es) over %d of the %d searches x %d sims (%d sims, %.1f s), "
+                    "oracle MCTSBot (PUCT, Dirichlet) with a free native evaluator -- "
+                    "network time excluded, the GPU line's included; %s" %
+                    (passes, n, R, sims, done, secs, cores_desc)}
 
 
 def cpu_baseline_playouts(game, seconds):

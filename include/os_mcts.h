@@ -214,7 +214,7 @@ int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
  * searches (bot rng seed bot_seeds[r]) advances, one os_az_step_async at a
  * time, to its next evaluator request, written into CALLER-OWNED DEVICE
  * buffers so the caller's network reads them in place:
- *   dev_kind[r]          0 none (finished), 1 Prior, 2 Evaluate
+ *   dev_kind[r]          0 none (finished), 1 Prior, 2 Evaluate, 3 both
  *   dev_obs[r][C*H*W]    ObservationTensor(current player), f32
  *   dev_legal[r][A]      legal-action mask (u8)
  * and answered before the next step in
@@ -249,6 +249,17 @@ int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,
                            uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
                            int32_t* dev_pending);
 int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos);
+/* Request mode of the next os_az_prepare*.  OS_AZ_REQUESTS_SEPARATE (default)
+ * asks exactly what the reference MCTSBot asks, when it asks it: Prior at an
+ * expansion, Evaluate at a leaf -- two evaluator rounds per simulation.
+ * OS_AZ_REQUESTS_FUSED, for an evaluator that is a pure function of
+ * (observation, legal actions) such as VPNetEvaluator (vpevaluator.cc:70-98,
+ * one cached inference serves both calls): every leaf request is kind 3 and
+ * its priors are kept for the node's later expansion, so each simulation
+ * costs one round.  Results are identical for a pure evaluator. */
+#define OS_AZ_REQUESTS_SEPARATE 0
+#define OS_AZ_REQUESTS_FUSED 1
+int os_az_set_requests(os_engine* e, int32_t mode);
 /* The Dirichlet noise os_az_prepare draws for one fresh MCTSBot(seed) at a
  * root with `count` legal actions: out[count] (normalised, legal-action
  * order); returns the MT19937 words consumed (< 0 on error).  Exposed so the

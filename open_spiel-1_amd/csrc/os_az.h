@@ -25,6 +25,18 @@
 // it consumed; the kernel mixes the priors and advances its stream by that
 // count.  go's positional-superko set of the pending simulation lives in the
 // continuation (AzLog), so searches resume mid-descent with it intact.
+//
+// Fused requests (`raw` != nullptr; os_az_set_requests OS_AZ_REQUESTS_FUSED):
+// for an evaluator that is a pure function of (observation, legal actions) --
+// VPNetEvaluator is: both calls are one cached inference of the same network
+// on the same input (vpevaluator.cc:70-98) -- the leaf's Evaluate request also
+// asks for its Prior (kAzBoth).  The priors are parked in legal-action order
+// in `raw`, in the arena slots the leaf's children will occupy (nodes[x].first
+// is set while nchild is still 0), and the expansion that the reference does
+// on the node's next visit takes them from there -- with the bot rng's shuffle
+// and Dirichlet mixing at exactly the same point of the stream.  Every
+// simulation then costs one evaluator round instead of two; results are
+// unchanged for a pure evaluator.
 #ifndef OS_AZ_H_
 #define OS_AZ_H_
 
@@ -33,7 +45,7 @@
 namespace osm {
 
 enum AzStage : int32_t { kAzStart = 0, kAzWaitPrior = 1, kAzWaitValue = 2, kAzDone = 3 };
-enum AzRequest : int32_t { kAzNone = 0, kAzPrior = 1, kAzValue = 2 };
+enum AzRequest : int32_t { kAzNone = 0, kAzPrior = 1, kAzValue = 2, kAzBoth = 3 };
 
 constexpr int kAzLogCap = 248;  // go: positions after the root on one tree path (<= 2 * 11 * 11)
 constexpr int kAzHeads = 122;   // go: stone-count buckets, 0 .. 11 * 11
@@ -97,7 +109,7 @@ struct AzIo {
   int32_t* kind;         // out: kAzNone / kAzPrior / kAzValue
   float* obs;            // out: ObservationTensor(current player), obs_size
   uint8_t* legal;        // out: legal-action mask, num_actions
-  const double* prior;   // in: action-indexed priors (read for legal actions)
+  const double* prior;   // in: action-indexed priors (read for legal actions; kAzPrior, kAzBoth)
   const double* value;   // in: player-0 value (Evaluate returns {v, -v})
 };
 
@@ -117,11 +129,13 @@ OS_HD void az_request(const GameCfg& g, const typename G::State& s, int kind, co
 // or finishes (kind = kAzNone, stage = kAzDone).  `ctx` is the game's
 // history context with its root fields set (go: Zobrist table, the positions
 // before the root, n_heads); its log is bound to the continuation here.
+// `raw` ([cap], or nullptr for separate Prior / Evaluate requests): the parked
+// priors of fused requests (see above).
 template <class G>
 OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
                    const typename G::State& root, AzSlot<G>& sl, Node<double>* nodes,
-                   double* prior, uint32_t cap, MtStream& bot, const AzIo& io, int obs_size,
-                   int num_actions, typename G::Ctx& ctx, const AzNoise& nz) {
+                   double* prior, double* raw, uint32_t cap, MtStream& bot, const AzIo& io,
+                   int obs_size, int num_actions, typename G::Ctx& ctx, const AzNoise& nz) {
   az_bind_log(ctx, sl.glog, sl.stage != kAzStart);
   const int P0 = G::to_move(root);
   const double inf = __builtin_huge_val();
@@ -130,6 +144,7 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
   int phase;  // 0 new simulation, 1 descend, 2 expand with priors, 3 value ready
   double v0 = 0.0;
   bool solved = false;
+  bool from_raw = false;  // phase 2 takes the parked priors of a fused request
   if (sl.stage == kAzDone) {
     *io.kind = kAzNone;
     return;
@@ -157,8 +172,22 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
     v0 = *io.value;
     solved = false;
     phase = 3;
+    if (raw != nullptr) {
+      // Park the leaf's priors (legal order) where its children will live.
+      const typename G::Legal l = G::legal(s, g, ctx);
+      const int nc = l.count;
+      if (sl.used + static_cast<uint32_t>(nc) > cap) {
+        sl.res.status = kArenaOverflow;
+        phase = -1;
+      } else {
+        for (int j = 0; j < nc; ++j) raw[sl.used + j] = io.prior[l.kth(j)];
+        nodes[sl.path[depth]].first = sl.used;
+        sl.used += nc;
+      }
+    }
   }
   for (;;) {
+    if (phase < 0) break;
     if (phase == 0) {
       if (sl.sim >= sp.max_simulations) break;
       s = root;
@@ -173,7 +202,7 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
       const uint32_t x = sl.path[depth];
       const typename G::Legal l = G::legal(s, g, ctx);
       const int nc = l.count;
-      if (sl.used + static_cast<uint32_t>(nc) > cap) {
+      if (!from_raw && sl.used + static_cast<uint32_t>(nc) > cap) {
         sl.res.status = kArenaOverflow;
         break;
       }
@@ -183,10 +212,11 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
       uint8_t perm[kMaxChildren];
       for (int k = 0; k < nc; ++k) perm[k] = static_cast<uint8_t>(k);
       CppShuffle(perm, nc, bot);
-      const uint32_t first = sl.used;
+      const uint32_t first = from_raw ? nodes[x].first : sl.used;
       for (int k = 0; k < nc; ++k) {
         const int j = perm[k];
         const int a = l.kth(j);
+        const double p = from_raw ? raw[first + j] : io.prior[a];
         Node<double>& c = nodes[first + k];
         c.first = 0;
         c.n = 0;
@@ -195,12 +225,12 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         c.nchild = 0;
         c.out = kUnsolved;
         // (1 - eps) * p + eps * noise, separately rounded (mcts.cc:269-271)
-        prior[first + k] = noisy ? (1.0 - nz.eps) * io.prior[a] + nz.eps * nz.noise[j]
-                                 : io.prior[a];
+        prior[first + k] = noisy ? (1.0 - nz.eps) * p + nz.eps * nz.noise[j] : p;
       }
       nodes[x].first = first;
       nodes[x].nchild = static_cast<uint8_t>(nc);
-      sl.used += nc;
+      if (!from_raw) sl.used += nc;
+      from_raw = false;
       sl.nodes_count += nc;
       sl.res.expanded += nc;
       phase = 1;
@@ -210,6 +240,10 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         const uint32_t x = sl.path[depth];
         const Node<double> nx = nodes[x];
         if (G::terminal(s, g) || nx.n <= 0) break;
+        if (nx.nchild == 0 && raw != nullptr && nx.first != 0) {
+          from_raw = true;  // parked by this node's fused request: expand now
+          break;
+        }
         if (nx.nchild == 0) {
           sl.s = s;
           sl.depth = depth;
@@ -254,6 +288,10 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         }
         sl.path[depth] = ci;
       }
+      if (from_raw) {
+        phase = 2;
+        continue;
+      }
       if (depth > sl.res.max_depth) sl.res.max_depth = depth;
       if (G::terminal(s, g)) {
         const int r0 = G::ret0(s, g, ctx);
@@ -266,7 +304,7 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         sl.depth = depth;
         az_save_log(ctx, sl.glog);
         sl.stage = kAzWaitValue;
-        az_request<G>(g, s, kAzValue, io, obs_size, num_actions, ctx);
+        az_request<G>(g, s, raw != nullptr ? kAzBoth : kAzValue, io, obs_size, num_actions, ctx);
         return;
       }
     }

@@ -762,6 +762,11 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   if ((rc = e->d_az_slots.ensure(Rz * slot_bytes)) ||
       (rc = e->d_az_prior.ensure(Rz * static_cast<size_t>(e->cap) * 8)))
     return rc;
+  // Fused requests park each evaluated leaf's priors until its expansion; the
+  // reserved arena (1 + sims * max_children) bounds them, as every simulation
+  // parks at most one leaf's children.
+  e->az_fused = e->az_requests == OS_AZ_REQUESTS_FUSED;
+  if (e->az_fused && (rc = e->d_az_raw.ensure(Rz * static_cast<size_t>(e->cap) * 8))) return rc;
   HIP_TRY(hipMemset(e->d_az_slots.p, 0, Rz * slot_bytes));  // stage kAzStart
   e->az_noise = alpha > 0.0;
   e->az_eps = eps;
@@ -1309,6 +1314,14 @@ int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,
   return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, nullptr, dirichlet_alpha,
                    dirichlet_epsilon, dev_kind, dev_obs, dev_legal, dev_prior, dev_value,
                    dev_pending, bot_keys ? bot_keys : nullptr, bot_pos);
+}
+
+int os_az_set_requests(os_engine* e, int32_t mode) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (mode != OS_AZ_REQUESTS_SEPARATE && mode != OS_AZ_REQUESTS_FUSED)
+    return Fail(OS_ERR_INVALID, "unknown request mode");
+  e->az_requests = mode;
+  return OS_OK;
 }
 
 int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos) {

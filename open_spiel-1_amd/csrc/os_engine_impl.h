@@ -135,6 +135,7 @@ struct AzArgs {
   void* slots;              // [R] AzSlot<G>
   Node<double>* arena;      // [R][cap]
   double* priors;           // [R][cap]
+  double* raw;              // [R][cap] parked priors of fused requests, or null
   uint32_t cap;
   uint32_t* mt;             // [R][624] bot rng
   const uint32_t* bot_seeds;
@@ -261,7 +262,9 @@ struct os_engine {
   double az_eps = 0.0;
   bool az_noise = false;
   bool az_import = false;  // os_az_prepare_stateful
-  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos;
+  int32_t az_requests = 0;  // os_az_set_requests (OS_AZ_REQUESTS_SEPARATE)
+  bool az_fused = false;    // mode of the prepared batch
+  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw;
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -293,7 +296,7 @@ struct os_engine {
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
-                     &d_sp_actor, &d_sp_pow, &d_az_pos};
+                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

@@ -70,8 +70,12 @@ struct CtxMaker<Go> {
   }
 };
 
+// One wave per workgroup at most (LaunchSearch clamps the block): with the
+// default 1024-thread bound the compiler caps VGPRs at 128 and spills the
+// search's working set to scratch, and lanes 32-63 of a wave64 running such
+// spill-heavy code returned wrong results on MI355X (k_az_step).
 template <class G, class R, int Policy>
-__global__ void k_mcts(DevArgs a) {
+__global__ __launch_bounds__(64) void k_mcts(DevArgs a) {
   const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (lr >= a.num_roots) return;
   const int64_t gr = a.root_base + lr;
@@ -549,8 +553,12 @@ struct AzCtx<Go> {
   }
 };
 
+// __launch_bounds__(64) matches the launch and lifts the 128-VGPR cap of the
+// default bound: without it the state machine spilled ~800 VGPRs to scratch
+// and searches in lanes 32-63 of each wave64 diverged from the oracle
+// (test_az.py many_roots); with it nothing spills to scratch.
 template <class G>
-__global__ void k_az_step(AzArgs a) {
+__global__ __launch_bounds__(64) void k_az_step(AzArgs a) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r >= a.num_roots) return;
   AzSlot<G>& sl = static_cast<AzSlot<G>*>(a.slots)[r];
@@ -587,7 +595,8 @@ __global__ void k_az_step(AzArgs a) {
   nz.eps = a.noise_eps;
   typename G::Ctx ctx = AzCtx<G>::make(a, r);
   az_step<G>(a.cfg, a.sp, a.puct, root, sl, nodes, a.priors + r * static_cast<int64_t>(a.cap),
-             a.cap, bot, io, a.obs_size, a.num_actions, ctx, nz);
+             a.raw ? a.raw + r * static_cast<int64_t>(a.cap) : nullptr, a.cap, bot, io,
+             a.obs_size, a.num_actions, ctx, nz);
   sl.mt_idx = bot.idx;
   sl.mt_pre = bot.pre;
   sl.res.rng_words += bot.words;
@@ -806,6 +815,7 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
     return Fail(OS_ERR_UNSUPPORTED, "go runs on the wave layout only (OS_LAYOUT_WAVE / AUTO)");
   } else {
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
+  if (bs > 64) bs = 64;  // k_mcts's __launch_bounds__
   const size_t per_lane = LdsPerLane<R>(a.path_cap, a.child_cap);
   if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
   if (bs < 1) return Fail(OS_ERR_CAPACITY, "per-lane LDS slice exceeds the CU's LDS");
@@ -919,6 +929,7 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.slots = e->d_az_slots.p;
   a.arena = static_cast<Node<double>*>(e->d_arena.p);
   a.priors = static_cast<double*>(e->d_az_prior.p);
+  a.raw = e->az_fused ? static_cast<double*>(e->d_az_raw.p) : nullptr;
   a.cap = e->cap;
   a.mt = static_cast<uint32_t*>(e->d_mt.p);
   a.bot_seeds = d.bot_seeds;

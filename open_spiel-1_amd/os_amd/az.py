@@ -15,11 +15,18 @@ in place and writes priors / values back -- no host round trip of the data.
 
 `evaluator(obs, legal, kind)` receives torch tensors on the GPU:
 obs float32 [N, C, H, W] (ObservationTensor of the player to move), legal bool
-[N, A], kind int32 [N] (1 = Prior wanted, 2 = Evaluate wanted, 0 = idle), and
-returns (prior float64 [N, A] action-indexed, value float64 [N] for player 0).
-Entries whose kind is 0 are ignored.  Results are bit-exact with the reference
-`MCTSBot(game, evaluator, uct_c, max_simulations, max_memory_mb, solve, seed,
-false, child_selection_policy)` driving the same evaluator.
+[N, A], kind int32 [N] (1 = Prior wanted, 2 = Evaluate wanted, 3 = both,
+0 = idle), and returns (prior float64 [N, A] action-indexed, value float64 [N]
+for player 0).  Entries whose kind is 0 are ignored.  Results are bit-exact with
+the reference `MCTSBot(game, evaluator, uct_c, max_simulations, max_memory_mb,
+solve, seed, false, child_selection_policy)` driving the same evaluator.
+
+requests="fused" (the default) suits an evaluator that is a pure function of
+(obs, legal) -- VPNetEvaluator is (vpevaluator.cc:70-98: Prior and Evaluate
+are one cached inference): each leaf asks for value AND prior at once (kind
+3) and the prior is kept for the node's later expansion, so a simulation costs
+one evaluator round, not two (include/os_mcts.h os_az_set_requests).
+requests="separate" asks exactly what the reference asks, when it asks it.
 """
 import ctypes
 
@@ -29,7 +36,8 @@ from . import _lib
 from . import engine as E
 from ._lib import check, lib, ptr
 
-KIND_NONE, KIND_PRIOR, KIND_VALUE = 0, 1, 2
+KIND_NONE, KIND_PRIOR, KIND_VALUE, KIND_BOTH = 0, 1, 2, 3
+_REQUESTS = {"separate": _lib.AZ_REQUESTS_SEPARATE, "fused": _lib.AZ_REQUESTS_FUSED}
 
 
 class ExternalEvaluatorSearch:
@@ -48,7 +56,7 @@ class ExternalEvaluatorSearch:
   def run(self, root_actions, root_offsets, bot_seeds, evaluator, puct=True,
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
           dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False,
-          bot_rng=None):
+          bot_rng=None, requests="fused", graph=False, graph_batch=8):
     """Runs every search to completion; returns the os_mcts_batch outputs.
 
     The evaluator may be called once more after the last step, with every
@@ -62,6 +70,14 @@ class ExternalEvaluatorSearch:
     noise drawn from the bot's rng before the root's shuffle (mcts.cc:265-273).
     time_steps: record a HIP event pair around every k_az_step launch on the
     launch stream (`step_ms()` then sums them).
+
+    graph=True: after two eager rounds, one round (k_az_step + the evaluator +
+    the response copies) is captured into a HIP graph and replayed
+    `graph_batch` times per host check of the pending count, so the host
+    neither launches each op nor waits on every round.  The evaluator must be
+    capturable (static shapes, no host synchronisation); rounds replayed after
+    the last search finished see only idle (kind 0) entries.  Not with
+    time_steps.
     """
     torch = self.torch
     offs = _lib.i64(root_offsets)
@@ -77,6 +93,9 @@ class ExternalEvaluatorSearch:
     p = E.make_params(uct_c=uct_c, max_simulations=max_simulations,
                       max_memory_mb=max_memory_mb, solve=solve)
     acts = _lib.i64(root_actions)
+    if requests not in _REQUESTS:
+      raise ValueError("requests must be 'fused' or 'separate'")
+    check(lib.os_az_set_requests(self.eng._h, _REQUESTS[requests]))
     if bot_rng is None:
       bs = _lib.u32(bot_seeds)
       check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
@@ -103,6 +122,9 @@ class ExternalEvaluatorSearch:
     # step k had left nothing pending, and its outputs are never read.
     pend_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
     done = torch.cuda.Event()
+    if graph and time_steps:
+      raise ValueError("time_steps needs eager rounds (graph=False)")
+    eager_rounds = 2 if graph else None
     while True:
       if time_steps:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -123,6 +145,10 @@ class ExternalEvaluatorSearch:
       if n == 0:
         break
       self.requests += n
+      if eager_rounds is not None and self.steps >= eager_rounds:
+        self._replay(st, evaluator, kind, obs, legal, prior, value, pending, pend_host,
+                     done, graph_batch)
+        break
     o = E._alloc_outputs(R, self.eng.max_children)
     check(lib.os_az_fetch(self.eng._h, self.eng.max_children, *E._out_ptrs(o)))
     if bot_rng is not None:
@@ -131,6 +157,34 @@ class ExternalEvaluatorSearch:
       check(lib.os_az_export_rng(self.eng._h, ptr(keys), ptr(pos)))
       self.bot_rng_out = (keys, pos)
     return o
+
+  def _replay(self, st, evaluator, kind, obs, legal, prior, value, pending, pend_host, done,
+              batch):
+    """Captures one round into a HIP graph and replays it until no search
+    is pending (checked every `batch` rounds)."""
+    torch = self.torch
+    total = torch.zeros(1, dtype=torch.int64, device=self.device)
+    g = torch.cuda.CUDAGraph()
+    st.synchronize()
+    with torch.cuda.graph(g):
+      cs = torch.cuda.current_stream(self.device)
+      check(lib.os_az_step_async(self.eng._h, cs.cuda_stream))
+      pr, v = evaluator(obs, legal.bool(), kind)
+      prior.copy_(pr)
+      value.copy_(v)
+      total.add_(pending)
+    with torch.cuda.stream(st):
+      while True:
+        for _ in range(batch):
+          g.replay()
+          self.steps += 1
+        pend_host.copy_(pending, non_blocking=True)
+        done.record(st)
+        done.synchronize()
+        if int(pend_host[0]) == 0:
+          break
+    st.synchronize()
+    self.requests += int(total.item())
 
   def step_ms(self):
     """Summed k_az_step time of the last run(time_steps=True), ms."""
@@ -164,7 +218,8 @@ class AlphaZeroActor:
   def play(self, start_actions, start_offsets, bot_seeds, actor_seeds, evaluator, max_len=None,
            uct_c=2.0, max_simulations=50, temperature=1.0, temperature_drop=10, resign=False,
            cutoff_value=0.9, cutoff_probability=0.8, dirichlet_alpha=0.0,
-           dirichlet_epsilon=0.0, solve=False, max_memory_mb=10, puct=True):
+           dirichlet_epsilon=0.0, solve=False, max_memory_mb=10, puct=True,
+           requests="fused"):
     """Plays G games; bot_seeds [G][2], actor_seeds [G].  Returns dict(actions
     [G][L] (-1 padded), length [G], returns [G][2], policy [G][L][A] (action-
     indexed), root_value [G][L])."""
@@ -220,7 +275,8 @@ class AlphaZeroActor:
       o = self.search.run(ra, ro, None, evaluator, puct=puct, max_simulations=max_simulations,
                           uct_c=uct_c, solve=solve, max_memory_mb=max_memory_mb,
                           dirichlet_alpha=dirichlet_alpha,
-                          dirichlet_epsilon=dirichlet_epsilon, bot_rng=(rk, rp))
+                          dirichlet_epsilon=dirichlet_epsilon, bot_rng=(rk, rp),
+                          requests=requests)
       self.searches += len(live)
       nk, npos = self.search.bot_rng_out
       still = []

@@ -436,6 +436,50 @@ int oref_selfplay(void* g, int64_t num_games, const int64_t* start_actions,
   return err.load() ? -1 : 0;
 }
 
+// CPU baseline of the external-evaluator search (bench.py --config az): the
+// same MCTSBot (PUCT, Dirichlet root noise) with a native evaluator that costs
+// nothing -- uniform Prior over LegalActions, Evaluate = {0, 0} -- so the time
+// is the search's own; R searches on `threads` host threads.  Returns seconds.
+class ZeroEvaluator : public oref::Evaluator {
+ public:
+  std::vector<double> Evaluate(const RState&) override { return {0.0, 0.0}; }
+  std::vector<std::pair<Action, double>> Prior(const RState& state) override {
+    const std::vector<Action> legal = state.LegalActions();
+    std::vector<std::pair<Action, double>> out;
+    for (Action a : legal) out.emplace_back(a, 1.0 / legal.size());
+    return out;
+  }
+};
+
+double oref_time_mcts_zero_eval(void* g, int64_t num_roots, const int64_t* root_actions,
+                                const int64_t* root_offsets, double uct_c,
+                                int32_t max_simulations, int32_t puct, double dirichlet_alpha,
+                                double dirichlet_epsilon, const uint32_t* bot_seeds,
+                                int32_t threads, int64_t* total_sims) {
+  auto* og = static_cast<OGame*>(g);
+  std::atomic<int64_t> sims{0};
+  if (threads < 1) threads = 1;
+  auto t0 = std::chrono::steady_clock::now();
+  auto work = [&](int t) {
+    ZeroEvaluator ev;
+    int64_t local = 0;
+    for (int64_t r = t; r < num_roots; r += threads) {
+      auto state = Replay(*og->game, root_actions + root_offsets[r],
+                          root_offsets[r + 1] - root_offsets[r]);
+      MCTSBot bot(*og->game, &ev, uct_c, max_simulations, 1000, true, bot_seeds[r], puct != 0,
+                  dirichlet_alpha, dirichlet_epsilon);
+      SearchStats st;
+      local += bot.MCTSearch(*state, &st)->explore_count;
+    }
+    sims += local;
+  };
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t) ts.emplace_back(work, t);
+  for (auto& t : ts) t.join();
+  *total_sims = sims.load();
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // AlphaZero's PlayGame (alpha_zero.cc:64-118) over the self-play pairing of
 // oref_selfplay (two MCTSBots, seeds bot_seeds[2g], [2g+1], UCT or PUCT,
 // sharing RandomRolloutEvaluator(n_rollouts, eval_seeds[g])) with one actor

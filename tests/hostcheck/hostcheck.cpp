@@ -183,6 +183,7 @@ int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp
   const int obs_size = ObservationShape(game, nullptr);
   std::vector<Node<double>> nodes(cap);
   std::vector<double> prior(cap);
+  std::vector<double> raw((puct & 2) ? cap : 0);  // fused requests
   std::vector<uint32_t> mt(kMtN);
   mt_seed(mt.data(), seed);
   MtStream bot{mt.data(), kMtN, 0, 0};
@@ -214,8 +215,8 @@ int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp
     nz.noise = noise.data();
   }
   for (;;) {
-    az_step<G>(game.cfg, sp, puct, rs, *sl, nodes.data(), prior.data(), cap, bot, io, obs_size,
-               A, ctx, nz);
+    az_step<G>(game.cfg, sp, puct & 1, rs, *sl, nodes.data(), prior.data(),
+               raw.empty() ? nullptr : raw.data(), cap, bot, io, obs_size, A, ctx, nz);
     if (kind == kAzNone) break;
     std::fill(pri.begin(), pri.end(), 0.0);
     cb(obs.data(), obs_size, legal.data(), A, kind, pri.data(), &value);

@@ -149,9 +149,10 @@ AZ_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_
 
 def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=True,
              uct_c=2.0, max_simulations=100, max_memory_mb=1000, solve=True,
-             dirichlet_alpha=0.0, dirichlet_epsilon=0.0):
+             dirichlet_alpha=0.0, dirichlet_epsilon=0.0, fused=False):
   """csrc/os_az.h stepped on the host; eval_fn(obs float32[obs_size], legal
-  bool[A], kind) -> (prior [A], value)."""
+  bool[A], kind) -> (prior [A], value).  fused: one kind-3 request per
+  simulation (OS_AZ_REQUESTS_FUSED); `calls` in the result counts requests."""
   L = lib()
   vp = ctypes.c_void_p
   L.hc_az_batch.argtypes = [ctypes.c_char_p, ctypes.c_int64, vp, vp, ctypes.c_double,
@@ -167,10 +168,12 @@ def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=Tru
            best_action=np.zeros(R, np.int64), nodes=np.zeros(R, np.int32))
   o["child_action"][:] = -1
   o["child_out"][:] = 2
+  calls = [0]
 
   def cb(obs, obs_size, legal, A, kind, prior_out, value_out):
     ob = np.ctypeslib.as_array(obs, shape=(obs_size,)).copy()
     lg = np.ctypeslib.as_array(legal, shape=(A,)).astype(bool)
+    calls[0] += 1
     pr, v = eval_fn(ob, lg, int(kind))
     for a in range(A):
       prior_out[a] = float(pr[a])
@@ -182,9 +185,10 @@ def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=Tru
   offs = np.ascontiguousarray(offs, np.int64)
   bs = np.ascontiguousarray(bot_seeds, np.uint32)
   rc = L.hc_az_batch(game_string.encode(), R, acts.ctypes.data, offs.ctypes.data, uct_c,
-                     max_simulations, max_memory_mb, int(solve), int(puct),
+                     max_simulations, max_memory_mb, int(solve), int(puct) | (2 if fused else 0),
                      float(dirichlet_alpha), float(dirichlet_epsilon), bs.ctypes.data,
                      fn, mc, *[o[k].ctypes.data for k in KEYS])
   if rc:
     raise RuntimeError(L.hc_last_error().decode())
+  o["calls"] = calls[0]
   return o

@@ -90,6 +90,11 @@ def lib():
         ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
         _u32p, _u32p, ctypes.c_double, ctypes.c_int32, ctypes.c_int32, ctypes.c_double,
         ctypes.c_double, EVAL_CB, ctypes.c_int32, _i64p, _i32p, _f64p, _f64p, _f64p]
+    L.oref_time_mcts_zero_eval.restype = ctypes.c_double
+    L.oref_time_mcts_zero_eval.argtypes = [
+        ctypes.c_void_p, ctypes.c_int64, _i64p, _i64p, ctypes.c_double, ctypes.c_int32,
+        ctypes.c_int32, ctypes.c_double, ctypes.c_double, _u32p, ctypes.c_int32,
+        ctypes.POINTER(ctypes.c_int64)]
     L.oref_evaluate_mcts_bots.restype = ctypes.c_int64
     L.oref_evaluate_mcts_bots.argtypes = [
         ctypes.c_void_p, ctypes.c_int32, _u32p, ctypes.c_int32, ctypes.c_uint32,
@@ -195,6 +200,19 @@ class Game:
         np.ascontiguousarray(bot_seeds, dtype=np.uint32),
         np.ascontiguousarray(eval_seeds, dtype=np.uint32), threads,
         ctypes.byref(sims))
+    return secs, sims.value
+
+  def time_mcts_zero_eval(self, root_actions, root_offsets, bot_seeds, uct_c=2.0,
+                          max_simulations=100, puct=True, dirichlet_alpha=0.0,
+                          dirichlet_epsilon=0.0, threads=1):
+    """(seconds, sims) of MCTSBot searches with a free native evaluator."""
+    R = len(root_offsets) - 1
+    sims = ctypes.c_int64()
+    secs = lib().oref_time_mcts_zero_eval(
+        self._h, R, np.ascontiguousarray(root_actions, dtype=np.int64),
+        np.ascontiguousarray(root_offsets, dtype=np.int64), uct_c, max_simulations, int(puct),
+        dirichlet_alpha, dirichlet_epsilon, np.ascontiguousarray(bot_seeds, dtype=np.uint32),
+        threads, ctypes.byref(sims))
     return secs, sims.value
 
   def mcts_external(self, root_actions, root_offsets, bot_seeds, eval_fn, puct=True,

@@ -74,10 +74,37 @@ def test_host_state_machine_matches_oracle(game, puct):
   A = og.num_distinct_actions
   ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), puct=puct, uct_c=1.5,
                          max_simulations=sims, max_children=A)
-  got = hc.az_batch(game, acts, offs, seeds, A, toy_eval, puct=puct, uct_c=1.5,
+  sep = hc.az_batch(game, acts, offs, seeds, A, toy_eval, puct=puct, uct_c=1.5,
                     max_simulations=sims)
+  fused = hc.az_batch(game, acts, offs, seeds, A, toy_eval, puct=puct, uct_c=1.5,
+                      max_simulations=sims, fused=True)
+  for got in (sep, fused):
+    for k in E.OUTPUT_KEYS:
+      np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+  # one evaluator round per simulation instead of two (terminal leaves ask none)
+  assert fused["calls"] <= int(ref["root_n"].sum())
+  assert fused["calls"] < sep["calls"]
+
+
+@pytest.mark.parametrize("game,sims", [("connect_four", 6000),
+                                       ("breakthrough(rows=6,columns=6)", 2600)])
+def test_host_fused_requests_under_gc(game, sims):
+  # max_memory_mb=1 (13108 nodes): GC (mcts.cc:402-424) prunes expanded nodes
+  # and their re-expansion takes the parked priors again, not a new request.
+  acts, offs = E.roots_from_histories([[]])
+  seeds = np.array([3], np.uint32)
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  kw = dict(puct=True, uct_c=1.5, max_simulations=sims, max_memory_mb=1)
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=A, **kw)
+  sep = hc.az_batch(game, acts, offs, seeds, A, toy_eval, **kw)
+  got = hc.az_batch(game, acts, offs, seeds, A, toy_eval, fused=True, **kw)
   for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(sep[k], ref[k], err_msg=k)
     np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+  big = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=A,
+                         **dict(kw, max_memory_mb=1000))
+  assert int(ref["nodes"][0]) < int(big["nodes"][0])  # GC ran (nodes_ shrank)
 
 
 @pytest.mark.parametrize("noise", NOISE)
@@ -90,10 +117,12 @@ def test_host_state_machine_dirichlet_matches_oracle(game, noise):
   ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), puct=True, uct_c=1.5,
                          max_simulations=sims, max_children=A, dirichlet_alpha=alpha,
                          dirichlet_epsilon=eps)
-  got = hc.az_batch(game, acts, offs, seeds, A, toy_eval, puct=True, uct_c=1.5,
-                    max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps)
-  for k in E.OUTPUT_KEYS:
-    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+  for fused in (False, True):
+    got = hc.az_batch(game, acts, offs, seeds, A, toy_eval, puct=True, uct_c=1.5,
+                      max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps,
+                      fused=fused)
+    for k in E.OUTPUT_KEYS:
+      np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
 
 def test_dirichlet_noise_changes_the_search():
@@ -130,7 +159,47 @@ def _gpu_toy_evaluator(A):
   return evaluator
 
 
-def _check_gpu(game, puct, alpha=0.0, eps=0.0):
+def _torch_toy_evaluator(A):
+  """toy_eval in torch f64 on the device (integer-valued sums, one exact
+  division: the same doubles as the numpy version) -- capturable in a HIP
+  graph."""
+  import torch
+
+  def evaluator(obs, legal, kind):
+    o = obs.reshape(obs.shape[0], -1).double()
+    w = (torch.arange(o.shape[1], device=o.device) % 7 + 1).double()
+    s = (o * w).sum(1)
+    value = (torch.remainder(s, 11.0) - 5.0) / 8.0
+    a = torch.arange(A, device=o.device).double()
+    raw = (1.0 + torch.remainder(a[None, :] * 3 + s[:, None], 5.0)) * legal.double()
+    prior = raw / raw.sum(1, keepdim=True).clamp_min(1.0)
+    return prior, value
+  return evaluator
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("game", ["connect_four", "hex(board_size=5)", "go(board_size=5)"])
+def test_gpu_graph_replayed_rounds_match_oracle(require_gpu, game):
+  from os_amd.az import ExternalEvaluatorSearch
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  R, sims = 80, 20
+  acts, offs = E.make_roots(game, R, seed_base=5, max_plies=4)
+  seeds = np.arange(R, dtype=np.uint32) + 9
+  kw = dict(puct=True, uct_c=1.25, max_simulations=sims, dirichlet_alpha=1.0,
+            dirichlet_epsilon=0.25)
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=A, **kw)
+  search = ExternalEvaluatorSearch(game)
+  for graph in (False, True):
+    got = search.run(acts, offs, seeds, _torch_toy_evaluator(A), graph=graph, graph_batch=4,
+                     **kw)
+    mc = search.eng.max_children
+    for k in E.OUTPUT_KEYS:
+      r = ref[k][:, :mc] if ref[k].ndim == 2 else ref[k]
+      np.testing.assert_array_equal(got[k], r, err_msg="%s graph=%s" % (k, graph))
+
+
+def _check_gpu(game, puct, alpha=0.0, eps=0.0, requests="fused"):
   from os_amd.az import ExternalEvaluatorSearch
   acts, offs, seeds, sims = _roots(game)
   og = oracle_lib.Game(game)
@@ -140,7 +209,8 @@ def _check_gpu(game, puct, alpha=0.0, eps=0.0):
                          dirichlet_epsilon=eps)
   search = ExternalEvaluatorSearch(game)
   got = search.run(acts, offs, seeds, _gpu_toy_evaluator(A), puct=puct, uct_c=1.5,
-                   max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps)
+                   max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps,
+                   requests=requests)
   mc = search.eng.max_children
   for k in E.OUTPUT_KEYS:
     r = ref[k][:, :mc] if ref[k].ndim == 2 else ref[k]
@@ -149,10 +219,47 @@ def _check_gpu(game, puct, alpha=0.0, eps=0.0):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("requests", ["fused", "separate"])
 @pytest.mark.parametrize("puct", [True, False])
 @pytest.mark.parametrize("game", sorted(CASES))
-def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct):
-  _check_gpu(game, puct)
+def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct, requests):
+  _check_gpu(game, puct, requests=requests)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("requests", ["separate", "fused"])
+def test_gpu_external_evaluator_many_roots(require_gpu, requests):
+  # 160 searches: several waves, every lane of a wave64 (the small cases
+  # above run <= 3 roots, all in lanes 0-2).
+  from os_amd.az import ExternalEvaluatorSearch
+  game = "connect_four"
+  R, sims = 160, 24
+  acts, offs = E.make_roots(game, R, seed_base=77, max_plies=6)
+  seeds = np.arange(R, dtype=np.uint32) * 3 + 1
+  og = oracle_lib.Game(game)
+  kw = dict(puct=True, uct_c=1.25, max_simulations=sims, dirichlet_alpha=1.0,
+            dirichlet_epsilon=0.25)
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=7, **kw)
+  got = ExternalEvaluatorSearch(game).run(acts, offs, seeds, _gpu_toy_evaluator(7),
+                                          requests=requests, **kw)
+  bad = sorted({int(r) for k in E.OUTPUT_KEYS
+                for r in np.nonzero((got[k] != ref[k]).reshape(R, -1).any(axis=1))[0]})
+  assert not bad, "roots differing from the oracle: %s" % bad
+
+
+@pytest.mark.gpu
+def test_gpu_fused_requests_halve_the_rounds(require_gpu):
+  from os_amd.az import ExternalEvaluatorSearch
+  acts, offs, seeds, sims = _roots("connect_four")
+  ev = _gpu_toy_evaluator(7)
+  search = ExternalEvaluatorSearch("connect_four")
+  a = search.run(acts, offs, seeds, ev, max_simulations=sims, requests="separate")
+  sep = (search.steps, search.requests)
+  b = search.run(acts, offs, seeds, ev, max_simulations=sims, requests="fused")
+  assert search.steps <= sims + 2 < sep[0]
+  assert search.requests < sep[1]
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 @pytest.mark.gpu
@@ -160,6 +267,7 @@ def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct):
 @pytest.mark.parametrize("game", sorted(CASES))
 def test_gpu_external_evaluator_dirichlet_matches_oracle(require_gpu, game, noise):
   _check_gpu(game, True, *noise)
+  _check_gpu(game, True, *noise, requests="separate")
 
 
 @pytest.mark.gpu
@@ -197,6 +305,7 @@ def test_gpu_alphazero_actor_matches_oracle(require_gpu, game, sims, t, drop, re
             dirichlet_alpha=noise[0], dirichlet_epsilon=noise[1])
   ref = og.az_actor(acts, offs, bots, actor, _oracle_eval_fn(game), og.max_game_length, **kw)
   got = AlphaZeroActor(game).play(acts, offs, bots, actor, _gpu_toy_evaluator(A),
-                                  og.max_game_length, **kw)
+                                  og.max_game_length,
+                                  requests="separate" if resign else "fused", **kw)
   for k in ("actions", "length", "returns", "policy", "root_value"):
     np.testing.assert_array_equal(got[k], ref[k], err_msg=k)

@@ -154,20 +154,22 @@ def test_chance_node_api():
 @pytest.mark.gpu
 @pytest.mark.parametrize("gs", PIGS)
 @pytest.mark.parametrize("policy", ["cpp", "numpy"])
-def test_gpu_search_matches_oracle(require_gpu, gs, policy):
+@pytest.mark.parametrize("block", [0, 64])
+def test_gpu_search_matches_oracle(require_gpu, gs, policy, block):
+  # block 64: full wave64 workgroups, searches in lanes 32-63 too
   from os_amd import _lib
-  R = 64
+  R = 64 if block == 0 else 96
   acts, offs = _roots(gs, R)
   bs = np.arange(R, dtype=np.uint32) * 5 + 3
   es = bs + np.uint32(1 << 20)
   eng = E.Engine(gs)
   if policy == "cpp":
     ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_simulations=300, max_children=6)
-    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300)
+    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300, block_size=block)
   else:
     ref = H.mcts_batch(gs, acts, offs, bs, es, 6, max_simulations=300,
                        policy=_lib.POLICY_NUMPY)
-    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300,
+    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300, block_size=block,
                          policy=_lib.POLICY_NUMPY)
   for k in E.OUTPUT_KEYS:
     np.testing.assert_array_equal(got[k], ref[k][:, :got[k].shape[1]] if ref[k].ndim == 2

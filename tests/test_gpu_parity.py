@@ -23,8 +23,8 @@ CASES = [
     ("breakthrough(rows=6,columns=5)", 16, 300, 6),
     ("breakthrough(rows=4,columns=3)", 16, 300, 2),  # narrow boards: edge columns,
     ("breakthrough(rows=5,columns=2)", 16, 200, 2),  # short games, solver proofs
-    ("hex(board_size=5)", 32, 400, 6),
-    ("hex", 8, 400, 4),
+    ("hex(board_size=5)", 96, 400, 6),  # > 64 roots: every lane of a wave64 (block 64)
+    ("hex", 72, 200, 4),
     ("go(board_size=7,komi=4.5)", 8, 200, 6),
     ("go(board_size=9)", 8, 160, 8),
 ]

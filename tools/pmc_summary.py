@@ -3,8 +3,9 @@
 
   python tools/pmc_summary.py gpurun_out/pmc <kernel> <game> [out.json]
 
-Averages every counter over the kernel's dispatches, divides by the sims per
-launch (from the bench JSON line each pass printed), and records the HBM bytes
+Averages every counter over the kernel's dispatches, divides by the units per
+launch (from the bench JSON line each pass printed: config.units_per_launch,
+else the sims / playouts per step -- one launch per step), and records the HBM bytes
 per launch as MI355X_MICROARCH.md §HBM prescribes for gfx950:
   traffic = 2 x FETCH_SIZE (reported at half the bytes of 128-B requests)
             + WRITE_SIZE, both KB -> bytes.
@@ -48,7 +49,8 @@ def main():
       for line in open(log):
         if line.startswith("{"):
           cfg = json.loads(line)["config"]
-          sims = cfg.get("sims_per_step_per_gpu", cfg.get("playouts_per_step_per_gpu"))
+          sims = cfg.get("units_per_launch", cfg.get("sims_per_step_per_gpu",
+                                                     cfg.get("playouts_per_step_per_gpu")))
   sys.path.insert(0, ROOT)
   import bench
   rec = {"kernel": kernel, "game": game, "sims_per_launch": sims,
