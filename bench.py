@@ -59,6 +59,9 @@ CONFIGS = {
     # SURVEY §8f rank 2 (not a BASELINE config): PUCT search with an external
     # (network) evaluator, batched across searches; AlphaZero root noise.
     "az": ("az", "connect_four", 16384, 128, 4),
+    # go search (not a BASELINE config): independent go9 roots, random
+    # rollouts + solver, as c2 on connect_four.
+    "g9": ("search", "go(board_size=9)", 65536, 256, 6),
 }
 KERNEL = {"wave": "k_wsearch", "lane": "k_mcts"}
 PAGED_ABOVE = 4 << 30  # --arena auto: page the arena when the reservation exceeds this
@@ -230,6 +233,8 @@ def _resolved_layout(game, R, layout):
   from os_amd import _lib
   if layout != _lib.LAYOUT_AUTO:
     return "wave" if layout == _lib.LAYOUT_WAVE else "lane"
+  if game.startswith("go") and R >= 16384:
+    return "lane"  # k_lsearch (C++ policy)
   return "wave"  # hex included: C++ policy, board_size 11
 
 
@@ -361,7 +366,8 @@ def bench_search(args, ctx, layout):
       "parallelism": "dp%d (independent roots, no collective)" % ctx.world,
       "layout": lay, "block_size": args.block or (64 if lay == "wave" else 16),
       "sims_per_step_per_gpu": sims_per_step})
-  line["roofline"] = _roofline(KERNEL[lay], game, alg_bytes, kernel_ms, sims_per_step, "sim")
+  kern = "k_lsearch" if game.startswith("go") and lay == "lane" else KERNEL[lay]
+  line["roofline"] = _roofline(kern, game, alg_bytes, kernel_ms, sims_per_step, "sim")
   line["cpu_baseline"] = cpu
   line["parity"] = parity
   line["tree_stats"] = stats

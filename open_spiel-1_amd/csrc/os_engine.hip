@@ -160,6 +160,10 @@ DevArgs MakeArgs(os_engine* e) {
   a.root_hashes = static_cast<const uint64_t*>(e->d_rhash.p);
   a.root_nhash = static_cast<const int32_t*>(e->d_rnh.p);
   a.hash_stride = e->hash_stride;
+  a.lstride = e->chunk_roots;
+  a.lpath = e->d_lpath.p;
+  a.lglog = static_cast<uint64_t*>(e->d_glog.p);
+  a.lglink = static_cast<uint32_t*>(e->d_glink.p);
   a.results = static_cast<SearchResult*>(e->d_res.p);
   a.max_children = e->max_children;
   a.child_action = static_cast<int32_t*>(e->d_cact.p);
@@ -221,8 +225,10 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
     return Fail(OS_ERR_UNSUPPORTED, "games with chance nodes run the lane layout only");
   if (p->child_selection != OS_SELECT_UCT && p->child_selection != OS_SELECT_PUCT)
     return Fail(OS_ERR_INVALID, "unknown child_selection");
-  if (search && e->game.cfg.kind == kGo && p->layout == OS_LAYOUT_LANE)
-    return Fail(OS_ERR_UNSUPPORTED, "go runs on the wave layout only (OS_LAYOUT_WAVE / AUTO)");
+  if (search && e->game.cfg.kind == kGo && p->layout == OS_LAYOUT_LANE &&
+      p->policy != OS_POLICY_CPP)
+    return Fail(OS_ERR_UNSUPPORTED,
+                "go's lane layout runs the C++ policy (the wave layout runs numpy bots)");
   return OS_OK;
 }
 
@@ -231,13 +237,28 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
 // hex_rollout_lanes: 6.5e7 vs 1.4e7 sims/s at 4096 roots, profiles/r01).
 // Breakthrough at C3's 65536 roots: wave 8.3e7 vs lane 3.3e7 sims/s
 // (profiles/r02), so a large batch no longer switches to the lane layout.
+// go9 at 256 sims (profiles/r03/g9_*): wave 5.0e6 / 6.3e6 sims/s at 4096 /
+// 16384 roots, lane (k_lsearch) 2.2e6 / 8.6e6 -- the lane layout needs enough
+// searches to fill the chip, so go takes it from 16384 roots.
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
-  (void)R;
   if (layout != OS_LAYOUT_AUTO) return layout;
   if (cfg.kind == kPig) return OS_LAYOUT_LANE;  // chance nodes: os_chance.h
+  if (cfg.kind == kGo)
+    return policy == OS_POLICY_CPP && R >= 16384 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
   if (cfg.kind == kHex)
     return policy == OS_POLICY_CPP && cfg.rows >= 3 ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
   return OS_LAYOUT_WAVE;
+}
+
+// Per-search HBM buffers of the global-memory lane layout (k_lsearch, go):
+// visit path, position log + links (the expansion buffer is in LDS).
+bool LaneGlobal(const os_engine* e) {
+  return e->game.cfg.kind == kGo && e->params.layout == OS_LAYOUT_LANE;
+}
+size_t LaneGlobalBytes(const os_engine* e) {
+  if (!LaneGlobal(e)) return 0;
+  const size_t pe = e->node_bytes == 16 ? sizeof(PathEnt<int32_t>) : sizeof(PathEnt<double>);
+  return (e->game.cfg.max_game_length + 2) * pe + static_cast<size_t>(kGoLogCap) * 12;
 }
 
 // Nodes per page of the paged arena: room for 64 expansions of the widest
@@ -272,7 +293,7 @@ int SizeArena(os_engine* e, bool allow_paged) {
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   // The arena this engine already holds is released before a larger one.
   const size_t budget = static_cast<size_t>((free_b + e->d_arena.bytes) * 0.6);
-  const size_t mt_bytes = 2 * kMtN * 4;
+  const size_t mt_bytes = 2 * kMtN * 4 + LaneGlobalBytes(e);
   e->paged = false;
   e->page_nodes = 0;
   e->pool_pages = 0;
@@ -430,6 +451,13 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   // Work buffers.
   const size_t C = static_cast<size_t>(e->chunk_roots);
   if ((rc = e->d_mt.ensure(C * 2 * kMtN * 4))) return rc;
+  if (LaneGlobal(e)) {
+    const size_t pe = e->node_bytes == 16 ? sizeof(PathEnt<int32_t>) : sizeof(PathEnt<double>);
+    if ((rc = e->d_lpath.ensure(C * (cfg.max_game_length + 2) * pe)) ||
+        (rc = e->d_glog.ensure(C * kGoLogCap * 8)) ||
+        (rc = e->d_glink.ensure(C * kGoLogCap * 4)))
+      return rc;
+  }
   if ((rc = AllocArena(e))) return rc;
   const size_t MC = Rz * e->max_children;
   if ((rc = e->d_res.ensure(Rz * sizeof(SearchResult))) || (rc = e->d_cact.ensure(MC * 4)) ||

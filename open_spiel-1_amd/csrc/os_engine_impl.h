@@ -64,6 +64,12 @@ struct DevArgs {
   const uint64_t* root_hashes;  // [total][hash_stride]
   const int32_t* root_nhash;    // [total]
   int32_t hash_stride;
+  // Global-memory lane layout (k_lsearch, go): per-search buffers, contiguous
+  // per search (the MT streams use `mt` as [chunk][2][624]).
+  int64_t lstride;        // searches per launch chunk
+  void* lpath;            // [chunk][path_cap] PathEnt<R>
+  uint64_t* lglog;        // [chunk][kGoLogCap] position logs
+  uint32_t* lglink;       // [chunk][kGoLogCap] stone count + same-count links
   // outputs, indexed by global root
   SearchResult* results;
   int32_t max_children;
@@ -265,6 +271,7 @@ struct os_engine {
   int32_t az_requests = 0;  // os_az_set_requests (OS_AZ_REQUESTS_SEPARATE)
   bool az_fused = false;    // mode of the prepared batch
   osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw;
+  osx::DevBuf d_lpath;  // k_lsearch visit paths (go lane layout)
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -296,7 +303,7 @@ struct os_engine {
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
-                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw};
+                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

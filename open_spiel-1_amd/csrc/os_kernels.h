@@ -153,6 +153,93 @@ __global__ __launch_bounds__(64) void k_mcts(DevArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Lane-per-search kernel with the per-search buffers in HBM (go's
+// OS_LAYOUT_LANE): one lane per search, 64 searches per wave, so leaf
+// rollouts run 64 at a time instead of one per wave (profiles/r03/g9).  The
+// bot and evaluator MT19937 streams (MtStreamPf: std::mt19937 words, only the
+// twisted words stored, the next word's inputs read ahead), the visit path and
+// go's position log are contiguous per search; the expansion buffer, the
+// log's bucket heads and the Zobrist table sit in LDS (buffers lane-
+// interleaved).  C++ policy, fresh bots.
+template <class G>
+struct LCtx {
+  __device__ static NoCtx make(const DevArgs&, int64_t, int64_t, uint8_t*) { return NoCtx(); }
+};
+template <>
+struct LCtx<Go> {
+  __device__ static GoCtx make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t* lds_heads) {
+    GoCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = a.lglog + lr * kGoLogCap;
+    c.link = a.lglink + lr * kGoLogCap;
+    c.head = lds_heads + (threadIdx.x & 63);
+    c.head_stride = 64;
+    c.stride = 1;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.n_heads = a.cfg.rows * a.cfg.cols + 1;
+    c.init_filters();
+    return c;
+  }
+};
+
+constexpr int kLsActCap = 124;  // LDS expansion buffer entries per lane (>= go 11x11's 122)
+constexpr int kLsZob = 2 * 121;  // Zobrist words of go up to 11x11
+
+template <class G, class R>
+__global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
+  // LDS: go's bucket heads and the expansion buffers, lane-interleaved
+  // ([i][64]), and the Zobrist table (read by every move of every lane).
+  __shared__ uint8_t heads[G::State::kNeedsLog ? kGoHeads * 64 : 1];
+  __shared__ uint8_t acts[kLsActCap * 64];  // go actions are < 256
+  __shared__ uint64_t zob[G::State::kNeedsLog ? kLsZob : 1];
+  if constexpr (G::State::kNeedsLog) {
+    const int nz = 2 * a.cfg.rows * a.cfg.cols;
+    for (int i = threadIdx.x; i < nz; i += blockDim.x) zob[i] = a.zob[i];
+    __syncthreads();
+  }
+  const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (lr >= a.num_roots) return;
+  const int64_t gr = a.root_base + lr;
+  // Per-search contiguous buffers: the lanes of a wave drift apart (each at
+  // its own draw count, log length and depth), so a batch-SoA layout would
+  // touch a new cache line per word; contiguous, a search reuses its lines.
+  MtStreamPf bot{a.mt + lr * 2 * kMtN, 1, 0, 0};
+  MtStreamPf ev{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0};
+  bot.seed(a.bot_seeds[gr]);
+  ev.seed(a.eval_seeds[gr]);
+  StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
+  StridedPtr<uint8_t> act{acts + (threadIdx.x & 63), 64};
+  typename G::Ctx ctx = LCtx<G>::make(a, gr, lr, heads);
+  if constexpr (G::State::kNeedsLog) ctx.zob = zob;
+  const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  SearchResult res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot,
+                                                   ev, path, act, a.path_cap);
+  res.rng_words = bot.words + ev.words;
+  a.results[gr] = res;
+  const Node<R>& rn = nodes[0];
+  const int P0 = G::to_move(root);
+  const int nc = rn.nchild;
+  a.nchild[gr] = nc;
+  a.root_n[gr] = rn.n;
+  a.root_w[gr] = static_cast<double>(rn.w);
+  a.root_out[gr] = out_sign<G>(rn.out, P0, a.cfg);
+  const int64_t ob = gr * a.max_children;
+  for (int k = 0; k < nc && k < a.max_children; ++k) {
+    const Node<R>& c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = static_cast<double>(c.w);
+    a.child_out[ob + k] = out_sign<G>(c.out, P0, a.cfg);
+  }
+  const int b = best_child_g<G>(nodes, P0, a.cfg);
+  a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+}
+
+// ---------------------------------------------------------------------------
 // Wave-per-search kernel (default layout): one 64-lane workgroup per search.
 template <class G>
 struct WaveCtxMaker {
@@ -247,6 +334,9 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr, glog);
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   PhaseCycles ph = {};  // paged: the root's page is page lr = blockIdx.x
+#if OS_PHASE_TIMING
+  if constexpr (std::is_same<G, Go>::value) ctx.sub = ph.c;
+#endif
   SearchResult res = shared
       ? wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE>(
             a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path, a.path_cap, ph, lcache)
@@ -646,11 +736,17 @@ struct RollCtx<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
+#if OS_ROLL_AOS & 2
+    c.log = a.glog + i * kGoLogCap;
+    c.link = a.glink + i * kGoLogCap;
+    c.stride = 1;
+#else
     c.log = a.glog + i;
     c.link = a.glink + i;
+    c.stride = static_cast<int32_t>(a.n);
+#endif
     c.head = lds_heads + (threadIdx.x & 63);
     c.head_stride = 64;
-    c.stride = static_cast<int32_t>(a.n);
     c.n_log = 0;
     c.cap = kGoLogCap;
     c.n_heads = a.cfg.rows * a.cfg.cols + 1;
@@ -709,11 +805,32 @@ __global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
 // One lane per RandomRolloutEvaluator.  The lanes of a wave start together
 // and draw two words per move in lockstep, so the MT19937 states and go's
 // position logs are batch-SoA in HBM: one contiguous line per word / entry.
+// A/B switch for the C5 traffic study: bit 0 keeps each playout's MT state
+// contiguous ([n][624]), bit 1 its position log ([n][kGoLogCap]).
+#ifndef OS_ROLL_AOS
+#define OS_ROLL_AOS 0
+#endif
 template <class G>
 __global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
-  MtStreamSoA ev{a.mt + i, a.n, 0, 0};
+  // OS_ROLL_MT (A/B): 0 MtStreamSoA, 1 MtStreamReg (first block from seed
+  // cursors alone: no MT traffic below 624 words, more VALU), 2 MtStreamPf.
+#ifndef OS_ROLL_MT
+#define OS_ROLL_MT 0
+#endif
+#if OS_ROLL_MT == 1
+  using RollMt = MtStreamReg;
+#elif OS_ROLL_MT == 2
+  using RollMt = MtStreamPf;
+#else
+  using RollMt = MtStreamSoA;
+#endif
+#if OS_ROLL_AOS & 1
+  RollMt ev{a.mt + i * kMtN, 1, 0, 0};
+#else
+  RollMt ev{a.mt + i, a.n, 0, 0};
+#endif
   ev.seed(a.seeds[i]);
   __shared__ uint8_t heads[G::State::kNeedsLog ? kGoHeads * 64 : 1];
   typename G::Ctx ctx = RollCtx<G>::make(a, i, heads);
@@ -806,13 +923,25 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
     if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
   }
   if constexpr (G::State::kNeedsLog) {
-    // Go searches run one wave per search only.  A lane-per-search go search
-    // keeps its superko log in private memory (4.6 KB of scratch per lane,
-    // ~2700 spilled registers) and hung on MI355X with f64 rewards
-    // (n_rollouts > 1) while the host build of the same code is clean under
-    // ASan/UBSan: it is not built.
-    (void)stream;
-    return Fail(OS_ERR_UNSUPPORTED, "go runs on the wave layout only (OS_LAYOUT_WAVE / AUTO)");
+    // go: k_lsearch, per-search buffers in HBM (the LDS-slice kernel k_mcts
+    // would hold the superko log in private memory).
+    if (Policy != kPolicyCpp || a.import_state)
+      return Fail(OS_ERR_UNSUPPORTED,
+                  "go's lane layout runs fresh C++-policy bots (the wave layout runs the rest)");
+    if (a.child_cap > kLsActCap || 2 * a.cfg.rows * a.cfg.cols > kLsZob)
+      return Fail(OS_ERR_UNSUPPORTED, "go board too large for k_lsearch");
+    for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+      const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+      a.root_base = base;
+      a.num_roots = n;
+      const unsigned grid = static_cast<unsigned>((n + 63) / 64);
+      hipLaunchKernelGGL((k_lsearch<G, R>), dim3(grid), dim3(64), 0, stream, a);
+      hipError_t err = hipGetLastError();
+      if (err != hipSuccess)
+        return Fail(OS_ERR_DEVICE, std::string("k_lsearch launch failed: ") +
+                                       hipGetErrorString(err));
+    }
+    return OS_OK;
   } else {
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
   if (bs > 64) bs = 64;  // k_mcts's __launch_bounds__

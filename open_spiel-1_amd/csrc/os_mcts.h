@@ -215,15 +215,26 @@ struct PathEnt {
   R w;             // total_reward before this simulation's backup
 };
 
+// Element i of a batch-SoA array at p[i * stride]: the per-search buffers of
+// the global-memory lane layout (k_lsearch), where the lanes of a wave hold
+// the same index of their own searches in one contiguous line.
+template <class T>
+struct StridedPtr {
+  T* p;
+  int64_t stride;
+  OS_HD T& operator[](int i) const { return p[static_cast<int64_t>(i) * stride]; }
+};
+
 // One complete search from `root`.  `bot` and `ev` are the two MT19937
 // streams (the same object under kPolicyNumpy).  `actbuf` holds >=
-// max_children entries, `path` >= path_cap >= MaxGameLength + 1 entries.
-template <class G, class R, int Policy, class Rng>
+// max_children entries, `path` >= path_cap >= MaxGameLength + 1 entries
+// (pointers, or StridedPtr views of batch-SoA buffers).
+template <class G, class R, int Policy, class Rng, class PathA, class ActA>
 OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
                                const typename G::State& root,
                                typename G::Ctx& ctx, Node<R>* nodes,
-                               uint32_t cap, Rng& bot, Rng& ev, PathEnt<R>* path,
-                               uint16_t* actbuf, int path_cap) {
+                               uint32_t cap, Rng& bot, Rng& ev, PathA path,
+                               ActA actbuf, int path_cap) {
   SearchResult res;
   res.status = kOk;
   res.sims = 0;
@@ -310,8 +321,7 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         chosen = 0;
         res.scanned += cur_nc;
         Node<R> bc = nodes[cur_first];
-        for (int k = 0; k < cur_nc; ++k) {
-          const Node<R> c = nodes[cur_first + k];
+        auto consider = [&](const Node<R>& c, int k) {
           double v;
           if (c.out != kUnsolved) {
             v = outcome_for(c.out, cp);
@@ -328,7 +338,19 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
             chosen = k;
             bc = c;
           }
+        };
+        // Four children loaded before any is scored: one memory latency per
+        // four nodes on the lane layouts, the same first-maximum order.
+        int k = 0;
+        for (; k + 4 <= cur_nc; k += 4) {
+          const Node<R> c0 = nodes[cur_first + k], c1 = nodes[cur_first + k + 1];
+          const Node<R> c2 = nodes[cur_first + k + 2], c3 = nodes[cur_first + k + 3];
+          consider(c0, k);
+          consider(c1, k + 1);
+          consider(c2, k + 2);
+          consider(c3, k + 3);
         }
+        for (; k < cur_nc; ++k) consider(nodes[cur_first + k], k);
         c_action = bc.action;
         c_first = bc.first;
         c_n = bc.n;

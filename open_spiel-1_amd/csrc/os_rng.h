@@ -135,6 +135,182 @@ struct MtStreamSoA {
   }
 };
 
+// MtStreamSoA whose first block never touches memory: std::mt19937's word
+// t_i of block 0 is y(x_i, x_{i+1}) ^ x_{i+397} for i < 227 and
+// y(x_i, x_{i+1}) ^ t_{i-227} for i >= 227, where x are the init_genrand
+// words -- so every t_i is a function of x alone: for 227 <= i < 454,
+// t_{i-227} = y(x_{i-227}, x_{i-226}) ^ x_{i+170}; for i >= 454 one level
+// more, t_{i-227} = y(x_{i-227}, x_{i-226}) ^ y(x_{i-454}, x_{i-453}) ^ x_{i-57}.
+// Running cursors over x give every word of the block without storing or
+// reading one.  Word 623 reads the new t_0.  Only a stream that leaves block 0
+// (> 624 words: a go9 random playout draws ~230) writes block 0 out, from the
+// seed, and continues in memory as MtStreamSoA does.
+struct MtStreamReg {
+  uint32_t* s;
+  int64_t stride;
+  int idx;
+  uint32_t words;
+  int blk0;
+  uint32_t seed0;
+  uint32_t lo0, lo1, hi;   // x_i, x_{i+1}, x_{i+397} (i < 227)
+  uint32_t lag0, lag1, mid;  // x_{i-227}, x_{i-226}, x_{i+170} (i >= 227)
+  uint32_t lg0, lg1, far;    // x_{i-454}, x_{i-453}, x_{i-57} (i >= 454)
+  uint32_t x397;            // x_397 (mid's and far's start)
+
+  OS_HD uint32_t& at(int i) const { return s[static_cast<int64_t>(i) * stride]; }
+  OS_HD static uint32_t mix(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+  OS_HD void seed(uint32_t v) {
+    seed0 = v;
+    lo0 = v;
+    lo1 = MtStreamSoA::seed_step(v, 1);
+    uint32_t x = lo1;
+    for (int k = 2; k <= kMtM; ++k) x = MtStreamSoA::seed_step(x, k);
+    hi = x;
+    x397 = x;
+    lag0 = lag1 = mid = 0;
+    lg0 = lg1 = far = 0;
+    idx = 0;
+    blk0 = 1;
+    words = 0;
+  }
+  // Leaves block 0: writes its 624 words (recomputed from the seed) for the
+  // in-memory twist of block 1.
+  OS_HD void spill_block0() {
+    uint32_t a = seed0, b = MtStreamSoA::seed_step(seed0, 1), h = x397;
+    for (int i = 0; i < kMtN; ++i) {
+      const uint32_t bb = (i + 1 == kMtN) ? at(0) : b;
+      const uint32_t m = (i + kMtM < kMtN) ? h : at(i + kMtM - kMtN);
+      at(i) = m ^ mix(a, bb);
+      a = b;
+      b = MtStreamSoA::seed_step(b, i + 2);
+      h = MtStreamSoA::seed_step(h, i + kMtM + 1);
+    }
+    blk0 = 0;
+  }
+  OS_HD uint32_t next() {
+    ++words;
+    if (blk0) {
+      const int i = idx;
+      if (i < kMtN) {
+        uint32_t v;
+        if (i < kMtN - kMtM) {  // i < 227
+          v = hi ^ mix(lo0, lo1);
+          hi = MtStreamSoA::seed_step(hi, i + kMtM + 1);
+          if (i + 1 == kMtN - kMtM) {  // the second form starts at 227
+            lag0 = seed0;
+            lag1 = MtStreamSoA::seed_step(seed0, 1);
+            mid = x397;
+          }
+        } else {
+          constexpr int kL = kMtN - kMtM;  // 227
+          uint32_t t;                      // t_{i-227}
+          if (i < 2 * kL) {
+            t = mid ^ mix(lag0, lag1);
+            mid = MtStreamSoA::seed_step(mid, i + kMtM - kL + 1);  // x_{i+171}
+            if (i + 1 == 2 * kL) {
+              lg0 = seed0;
+              lg1 = MtStreamSoA::seed_step(seed0, 1);
+              far = x397;
+            }
+          } else {
+            t = far ^ mix(lg0, lg1) ^ mix(lag0, lag1);
+            lg0 = lg1;
+            lg1 = MtStreamSoA::seed_step(lg1, i - 2 * kL + 2);        // x_{i-452}
+            far = MtStreamSoA::seed_step(far, i + kMtM - 2 * kL + 1);  // x_{i-56}
+          }
+          const uint32_t b = (i + 1 == kMtN)
+                                 ? x397 ^ mix(seed0, MtStreamSoA::seed_step(seed0, 1))  // new t_0
+                                 : lo1;
+          v = t ^ mix(lo0, b);
+          lag0 = lag1;
+          lag1 = MtStreamSoA::seed_step(lag1, i - kL + 2);  // x_{i-225}
+        }
+        lo0 = lo1;
+        lo1 = MtStreamSoA::seed_step(lo1, i + 2);
+        idx = i + 1;
+        return MtStream::temper(v);
+      }
+      spill_block0();
+      idx = kMtN;
+    }
+    if (idx >= kMtN) idx = 0;
+    const int i = idx;
+    const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+    const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+    const uint32_t y = (at(i) & 0x80000000u) | (at(i1) & 0x7fffffffu);
+    const uint32_t v = at(im) ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    at(i) = v;
+    idx = i + 1;
+    return MtStream::temper(v);
+  }
+};
+
+// MtStreamSoA with the next word's twist inputs read ahead: after word i is
+// produced, s[i+2] and s[(i+1+397) % 624] are loaded (s[i+1] is already held),
+// so the loads of a draw are in flight while the caller works between draws
+// instead of stalling it.  The in-place twist order is unchanged: word i reads
+// s[(i+397) % 624] after it was rewritten this pass (i >= 227) and, for
+// i = 623, s[0] after word 0 of this pass -- each read is issued after the
+// store it must see, from the same lane.  Same words as std::mt19937.
+struct MtStreamPf {
+  uint32_t* s;
+  int64_t stride;
+  int idx;
+  uint32_t words;
+  int blk0;  // 1 while the first block is being drawn (MtStreamSoA cursors)
+  uint32_t lo0, lo1, hi;
+  uint32_t a_i, a_i1, a_im;  // s[idx], s[idx + 1], s[idx + 397] (mod 624), read ahead
+
+  OS_HD uint32_t& at(int i) const { return s[static_cast<int64_t>(i) * stride]; }
+  OS_HD void seed(uint32_t v) {
+    lo0 = v;
+    lo1 = MtStreamSoA::seed_step(v, 1);
+    uint32_t x = lo1;
+    for (int k = 2; k <= kMtM; ++k) x = MtStreamSoA::seed_step(x, k);
+    hi = x;
+    idx = 0;
+    blk0 = 1;
+    words = 0;
+    a_i = a_i1 = a_im = 0;
+  }
+  OS_HD uint32_t next() {
+    ++words;
+    const int i = idx;
+    uint32_t v;
+    if (blk0) {
+      const uint32_t b = (i + 1 == kMtN) ? at(0) : lo1;
+      const uint32_t m = (i + kMtM < kMtN) ? hi : at(i + kMtM - kMtN);
+      const uint32_t y = (lo0 & 0x80000000u) | (b & 0x7fffffffu);
+      v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      at(i) = v;
+      lo0 = lo1;
+      lo1 = MtStreamSoA::seed_step(lo1, i + 2);
+      hi = MtStreamSoA::seed_step(hi, i + kMtM + 1);
+      if (i + 1 == kMtN) {  // block 1 reads the stored block 0
+        blk0 = 0;
+        a_i = at(0);
+        a_i1 = at(1);
+        a_im = at(kMtM);
+      }
+    } else {
+      const uint32_t y = (a_i & 0x80000000u) | (a_i1 & 0x7fffffffu);
+      v = a_im ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      at(i) = v;
+      const int j = (i + 1 == kMtN) ? 0 : i + 1;  // the next word
+      const int j1 = (j + 1 == kMtN) ? 0 : j + 1;
+      const int jm = (j + kMtM >= kMtN) ? j + kMtM - kMtN : j + kMtM;
+      a_i = a_i1;  // s[j]: not rewritten since it was read
+      a_i1 = at(j1);
+      a_im = at(jm);
+    }
+    idx = (i + 1 == kMtN) ? 0 : i + 1;
+    return MtStream::temper(v);
+  }
+};
+
 OS_HD uint64_t umulhi64(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __umul64hi(a, b);
@@ -191,14 +367,15 @@ OS_HD uint32_t Lemire32(G& g, uint32_t m) {
 }
 
 // std::shuffle from libstdc++ 11 (bits/stl_algo.h, "pair" path valid for
-// n <= 65535 with a 32-bit URBG).  T is any swappable element type.
-template <class T, class G>
-OS_HD void CppShuffle(T* a, int n, G& g) {
+// n <= 65535 with a 32-bit URBG).  A is a pointer or an indexable view
+// (StridedPtr) of any swappable element type.
+template <class A, class G>
+OS_HD void CppShuffle(A a, int n, G& g) {
   if (n <= 1) return;
   int i = 1;
   if ((n & 1) == 0) {
     uint32_t j = Lemire32(g, 2u);
-    T t = a[1]; a[1] = a[j]; a[j] = t;
+    auto t = a[1]; a[1] = a[j]; a[j] = t;
     i = 2;
   }
   while (i != n) {
@@ -206,7 +383,7 @@ OS_HD void CppShuffle(T* a, int n, G& g) {
     const uint32_t b1 = b0 + 1u;
     const uint32_t x = Lemire32(g, b0 * b1);
     const uint32_t p0 = x / b1, p1 = x % b1;
-    T t = a[i]; a[i] = a[p0]; a[p0] = t;
+    auto t = a[i]; a[i] = a[p0]; a[p0] = t;
     t = a[i + 1]; a[i + 1] = a[p1]; a[p1] = t;
     i += 2;
   }
@@ -301,11 +478,11 @@ OS_HD uint32_t NpChoice(G& g, uint32_t n) {
 }
 
 // numpy RandomState.shuffle(list): Fisher-Yates from the end.
-template <class T, class G>
-OS_HD void NpShuffle(T* a, int n, G& g) {
+template <class A, class G>
+OS_HD void NpShuffle(A a, int n, G& g) {
   for (int i = n - 1; i >= 1; --i) {
     uint32_t j = NpRandomInterval(g, static_cast<uint32_t>(i));
-    T t = a[i]; a[i] = a[j]; a[j] = t;
+    auto t = a[i]; a[i] = a[j]; a[j] = t;
   }
 }
 

@@ -79,7 +79,10 @@
 namespace osm {
 
 enum PhaseId { kPhSelect = 0, kPhExpand, kPhRollout, kPhBackup, kPhSolver, kPhTail,
-               kPhTwist, kPhTotal, kNumPhases };
+               kPhTwist, kPhTotal,
+               // go rollout breakdown (inside kPhRollout): legal + draw, apply
+               // (with the superko insert), the insert alone, the final score
+               kPhGoLegal, kPhGoApply, kPhGoInsert, kPhGoScore, kNumPhases };
 struct PhaseCycles {
   uint64_t c[kNumPhases];
 };
@@ -359,6 +362,9 @@ struct WaveMt {
 // LDS, compared 64 entries at a time.  Candidates as in GoCtx (os_games.h):
 // only entries logged before the most recent capture can repeat a position.
 struct GoWaveCtx {
+#if OS_PHASE_TIMING
+  uint64_t* sub;  // PhaseCycles::c of the search (go breakdown)
+#endif
   const uint64_t* zob;
   const uint64_t* base;   // hashes before the root (global)
   int32_t n_base;
@@ -396,18 +402,26 @@ struct GoWaveCtx {
   }
   __device__ bool insert(uint64_t h, bool captured, int stones) {
     (void)stones;
+#if OS_PHASE_TIMING
+    const uint64_t t0 = OS_PH_NOW();
+#endif
     if (captured) {
       cand_end = n_log;
       cand_filt = filt;
     }
-    if (candidate(h)) return false;
-    if (n_log < cap) {
-      if (lane_id() == 0) log[n_log] = h;
-      __builtin_amdgcn_wave_barrier();
-      ++n_log;
+    const bool dup = candidate(h);
+    if (!dup) {
+      if (n_log < cap) {
+        if (lane_id() == 0) log[n_log] = h;
+        __builtin_amdgcn_wave_barrier();
+        ++n_log;
+      }
+      filt.add(GoCtx::fbit(h));
     }
-    filt.add(GoCtx::fbit(h));
-    return true;
+#if OS_PHASE_TIMING
+    OS_PH_ADD(sub[kPhGoInsert], t0);
+#endif
+    return !dup;
   }
 };
 
@@ -1207,6 +1221,9 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
     s = make_uniform(s);  // keep the playout on the scalar unit
 #endif
     if (G::terminal(s, g)) break;
+#if OS_PHASE_TIMING
+    const uint64_t t0 = OS_PH_NOW();
+#endif
     const typename G::Legal l = G::legal(s, g, ctx);
     uint32_t k;
     if (Policy == kPolicyCpp && SmallAbsl<G>::value)
@@ -1215,9 +1232,24 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
       k = ev.uniform_lanes(static_cast<uint32_t>(l.count));
     else
       k = NpChoice(ev, static_cast<uint32_t>(l.count));
-    G::apply(s, g, ctx, l.kth(static_cast<int>(k)));
+    const int act = l.kth(static_cast<int>(k));
+#if OS_PHASE_TIMING
+    const uint64_t t1 = OS_PH_NOW();
+    if constexpr (std::is_same<G, Go>::value) OS_PH_ADD(ctx.sub[kPhGoLegal], t0);
+#endif
+    G::apply(s, g, ctx, act);
+#if OS_PHASE_TIMING
+    if constexpr (std::is_same<G, Go>::value) OS_PH_ADD(ctx.sub[kPhGoApply], t1);
+#endif
   }
+#if OS_PHASE_TIMING
+  const uint64_t t2 = OS_PH_NOW();
+  const int r0 = G::ret0(s, g, ctx);
+  if constexpr (std::is_same<G, Go>::value) OS_PH_ADD(ctx.sub[kPhGoScore], t2);
+  return r0;
+#else
   return G::ret0(s, g, ctx);
+#endif
 }
 
 // A child node as ONE 16-byte load (Node<int32_t> is 16-byte aligned in the

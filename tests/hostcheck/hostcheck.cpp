@@ -319,6 +319,20 @@ void hc_mt_words_soa(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
   g.seed(seed);
   for (int64_t i = 0; i < n; ++i) out[i] = g.next();
 }
+// k_lsearch's read-ahead SoA stream (MtStreamPf), same interleaving.
+void hc_mt_words_pf(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
+  std::vector<uint32_t> s(kMtN * stride, 0xdeadbeefu);
+  MtStreamPf g{s.data() + stride - 1, stride, 0, 0};
+  g.seed(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = g.next();
+}
+// k_rollouts' register-only first block (MtStreamReg), same interleaving.
+void hc_mt_words_reg(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
+  std::vector<uint32_t> s(kMtN * stride, 0xdeadbeefu);
+  MtStreamReg g{s.data() + stride - 1, stride, 0, 0};
+  g.seed(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = g.next();
+}
 void hc_absl_uniform(uint32_t seed, uint32_t n, int64_t k, uint64_t* out) {
   std::vector<uint32_t> s(kMtN);
   mt_seed(s.data(), seed);

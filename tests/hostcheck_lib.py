@@ -29,6 +29,8 @@ def lib():
     L.hc_go_score.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64]
     L.hc_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
     L.hc_mt_words_soa.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
+    L.hc_mt_words_pf.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
+    L.hc_mt_words_reg.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
     L.hc_absl_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp]
     L.hc_cpp_shuffle.argtypes = [ctypes.c_uint32, ctypes.c_int32, vp]
     L.hc_np_ops.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp, vp,
@@ -96,6 +98,18 @@ def mt_words(seed, n):
 def mt_words_soa(seed, stride, n):
   out = np.zeros(n, np.uint32)
   lib().hc_mt_words_soa(seed, stride, n, out.ctypes.data)
+  return out
+
+
+def mt_words_reg(seed, stride, n):
+  out = np.zeros(n, np.uint32)
+  lib().hc_mt_words_reg(seed, stride, n, out.ctypes.data)
+  return out
+
+
+def mt_words_pf(seed, stride, n):
+  out = np.zeros(n, np.uint32)
+  lib().hc_mt_words_pf(seed, stride, n, out.ctypes.data)
   return out
 
 

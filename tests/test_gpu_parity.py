@@ -55,10 +55,6 @@ def test_search_bit_exact(E, gs, R, sims, plies, layout, block):
   bs = np.arange(R, dtype=np.uint32)
   es = bs + np.uint32(1 << 20)
   lay = _lib.LAYOUT_WAVE if layout == "wave" else _lib.LAYOUT_LANE
-  if gs.startswith("go") and layout == "lane":  # go runs one wave per search only
-    with pytest.raises(ValueError):
-      eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims, layout=lay)
-    return
   got = eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
                        block_size=block, layout=lay)
   ref = O.Game(gs).mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
@@ -80,6 +76,32 @@ def test_search_variants(E, gs, n_rollouts, solve, uct_c):
   ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children,
                               threads=8, **kw)
   _cmp(E, got, ref)
+
+
+# go's lane layout (k_lsearch: one lane per search, every per-search buffer
+# batch-SoA in HBM): > 64 searches so every lane of a wave64 runs one, all
+# board sizes the device takes, f64 rewards, solver off, a GC budget.
+@pytest.mark.parametrize("gs,R,sims,plies,kw", [
+    ("go(board_size=5,komi=0.5)", 96, 300, 4, {}),
+    ("go(board_size=7,komi=4.5)", 80, 200, 6, dict(n_rollouts=2, solve=False, uct_c=0.9)),
+    ("go(board_size=9)", 72, 160, 8, {}),
+    ("go(board_size=9)", 40, 120, 20, dict(n_rollouts=3)),
+    ("go(board_size=11,komi=6.5)", 66, 80, 6, {}),
+    ("go(board_size=5,komi=0.5)", 70, 2000, 2, dict(max_memory_mb=1)),
+])
+def test_go_lane_layout_bit_exact(E, gs, R, sims, plies, kw):
+  from os_amd import _lib
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, R, 4242, plies)
+  bs = np.arange(R, dtype=np.uint32) * 7 + 2
+  es = bs + np.uint32(1 << 20)
+  kw = dict(dict(uct_c=2.0, max_simulations=sims), **kw)
+  got = eng.mcts_batch(acts, offs, bs, es, layout=_lib.LAYOUT_LANE, **kw)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, threads=8,
+                              **kw)
+  _cmp(E, got, ref)
+  if kw.get("max_memory_mb") == 1:
+    assert eng.stats()["gc_runs"] > 0
 
 
 def test_garbage_collection_on_device(E):
@@ -310,8 +332,6 @@ def test_puct_bit_exact(E, gs, R, sims, plies, layout, nr, solve, uct_c):
   es = bs + np.uint32(1 << 20)
   kw = dict(uct_c=uct_c, max_simulations=sims, n_rollouts=nr, solve=solve)
   lay = _lib.LAYOUT_WAVE if layout == "wave" else _lib.LAYOUT_LANE
-  if gs.startswith("go") and layout == "lane":
-    pytest.skip("go runs one wave per search only")
   got = eng.mcts_batch(acts, offs, bs, es, layout=lay, child_selection=_lib.SELECT_PUCT, **kw)
   ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, threads=8,
                               puct=True, **kw)

@@ -21,6 +21,23 @@ def test_soa_stream_matches_std_mt19937(seed, stride):
   assert np.array_equal(H.mt_words_soa(seed, stride, 2000), O.mt19937(seed, 2000))
 
 
+@pytest.mark.parametrize("seed", [0, 1, 42, 5489, 2**32 - 1])
+@pytest.mark.parametrize("stride", [1, 3, 64])
+def test_register_block0_stream_matches_std_mt19937(seed, stride):
+  # k_rollouts' stream: block 0 from seed cursors alone (no memory), block 1+
+  # in memory after block 0 is written out from the seed.
+  for n in (1, 227, 228, 623, 624, 625, 2600):
+    assert np.array_equal(H.mt_words_reg(seed, stride, n), O.mt19937(seed, n)), n
+
+
+@pytest.mark.parametrize("seed", [0, 1, 42, 5489, 2**32 - 1])
+@pytest.mark.parametrize("stride", [1, 3, 64])
+def test_read_ahead_stream_matches_std_mt19937(seed, stride):
+  # k_lsearch's stream: loads of the next word's twist inputs issued after
+  # each draw; four blocks cover every wrap (word 623 reads the new s[0]).
+  assert np.array_equal(H.mt_words_pf(seed, stride, 2600), O.mt19937(seed, 2600))
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 48, 82, 121, 768])
 def test_absl_uniform_matches_oracle(n):
   for seed in (3, 99):

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "open_spiel-1_amd"))
 from os_amd import _lib  # noqa: E402
 from os_amd import engine as E  # noqa: E402
 
-PHASES = ("select", "expand", "rollout", "backup", "solver", "tail", "twist", "total")
+PHASES = ("select", "expand", "rollout", "backup", "solver", "tail", "twist", "total",
+          "go_legal", "go_apply", "go_insert", "go_score")
 GAMES = (("connect_four", 8), ("tic_tac_toe", 4), ("breakthrough", 6), ("hex", 6),
          ("go(board_size=9)", 6))
 
@@ -25,7 +26,10 @@ def main():
   roots = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
   sims = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
   buf = np.zeros(len(PHASES), np.uint64)
+  only = sys.argv[3] if len(sys.argv) > 3 else ""
   for gs, plies in GAMES:
+    if only not in gs:
+      continue
     eng = E.Engine(gs)
     acts, offs = E.make_roots(gs, roots, seed_base=1000, max_plies=plies)
     seeds = np.arange(roots, dtype=np.uint32)
