@@ -164,6 +164,7 @@ DevArgs MakeArgs(os_engine* e) {
   a.lpath = e->d_lpath.p;
   a.lglog = static_cast<uint64_t*>(e->d_glog.p);
   a.lglink = static_cast<uint32_t*>(e->d_glink.p);
+  a.lheads = static_cast<uint16_t*>(e->d_lheads.p);
   a.results = static_cast<SearchResult*>(e->d_res.p);
   a.max_children = e->max_children;
   a.child_action = static_cast<int32_t*>(e->d_cact.p);
@@ -215,6 +216,16 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
   if (p->layout != OS_LAYOUT_WAVE && p->layout != OS_LAYOUT_LANE &&
       p->layout != OS_LAYOUT_AUTO)
     return Fail(OS_ERR_INVALID, "unknown layout");
+  if (GoBigBoard(e->game.cfg)) {
+    // k_lsearch only: dynamic path / log capacities, 8-bit child counts.
+    if (!search)
+      return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
+    if (p->layout == OS_LAYOUT_WAVE || p->policy != OS_POLICY_CPP)
+      return Fail(OS_ERR_UNSUPPORTED,
+                  "go above 11 x 11 runs C++-policy searches on the lane layout");
+    return p->child_selection == OS_SELECT_UCT || p->child_selection == OS_SELECT_PUCT
+               ? OS_OK : Fail(OS_ERR_INVALID, "unknown child_selection");
+  }
   if (e->game.cfg.max_children > kMaxChildren)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxChildren");
   // Games with chance nodes bound the tree depth instead (kChancePathCap;
@@ -242,7 +253,7 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
 // searches to fill the chip, so go takes it from 16384 roots.
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
   if (layout != OS_LAYOUT_AUTO) return layout;
-  if (cfg.kind == kPig) return OS_LAYOUT_LANE;  // chance nodes: os_chance.h
+  if (cfg.kind == kPig || GoBigBoard(cfg)) return OS_LAYOUT_LANE;  // os_chance.h / k_lsearch
   if (cfg.kind == kGo)
     return policy == OS_POLICY_CPP && R >= 16384 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
   if (cfg.kind == kHex)
@@ -255,10 +266,13 @@ int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t pol
 bool LaneGlobal(const os_engine* e) {
   return e->game.cfg.kind == kGo && e->params.layout == OS_LAYOUT_LANE;
 }
+int LaneLogCap(const GameCfg& c) { return GoBigBoard(c) ? kGoLogCapBig : kGoLogCap; }
 size_t LaneGlobalBytes(const os_engine* e) {
   if (!LaneGlobal(e)) return 0;
   const size_t pe = e->node_bytes == 16 ? sizeof(PathEnt<int32_t>) : sizeof(PathEnt<double>);
-  return (e->game.cfg.max_game_length + 2) * pe + static_cast<size_t>(kGoLogCap) * 12;
+  return (e->game.cfg.max_game_length + 2) * pe +
+         static_cast<size_t>(LaneLogCap(e->game.cfg)) * 12 +
+         (GoBigBoard(e->game.cfg) ? kGoHeadsBig * 2 : 0);
 }
 
 // Nodes per page of the paged arena: room for 64 expansions of the widest
@@ -288,7 +302,8 @@ int SizeArena(os_engine* e, bool allow_paged) {
   // DFS stack then lives in the arena tail, so reserve room for it.
   const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
   const bool gc_possible = max_nodes > 1 && worst >= max_nodes;
-  if (gc_possible) worst += GcStackReserve(cfg.max_children);
+  if (gc_possible)
+    worst += GcStackReserve(cfg.max_children, std::max(kMaxPath, cfg.max_game_length + 2));
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   // The arena this engine already holds is released before a larger one.
@@ -453,9 +468,10 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   if ((rc = e->d_mt.ensure(C * 2 * kMtN * 4))) return rc;
   if (LaneGlobal(e)) {
     const size_t pe = e->node_bytes == 16 ? sizeof(PathEnt<int32_t>) : sizeof(PathEnt<double>);
+    const size_t lc = LaneLogCap(cfg);
     if ((rc = e->d_lpath.ensure(C * (cfg.max_game_length + 2) * pe)) ||
-        (rc = e->d_glog.ensure(C * kGoLogCap * 8)) ||
-        (rc = e->d_glink.ensure(C * kGoLogCap * 4)))
+        (rc = e->d_glog.ensure(C * lc * 8)) || (rc = e->d_glink.ensure(C * lc * 4)) ||
+        (GoBigBoard(cfg) && (rc = e->d_lheads.ensure(C * kGoHeadsBig * 2))))
       return rc;
   }
   if ((rc = AllocArena(e))) return rc;
@@ -479,7 +495,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
 int Run(os_engine* e, hipStream_t stream) {
   HIP_TRY(hipSetDevice(e->device));
   if (e->num_roots == 0) return OS_OK;
-  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  const GameLaunchers* L = LaunchersFor(e->game.cfg);
   if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
   if (e->paged) HIP_TRY(hipMemsetAsync(e->d_page_next.p, 0, 4, stream));
   return L->search(e, MakeArgs(e), stream);
@@ -589,6 +605,8 @@ int ArenaCap(const os_engine* e, const os_mcts_params* p, uint32_t* cap_out) {
 int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* start_actions,
               const int64_t* start_offsets, const uint32_t* bot_seeds,
               const uint32_t* eval_seeds, int32_t max_len, int32_t record) {
+  if (GoBigBoard(e->game.cfg))
+    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
   const bool with_visits = (record & OS_RECORD_VISITS) != 0;
   const bool with_obs = (record & OS_RECORD_OBSERVATIONS) != 0;
   const bool with_policy = (record & OS_RECORD_POLICY) != 0;
@@ -702,8 +720,9 @@ int SpRun(os_engine* e, hipStream_t stream) {
   if (!e->sp_ready) return Fail(OS_ERR_INVALID, "os_selfplay_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
   if (e->sp_games == 0) return OS_OK;
-  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
-  if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  const GameLaunchers* L = LaunchersFor(e->game.cfg);
+  if (!L || !L->selfplay)
+    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
   return L->selfplay(e, stream);
 }
 
@@ -783,7 +802,7 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   if (rc) return rc;
   if (e->chunk_roots < R)
     return Fail(OS_ERR_CAPACITY, "external-evaluator searches must all fit in HBM at once");
-  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  const GameLaunchers* L = LaunchersFor(e->game.cfg);
   if (!L || !L->az) return Fail(OS_ERR_UNSUPPORTED, "game");
   const size_t slot_bytes = L->az_slot_bytes;
   const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
@@ -851,7 +870,7 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
 int AzStep(os_engine* e, hipStream_t stream) {
   if (!e->az_ready) return Fail(OS_ERR_INVALID, "os_az_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
-  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
+  const GameLaunchers* L = LaunchersFor(e->game.cfg);
   if (!L || !L->az) return Fail(OS_ERR_UNSUPPORTED, "game");
   return L->az(e, stream);
 }
@@ -859,6 +878,8 @@ int AzStep(os_engine* e, hipStream_t stream) {
 // Uploads one root + n evaluator seeds for the rollout kernels.
 int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
                 const uint32_t* seeds) {
+  if (GoBigBoard(e->game.cfg))
+    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
   int rc;
   const size_t sb = e->game.state_bytes;
   if ((rc = e->d_roots.ensure(sb))) return rc;
@@ -896,8 +917,9 @@ int RollRun(os_engine* e, hipStream_t stream) {
   if (!e->roll_ready) return Fail(OS_ERR_INVALID, "os_rollouts_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
   if (e->roll_n == 0) return OS_OK;
-  const GameLaunchers* L = LaunchersFor(e->game.cfg.kind);
-  if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
+  const GameLaunchers* L = LaunchersFor(e->game.cfg);
+  if (!L || !L->rollouts)
+    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
   return L->rollouts(e, stream);
 }
 
@@ -1059,10 +1081,14 @@ int os_engine_create(const char* game_string, int32_t device, os_engine** out) {
   std::string err = LoadHostGame(game_string, &e->game, &unsupported);
   if (!err.empty()) return Fail(unsupported ? OS_ERR_UNSUPPORTED : OS_ERR_INVALID, err);
   const GameCfg& cfg = e->game.cfg;
-  if ((cfg.kind == kHex || cfg.kind == kGo) && cfg.rows > kB128Side)
+  if (cfg.kind == kHex && cfg.rows > kB128Side)
     return Fail(OS_ERR_UNSUPPORTED,
-                "the device engine runs hex / go up to 11 x 11 (B128 bitboards); larger "
+                "the device engine runs hex up to 11 x 11 (B128 bitboards); larger "
                 "boards are supported by the State API only");
+  if (cfg.kind == kGo && cfg.rows > kGoDeviceMaxSide)
+    return Fail(OS_ERR_UNSUPPORTED,
+                "the device engine runs go up to 15 x 15 (lane-layout searches above "
+                "11 x 11); larger boards are supported by the State API only");
   int ndev = 0;
   hipError_t he = hipGetDeviceCount(&ndev);
   if (he != hipSuccess || ndev == 0)

@@ -39,6 +39,11 @@ inline int Fail(int code, const std::string& msg) {
 
 constexpr int kGoLogCap = 248;              // >= 2 * 11 * 11 + 4
 constexpr int kGoHeads = 122;               // stone counts 0 .. 11 * 11
+// go 12 x 12 .. 15 x 15 on the device (k_lsearch over B384 bitboards; node
+// nchild and the LDS action buffer are 8-bit, so <= 226 children).
+constexpr int kGoDeviceMaxSide = 15;
+constexpr int kGoLogCapBig = 2 * 15 * 15 + 4;
+constexpr int kGoHeadsBig = 15 * 15 + 1;
 constexpr size_t kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
 constexpr int kDefaultBlock = 16;           // searches (lanes) per workgroup (lane layout)
 
@@ -68,8 +73,9 @@ struct DevArgs {
   // per search (the MT streams use `mt` as [chunk][2][624]).
   int64_t lstride;        // searches per launch chunk
   void* lpath;            // [chunk][path_cap] PathEnt<R>
-  uint64_t* lglog;        // [chunk][kGoLogCap] position logs
-  uint32_t* lglink;       // [chunk][kGoLogCap] stone count + same-count links
+  uint64_t* lglog;        // [chunk][log cap] position logs
+  uint32_t* lglink;       // [chunk][log cap] stone count + same-count links
+  uint16_t* lheads;       // [chunk][kGoHeadsBig] bucket heads (boards > 11 x 11)
   // outputs, indexed by global root
   SearchResult* results;
   int32_t max_children;
@@ -271,7 +277,7 @@ struct os_engine {
   int32_t az_requests = 0;  // os_az_set_requests (OS_AZ_REQUESTS_SEPARATE)
   bool az_fused = false;    // mode of the prepared batch
   osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw;
-  osx::DevBuf d_lpath;  // k_lsearch visit paths (go lane layout)
+  osx::DevBuf d_lpath, d_lheads;  // k_lsearch visit paths, big-board heads
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -303,7 +309,7 @@ struct os_engine {
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
-                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath};
+                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath, &d_lheads};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }
@@ -328,7 +334,11 @@ extern GameLaunchers kConnectFourLaunchers;
 extern GameLaunchers kBreakthroughLaunchers;
 extern GameLaunchers kHexLaunchers;
 extern GameLaunchers kGoLaunchers;
+extern GameLaunchers kGoBigLaunchers;
 extern GameLaunchers kPigLaunchers;
+
+// go above 11 x 11 runs lane-layout searches only (os_game_go_big.hip).
+inline bool GoBigBoard(const GameCfg& c) { return c.kind == kGo && c.rows > 11; }
 
 inline const GameLaunchers* LaunchersFor(int32_t kind) {
   switch (kind) {
@@ -340,6 +350,9 @@ inline const GameLaunchers* LaunchersFor(int32_t kind) {
     case kPig: return &kPigLaunchers;
   }
   return nullptr;
+}
+inline const GameLaunchers* LaunchersFor(const GameCfg& c) {
+  return GoBigBoard(c) ? &kGoBigLaunchers : LaunchersFor(c.kind);
 }
 
 }  // namespace osx

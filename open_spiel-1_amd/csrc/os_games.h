@@ -490,13 +490,14 @@ struct Filter256 {
 // scan -- and the buckets give the same answers as testing the whole set.
 // Positions before the root (`base`, counts unknown) are scanned behind a
 // 256-bit pre-filter.  Arrays may be batch-SoA: element i at [i * stride].
-struct GoCtx {
+template <class H>
+struct GoCtxT {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
   const uint64_t* base;    // hashes of positions before this search's root
   int32_t n_base;
   uint64_t* log;           // hashes added since the root (capacity cap)
   uint32_t* link;          // [cap] stone count << 16 | previous same-count entry + 1
-  uint8_t* head;           // [n_heads] last entry + 1 with k stones (cap <= 255)
+  H* head;                 // [n_heads] last entry + 1 with k stones (cap <= max of H)
   int32_t stride;          // SoA stride of log / link (1: contiguous)
   int32_t head_stride;     // stride of head (k_rollouts: LDS, 64 lanes)
   int32_t n_log;
@@ -548,7 +549,7 @@ struct GoCtx {
     while (n_log > m) {
       --n_log;
       const uint32_t lk = link[static_cast<int64_t>(n_log) * stride];
-      head[static_cast<int>(lk >> 16) * head_stride] = static_cast<uint8_t>(lk & 0xFFFFu);
+      head[static_cast<int>(lk >> 16) * head_stride] = static_cast<H>(lk & 0xFFFFu);
     }
   }
   // Logs the position after a non-pass move; false if it was already present
@@ -561,12 +562,16 @@ struct GoCtx {
       const int hk = stones * head_stride;
       log[e] = h;
       link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
-      head[hk] = static_cast<uint8_t>(n_log + 1);
+      head[hk] = static_cast<H>(n_log + 1);
       ++n_log;
     }
     return true;
   }
 };
+// u8 bucket heads (log cap <= 255: boards up to 11 x 11, and the host's
+// one-move logs); u16 heads for the longer logs of larger boards (k_lsearch).
+using GoCtx = GoCtxT<uint8_t>;
+using GoCtxW = GoCtxT<uint16_t>;
 
 template <class B>
 struct GoT {

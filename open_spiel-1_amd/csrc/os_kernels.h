@@ -160,10 +160,46 @@ __global__ __launch_bounds__(64) void k_mcts(DevArgs a) {
 // twisted words stored, the next word's inputs read ahead), the visit path and
 // go's position log are contiguous per search; the expansion buffer, the
 // log's bucket heads and the Zobrist table sit in LDS (buffers lane-
-// interleaved).  C++ policy, fresh bots.
+// interleaved).  C++ policy; fresh bots, or bots continuing numpy-form
+// (key, pos) streams (os_mcts_stateful).
+// LDS / HBM capacities of k_lsearch per game: expansion-buffer entries per
+// lane (u8 actions), Zobrist words, LDS bucket heads (u8, lane-interleaved;
+// boards above 11 x 11 keep u16 heads per search in HBM), position-log cap.
+template <class G>
+struct LsCaps {
+  static constexpr int act = 1, zob = 1, heads = 1, log = 1;
+};
+template <>
+struct LsCaps<Go> {
+  static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads * 64, log = kGoLogCap;
+};
+template <>
+struct LsCaps<GoBig> {
+  static constexpr int act = 226, zob = 2 * 225, heads = 1, log = kGoLogCapBig;
+};
+
 template <class G>
 struct LCtx {
   __device__ static NoCtx make(const DevArgs&, int64_t, int64_t, uint8_t*) { return NoCtx(); }
+};
+template <>
+struct LCtx<GoBig> {
+  __device__ static GoCtxW make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t*) {
+    GoCtxW c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = a.lglog + lr * kGoLogCapBig;
+    c.link = a.lglink + lr * kGoLogCapBig;
+    c.head = a.lheads + lr * kGoHeadsBig;
+    c.head_stride = 1;
+    c.stride = 1;
+    c.n_log = 0;
+    c.cap = kGoLogCapBig;
+    c.n_heads = a.cfg.rows * a.cfg.cols + 1;
+    c.init_filters();
+    return c;
+  }
 };
 template <>
 struct LCtx<Go> {
@@ -185,16 +221,13 @@ struct LCtx<Go> {
   }
 };
 
-constexpr int kLsActCap = 124;  // LDS expansion buffer entries per lane (>= go 11x11's 122)
-constexpr int kLsZob = 2 * 121;  // Zobrist words of go up to 11x11
-
 template <class G, class R>
 __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   // LDS: go's bucket heads and the expansion buffers, lane-interleaved
   // ([i][64]), and the Zobrist table (read by every move of every lane).
-  __shared__ uint8_t heads[G::State::kNeedsLog ? kGoHeads * 64 : 1];
-  __shared__ uint8_t acts[kLsActCap * 64];  // go actions are < 256
-  __shared__ uint64_t zob[G::State::kNeedsLog ? kLsZob : 1];
+  __shared__ uint8_t heads[LsCaps<G>::heads];
+  __shared__ uint8_t acts[LsCaps<G>::act * 64];  // go actions up to 15 x 15 are < 256
+  __shared__ uint64_t zob[LsCaps<G>::zob];
   if constexpr (G::State::kNeedsLog) {
     const int nz = 2 * a.cfg.rows * a.cfg.cols;
     for (int i = threadIdx.x; i < nz; i += blockDim.x) zob[i] = a.zob[i];
@@ -208,11 +241,16 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   // touch a new cache line per word; contiguous, a search reuses its lines.
   MtStreamPf bot{a.mt + lr * 2 * kMtN, 1, 0, 0};
   MtStreamPf ev{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0};
-  bot.seed(a.bot_seeds[gr]);
-  ev.seed(a.eval_seeds[gr]);
+  if (a.import_state) {  // the rows hold numpy-form keys (os_mcts_stateful)
+    bot.init_import(a.mt_pos[2 * gr]);
+    ev.init_import(a.mt_pos[2 * gr + 1]);
+  } else {
+    bot.seed(a.bot_seeds[gr]);
+    ev.seed(a.eval_seeds[gr]);
+  }
   StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
   StridedPtr<uint8_t> act{acts + (threadIdx.x & 63), 64};
-  typename G::Ctx ctx = LCtx<G>::make(a, gr, lr, heads);
+  auto ctx = LCtx<G>::make(a, gr, lr, heads);
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
   const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
@@ -237,6 +275,10 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   }
   const int b = best_child_g<G>(nodes, P0, a.cfg);
   a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+  if (a.import_state) {
+    a.mt_pos[2 * gr] = bot.finalize();
+    a.mt_pos[2 * gr + 1] = ev.finalize();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -913,6 +955,35 @@ int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   return OS_OK;
 }
 
+template <class G, class R>
+int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
+  if (a.shared_stream)
+    return Fail(OS_ERR_UNSUPPORTED, "go's lane layout runs C++-policy bots (separate streams)");
+  if (a.child_cap > LsCaps<G>::act || 2 * a.cfg.rows * a.cfg.cols > LsCaps<G>::zob)
+    return Fail(OS_ERR_UNSUPPORTED, "go board too large for k_lsearch");
+  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+    a.root_base = base;
+    a.num_roots = n;
+    const unsigned grid = static_cast<unsigned>((n + 63) / 64);
+    hipLaunchKernelGGL((k_lsearch<G, R>), dim3(grid), dim3(64), 0, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+      return Fail(OS_ERR_DEVICE, std::string("k_lsearch launch failed: ") +
+                                     hipGetErrorString(err));
+  }
+  return OS_OK;
+}
+
+// go above 11 x 11: lane-layout C++-policy searches only (os_game_go_big.hip).
+template <class G>
+int LaunchSearchOnly(os_engine* e, const DevArgs& a, hipStream_t stream) {
+  if (e->params.layout != OS_LAYOUT_LANE || e->params.policy != OS_POLICY_CPP)
+    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs C++-policy searches on the lane layout");
+  return e->node_bytes == 16 ? LaunchLs<G, int32_t>(e, a, stream)
+                             : LaunchLs<G, double>(e, a, stream);
+}
+
 template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   if constexpr (HasChance<G>::value) {
@@ -925,23 +996,8 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   if constexpr (G::State::kNeedsLog) {
     // go: k_lsearch, per-search buffers in HBM (the LDS-slice kernel k_mcts
     // would hold the superko log in private memory).
-    if (Policy != kPolicyCpp || a.import_state)
-      return Fail(OS_ERR_UNSUPPORTED,
-                  "go's lane layout runs fresh C++-policy bots (the wave layout runs the rest)");
-    if (a.child_cap > kLsActCap || 2 * a.cfg.rows * a.cfg.cols > kLsZob)
-      return Fail(OS_ERR_UNSUPPORTED, "go board too large for k_lsearch");
-    for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
-      const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
-      a.root_base = base;
-      a.num_roots = n;
-      const unsigned grid = static_cast<unsigned>((n + 63) / 64);
-      hipLaunchKernelGGL((k_lsearch<G, R>), dim3(grid), dim3(64), 0, stream, a);
-      hipError_t err = hipGetLastError();
-      if (err != hipSuccess)
-        return Fail(OS_ERR_DEVICE, std::string("k_lsearch launch failed: ") +
-                                       hipGetErrorString(err));
-    }
-    return OS_OK;
+    if (Policy != kPolicyCpp) return Fail(OS_ERR_UNSUPPORTED, "k_lsearch runs the C++ policy");
+    return LaunchLs<G, R>(e, a, stream);
   } else {
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
   if (bs > 64) bs = 64;  // k_mcts's __launch_bounds__
@@ -1177,6 +1233,13 @@ int SelfPlayEntry(os_engine* e, hipStream_t stream) {
 // evaluator search unsupported for it.
 // A non-const host variable: the device pass instantiates the launch code
 // (and so every kernel it launches) but does not emit the table itself.
+#define OS_DEFINE_SEARCH_ONLY_LAUNCHERS(G)                                            \
+  namespace osx {                                                                     \
+  extern GameLaunchers k##G##Launchers;                                               \
+  GameLaunchers k##G##Launchers = {&LaunchSearchOnly<G>, nullptr, nullptr, nullptr,  \
+                                   &PhaseCycles, 0};                                  \
+  }
+
 #define OS_DEFINE_LAUNCHERS(G, WITH_AZ)                                          \
   namespace osx {                                                                \
   extern GameLaunchers k##G##Launchers;                                          \

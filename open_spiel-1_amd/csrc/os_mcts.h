@@ -147,9 +147,8 @@ OS_HD int best_child(const Node<R>* nodes, int child_player) {
 }
 
 // One random playout to the end (mcts.cc:46-55 / mcts.py:62-70).
-template <class G, int Policy, class Rng>
-OS_HD int rollout_ret0(typename G::State s, const GameCfg& g, typename G::Ctx& ctx,
-                       Rng& ev) {
+template <class G, int Policy, class Rng, class Ctx>
+OS_HD int rollout_ret0(typename G::State s, const GameCfg& g, Ctx& ctx, Rng& ev) {
   while (!G::terminal(s, g)) {
     const typename G::Legal l = G::legal(s, g, ctx);
     const uint32_t k = Policy == kPolicyCpp
@@ -169,8 +168,8 @@ struct RewardOps<int32_t> {
 
 // Arena nodes to reserve for the GC traversal stack (u32 entries; the stack
 // never holds more than depth x max_children entries).
-OS_HD int64_t GcStackReserve(int max_children) {
-  return (static_cast<int64_t>(kMaxPath) * max_children * 4) / 16 + 64;
+OS_HD int64_t GcStackReserve(int max_children, int depth = kMaxPath) {
+  return (static_cast<int64_t>(depth) * max_children * 4) / 16 + 64;
 }
 
 // GarbageCollect (mcts.cc:430-443): every node with children whose
@@ -229,10 +228,10 @@ struct StridedPtr {
 // streams (the same object under kPolicyNumpy).  `actbuf` holds >=
 // max_children entries, `path` >= path_cap >= MaxGameLength + 1 entries
 // (pointers, or StridedPtr views of batch-SoA buffers).
-template <class G, class R, int Policy, class Rng, class PathA, class ActA>
+template <class G, class R, int Policy, class Rng, class PathA, class ActA, class Ctx>
 OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
                                const typename G::State& root,
-                               typename G::Ctx& ctx, Node<R>* nodes,
+                               Ctx& ctx, Node<R>* nodes,
                                uint32_t cap, Rng& bot, Rng& ev, PathA path,
                                ActA actbuf, int path_cap) {
   SearchResult res;

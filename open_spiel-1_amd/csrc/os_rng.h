@@ -263,6 +263,7 @@ struct MtStreamPf {
   int blk0;  // 1 while the first block is being drawn (MtStreamSoA cursors)
   uint32_t lo0, lo1, hi;
   uint32_t a_i, a_i1, a_im;  // s[idx], s[idx + 1], s[idx + 397] (mod 624), read ahead
+  int pre;   // 1: s holds a fully twisted block (numpy import), words idx.. unread
 
   OS_HD uint32_t& at(int i) const { return s[static_cast<int64_t>(i) * stride]; }
   OS_HD void seed(uint32_t v) {
@@ -275,9 +276,42 @@ struct MtStreamPf {
     blk0 = 1;
     words = 0;
     a_i = a_i1 = a_im = 0;
+    pre = 0;
+  }
+  // numpy legacy (key, p): s holds the twisted block key, p words consumed.
+  OS_HD void init_import(int p) {
+    blk0 = 0;
+    pre = 1;
+    idx = p;
+    words = 0;
+    a_i = a_i1 = a_im = 0;
+  }
+  OS_HD void prefetch0() {  // the twist of a new block starts at word 0
+    a_i = at(0);
+    a_i1 = at(1);
+    a_im = at(kMtM);
+  }
+  // Back to numpy's (key, pos) form: returns pos; the rest of a block being
+  // twisted is twisted in place (MtStream::finalize).
+  OS_HD int finalize() {
+    if (pre) return idx;
+    if (blk0 || idx == 0) return blk0 ? idx : kMtN;  // idx 0: the last block is used up
+    for (int i = idx; i < kMtN; ++i) {
+      const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+      const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+      const uint32_t y = (at(i) & 0x80000000u) | (at(i1) & 0x7fffffffu);
+      at(i) = at(im) ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    return idx;
   }
   OS_HD uint32_t next() {
     ++words;
+    if (pre) {
+      if (idx < kMtN) return MtStream::temper(at(idx++));
+      pre = 0;  // the imported block is used up: twist the next one
+      idx = 0;
+      prefetch0();
+    }
     const int i = idx;
     uint32_t v;
     if (blk0) {
@@ -291,9 +325,7 @@ struct MtStreamPf {
       hi = MtStreamSoA::seed_step(hi, i + kMtM + 1);
       if (i + 1 == kMtN) {  // block 1 reads the stored block 0
         blk0 = 0;
-        a_i = at(0);
-        a_i1 = at(1);
-        a_im = at(kMtM);
+        prefetch0();
       }
     } else {
       const uint32_t y = (a_i & 0x80000000u) | (a_i1 & 0x7fffffffu);

@@ -217,7 +217,7 @@ class MCTSBot(pyspiel.Bot):
     return (type(self.evaluator) is RandomRolloutEvaluator and
             self._child_selection_fn in (SearchNode.uct_value, SearchNode.puct_value) and
             not self._dirichlet_noise and
-            isinstance(self._game, pyspiel.Game) and self._game.on_device())
+            isinstance(self._game, pyspiel.Game) and self._game.on_device(numpy_policy=True))
 
   def restart_at(self, state):
     pass

@@ -179,13 +179,21 @@ class Game:
   def get_type(self):
     return _TYPES[self._info.kind]
 
-  # hex / go sides the device engine runs (B128 bitboards); larger boards
-  # (up to 19 x 19) have the State API only.
+  # hex / go sides the device engine runs: every search up to 11 x 11 (B128
+  # bitboards); go up to 15 x 15 with C++-policy searches (k_lsearch over
+  # B384 bitboards).  Larger boards (up to 19 x 19) have the State API only.
   DEVICE_MAX_SIDE = 11
+  DEVICE_MAX_SIDE_GO_CPP = 15
 
-  def on_device(self):
-    """Whether the GPU engine can search this game (else: host State API)."""
-    return self._info.kind not in (3, 4) or self._info.rows <= Game.DEVICE_MAX_SIDE
+  def on_device(self, numpy_policy=False):
+    """Whether the GPU engine can search this game (else: host State API);
+    numpy_policy: for the Python MCTSBot's RandomState streams."""
+    k, n = self._info.kind, self._info.rows
+    if k == 3 or (k == 4 and numpy_policy):
+      return n <= Game.DEVICE_MAX_SIDE
+    if k == 4:
+      return n <= Game.DEVICE_MAX_SIDE_GO_CPP
+    return True
 
   def get_parameters(self):
     k = self._info.kind

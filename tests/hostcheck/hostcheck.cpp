@@ -326,6 +326,13 @@ void hc_mt_words_pf(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
   g.seed(seed);
   for (int64_t i = 0; i < n; ++i) out[i] = g.next();
 }
+// MtStreamPf continuing a numpy (key, pos) state for k draws, exported back.
+void hc_mt_pf_roundtrip(uint32_t* key, int32_t* pos, int64_t k, uint32_t* out) {
+  MtStreamPf g{key, 1, 0, 0};
+  g.init_import(*pos);
+  for (int64_t i = 0; i < k; ++i) out[i] = g.next();
+  *pos = g.finalize();
+}
 // k_rollouts' register-only first block (MtStreamReg), same interleaving.
 void hc_mt_words_reg(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
   std::vector<uint32_t> s(kMtN * stride, 0xdeadbeefu);

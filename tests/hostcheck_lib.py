@@ -31,6 +31,7 @@ def lib():
     L.hc_mt_words_soa.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
     L.hc_mt_words_pf.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
     L.hc_mt_words_reg.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
+    L.hc_mt_pf_roundtrip.argtypes = [vp, vp, ctypes.c_int64, vp]
     L.hc_absl_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp]
     L.hc_cpp_shuffle.argtypes = [ctypes.c_uint32, ctypes.c_int32, vp]
     L.hc_np_ops.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp, vp,
@@ -151,6 +152,14 @@ def mt_roundtrip(key, pos, k):
   p = np.array([pos], dtype=np.int32)
   out = np.zeros(k, np.uint32)
   lib().hc_mt_roundtrip(key.ctypes.data, p.ctypes.data, k, out.ctypes.data)
+  return out, key, int(p[0])
+
+
+def mt_pf_roundtrip(key, pos, k):
+  key = np.array(key, dtype=np.uint32).copy()
+  p = np.array([pos], dtype=np.int32)
+  out = np.zeros(k, np.uint32)
+  lib().hc_mt_pf_roundtrip(key.ctypes.data, p.ctypes.data, k, out.ctypes.data)
   return out, key, int(p[0])
 
 

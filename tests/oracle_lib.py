@@ -286,8 +286,10 @@ class Game:
 
   def selfplay(self, start_actions, start_offsets, bot_seeds, eval_seeds, max_len,
                uct_c=2.0, max_simulations=100, n_rollouts=1, max_memory_mb=1000,
-               solve=True, with_visits=True, threads=1):
+               solve=True, with_visits=True, threads=1, truncate=False):
     """Games of two MCTSBots sharing one evaluator (mcts_example.cc PlayGame).
+    truncate: stop every game after max_len moves (the prefix) instead of
+    raising.
 
     bot_seeds: [G][2]; eval_seeds: [G].  Returns dict(actions [G][max_len]
     (-1 padded), length [G], returns [G][2], visits [G][max_len][A] or None).
@@ -305,7 +307,7 @@ class Game:
         np.ascontiguousarray(eval_seeds, dtype=np.uint32), max_len, out["actions"],
         out["length"], out["returns"],
         out["visits"].ctypes.data if with_visits else None, threads)
-    if rc:
+    if rc and not truncate:
       raise RuntimeError("oref_selfplay: game longer than max_len")
     return out
 

@@ -3,9 +3,11 @@
 State API (os_games.h HexT / GoT on B384 bitboards) follows the oracle move by
 move on random games (basic_tests.cc RandomSimTest shape: legal actions,
 current player, terminal, returns at every state; serialization round trips).
-The GPU engine runs hex / go up to 11 x 11: the GPU search refuses larger
-boards with ValueError at search time, and the Python MCTSBot's automatic
-backend searches them with its host loop."""
+The GPU engine runs hex up to 11 x 11 and go up to 15 x 15 (above 11 x 11:
+C++-policy searches on the lane layout, k_lsearch over B384 bitboards, parity
+in test_gpu_big_go_search_matches_oracle); the GPU search refuses larger
+boards with ValueError at search time, and the Python MCTSBot (numpy policy)
+searches go above 11 x 11 with its host loop, warning once."""
 import numpy as np
 import pytest
 
@@ -26,7 +28,10 @@ def test_default_go_is_19x19():
   assert g.num_distinct_actions() == 362 and g.max_game_length() == 722
   assert g.observation_tensor_shape() == [4, 19, 19]
   assert not g.on_device()
+  g13 = pyspiel.load_game("go(board_size=13)")
+  assert g13.on_device() and not g13.on_device(numpy_policy=True)
   h = pyspiel.load_game("hex(board_size=13)")
+  assert not h.on_device()
   assert h.num_distinct_actions() == 169 and h.observation_tensor_shape() == [9, 13, 13]
 
 
@@ -81,10 +86,62 @@ def test_gpu_search_refuses_big_boards_and_auto_backend_uses_host_loop():
   with pytest.warns(RuntimeWarning, match="host CPU"):
     root = bot.mcts_search(g.new_initial_state())
   assert root.explore_count == 12 and len(root.children) == 170
-  cbot = pyspiel.MCTSBot(g, pyspiel.RandomRolloutEvaluator(1, 1), 2.0, 10, 100, True, 1,
+  g19 = pyspiel.load_game("go")  # above the device's 15 x 15: a loud error
+  cbot = pyspiel.MCTSBot(g19, pyspiel.RandomRolloutEvaluator(1, 1), 2.0, 10, 100, True, 1,
                          False)
   with pytest.raises(ValueError):
-    cbot.step(g.new_initial_state())
+    cbot.step(g19.new_initial_state())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs,R,sims,plies,kw", [
+    ("go(board_size=13)", 70, 60, 10, {}),
+    ("go(board_size=12,komi=0.5)", 66, 80, 4, dict(n_rollouts=2, solve=False)),
+    ("go(board_size=15)", 66, 40, 20, {}),
+    ("go(board_size=13)", 40, 50, 6, dict(child_selection=1)),  # PUCT
+])
+def test_gpu_big_go_search_matches_oracle(require_gpu, gs, R, sims, plies, kw):
+  from os_amd import engine as E
+  eng = E.Engine(gs)
+  acts, offs = E.make_roots(gs, R, 77, plies)
+  bs = np.arange(R, dtype=np.uint32) * 5 + 1
+  es = bs + np.uint32(1 << 20)
+  kw = dict(dict(uct_c=2.0, max_simulations=sims), **kw)
+  got = eng.mcts_batch(acts, offs, bs, es, **kw)
+  okw = dict(kw)
+  if okw.pop("child_selection", 0) == 1:
+    okw["puct"] = True
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=eng.max_children, threads=8,
+                              **okw)
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_bot_plays_go13_as_the_oracle(require_gpu):
+  # pyspiel.MCTSBot (C++ semantics) on go 13 x 13: bot and evaluator streams
+  # continue across moves through the device (k_lsearch import / export).
+  # Two bots sharing one evaluator (mcts_example.cc PlayGame) = the oracle's
+  # self-play games, compared on the first moves with every root's visits.
+  g = pyspiel.load_game("go(board_size=13)")
+  ev = pyspiel.RandomRolloutEvaluator(1, 7)
+  bots = [pyspiel.MCTSBot(g, ev, 2.0, 40, 1000, True, s, False) for s in (3, 4)]
+  st = g.new_initial_state()
+  moves, visits = [], []
+  for _ in range(6):
+    root = bots[st.current_player()].mcts_search(st)
+    v = np.zeros(g.num_distinct_actions(), np.int32)
+    for c in root.children:
+      v[c.action] = c.explore_count
+    a = root.best_child().action
+    moves.append(a)
+    visits.append(v)
+    st.apply_action(a)
+  ref = O.Game("go(board_size=13)").selfplay(np.zeros(0, np.int64), np.array([0, 0]),
+                                              [[3, 4]], [7], 6, uct_c=2.0,
+                                              max_simulations=40, truncate=True)
+  assert moves == list(ref["actions"][0])
+  np.testing.assert_array_equal(np.array(visits), ref["visits"][0])
 
 
 @pytest.mark.parametrize("h,stones", [(2, ["d4", "q16"]), (4, ["d4", "q16", "d16", "q4"]),

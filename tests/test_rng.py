@@ -77,6 +77,21 @@ def test_numpy_state_roundtrip(k):
   assert np.array_equal(key, st2[1])
 
 
+@pytest.mark.parametrize("skip", [0, 37, 600, 624])
+@pytest.mark.parametrize("k", [0, 1, 100, 587, 588, 624, 625, 1500])
+def test_read_ahead_stream_numpy_roundtrip(skip, k):
+  # k_lsearch's imported bot streams (pyspiel.MCTSBot on go above 11 x 11).
+  rs = np.random.RandomState(11)
+  rs.randint(0, 2**32, size=skip, dtype=np.uint64)
+  st = rs.get_state()
+  out, key, pos = H.mt_pf_roundtrip(st[1], st[2], k)
+  ref = rs.randint(0, 2**32, size=k, dtype=np.uint64).astype(np.uint32)
+  assert np.array_equal(out, ref)
+  st2 = rs.get_state()
+  assert pos == st2[2]
+  assert np.array_equal(key, st2[1])
+
+
 def _py_absl_double(words):
   """abseil 20200225 GenerateRealFromBits<double, GeneratePositiveTag, true>
   over FastUniformBits<uint64> (first word high), restated in Python."""
