@@ -7,6 +7,7 @@
 #define OS_COMMON_H_
 
 #include <stdint.h>
+#include <type_traits>
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>

@@ -165,6 +165,7 @@ DevArgs MakeArgs(os_engine* e) {
   a.lglog = static_cast<uint64_t*>(e->d_glog.p);
   a.lglink = static_cast<uint32_t*>(e->d_glink.p);
   a.lheads = static_cast<uint16_t*>(e->d_lheads.p);
+  a.lact = static_cast<uint16_t*>(e->d_lact.p);
   a.results = static_cast<SearchResult*>(e->d_res.p);
   a.max_children = e->max_children;
   a.child_action = static_cast<int32_t*>(e->d_cact.p);
@@ -269,10 +270,10 @@ bool LaneGlobal(const os_engine* e) {
 int LaneLogCap(const GameCfg& c) { return GoBigBoard(c) ? kGoLogCapBig : kGoLogCap; }
 size_t LaneGlobalBytes(const os_engine* e) {
   if (!LaneGlobal(e)) return 0;
-  const size_t pe = e->node_bytes == 16 ? sizeof(PathEnt<int32_t>) : sizeof(PathEnt<double>);
+  const size_t pe = e->node_double ? sizeof(PathEnt<double>) : sizeof(PathEnt<int32_t>);
   return (e->game.cfg.max_game_length + 2) * pe +
          static_cast<size_t>(LaneLogCap(e->game.cfg)) * 12 +
-         (GoBigBoard(e->game.cfg) ? kGoHeadsBig * 2 : 0);
+         (GoBigBoard(e->game.cfg) ? (kGoHeadsBig + e->game.cfg.max_children + 1) * 2 : 0);
 }
 
 // Nodes per page of the paged arena: room for 64 expansions of the widest
@@ -402,9 +403,11 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   e->max_children = cfg.max_children;
   // f64 node rewards when they are not integers: rollout means, or pig's
   // -1 / (n - 1) losses with more than two players (pig.cc:94-111).
-  e->node_bytes = p->n_rollouts == 1 && cfg.pig_players <= 2
-                      ? static_cast<int>(sizeof(Node<int32_t>))
-                      : static_cast<int>(sizeof(Node<double>));
+  e->node_double = !(p->n_rollouts == 1 && cfg.pig_players <= 2);
+  e->node_wide = GoBigBoard(cfg);
+  e->node_bytes = static_cast<int>(
+      e->node_wide ? (e->node_double ? sizeof(Node<double, true>) : sizeof(Node<int32_t, true>))
+                   : (e->node_double ? sizeof(Node<double>) : sizeof(Node<int32_t>)));
   if ((rc = SizeArena(e, true))) return rc;
 
   // Root states (+ go hash sets) on the host.
@@ -467,11 +470,12 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   const size_t C = static_cast<size_t>(e->chunk_roots);
   if ((rc = e->d_mt.ensure(C * 2 * kMtN * 4))) return rc;
   if (LaneGlobal(e)) {
-    const size_t pe = e->node_bytes == 16 ? sizeof(PathEnt<int32_t>) : sizeof(PathEnt<double>);
+    const size_t pe = e->node_double ? sizeof(PathEnt<double>) : sizeof(PathEnt<int32_t>);
     const size_t lc = LaneLogCap(cfg);
     if ((rc = e->d_lpath.ensure(C * (cfg.max_game_length + 2) * pe)) ||
         (rc = e->d_glog.ensure(C * lc * 8)) || (rc = e->d_glink.ensure(C * lc * 4)) ||
-        (GoBigBoard(cfg) && (rc = e->d_lheads.ensure(C * kGoHeadsBig * 2))))
+        (GoBigBoard(cfg) && (rc = e->d_lheads.ensure(C * kGoHeadsBig * 2))) ||
+        (GoBigBoard(cfg) && (rc = e->d_lact.ensure(C * (cfg.max_children + 1) * 2))))
       return rc;
   }
   if ((rc = AllocArena(e))) return rc;
@@ -624,6 +628,8 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
   e->params = *p;
   e->params.layout = OS_LAYOUT_WAVE;
   e->paged = false;  // self-play trees use the reserved arena
+  e->node_double = p->n_rollouts != 1;
+  e->node_wide = false;
   e->node_bytes = p->n_rollouts == 1 ? static_cast<int>(sizeof(Node<int32_t>))
                                       : static_cast<int>(sizeof(Node<double>));
   if ((rc = ArenaCap(e, p, &e->cap))) return rc;
@@ -1216,17 +1222,21 @@ int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
 }
 
 // Copies node i of a raw node array into the export arrays at slot o.
+extern "C++" template <class N>
+static void ExportNodeT(const unsigned char* raw, uint32_t i, uint32_t o, uint32_t first,
+                        uint32_t* out_first, int32_t* n, double* w, int32_t* action,
+                        int32_t* nchild, int8_t* out0) {
+  const N& x = reinterpret_cast<const N*>(raw)[i];
+  n[o] = x.n; w[o] = x.w; action[o] = x.action; nchild[o] = x.nchild; out0[o] = x.out;
+  out_first[o] = first;
+}
 static void ExportNode(const unsigned char* raw, size_t nb, uint32_t i, uint32_t o,
                        uint32_t first, uint32_t* out_first, int32_t* n, double* w,
                        int32_t* action, int32_t* nchild, int8_t* out0) {
-  if (nb == sizeof(Node<int32_t>)) {
-    const Node<int32_t>& x = reinterpret_cast<const Node<int32_t>*>(raw)[i];
-    n[o] = x.n; w[o] = x.w; action[o] = x.action; nchild[o] = x.nchild; out0[o] = x.out;
-  } else {
-    const Node<double>& x = reinterpret_cast<const Node<double>*>(raw)[i];
-    n[o] = x.n; w[o] = x.w; action[o] = x.action; nchild[o] = x.nchild; out0[o] = x.out;
-  }
-  out_first[o] = first;
+  if (nb == sizeof(Node<int32_t>))
+    ExportNodeT<Node<int32_t>>(raw, i, o, first, out_first, n, w, action, nchild, out0);
+  else
+    ExportNodeT<Node<double>>(raw, i, o, first, out_first, n, w, action, nchild, out0);
 }
 
 int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
@@ -1242,6 +1252,25 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
   if (!first) return OS_OK;
   HIP_TRY(hipSetDevice(e->device));
   const size_t nb = e->node_bytes;
+  if (e->node_wide) {  // k_lsearch's wide nodes (go above 11 x 11): reserved arena
+    std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
+    HIP_TRY(hipMemcpy(raw.data(),
+                      static_cast<unsigned char*>(e->d_arena.p) +
+                          static_cast<size_t>(r) * e->cap * nb,
+                      raw.size(), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < used; ++i) {
+      if (e->node_double) {
+        using N = Node<double, true>;
+        ExportNodeT<N>(raw.data(), i, i, reinterpret_cast<const N*>(raw.data())[i].first, first,
+                       n, w, action, nchild, out0);
+      } else {
+        using N = Node<int32_t, true>;
+        ExportNodeT<N>(raw.data(), i, i, reinterpret_cast<const N*>(raw.data())[i].first, first,
+                       n, w, action, nchild, out0);
+      }
+    }
+    return OS_OK;
+  }
   if (!e->paged) {
     std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
     HIP_TRY(hipMemcpy(raw.data(),

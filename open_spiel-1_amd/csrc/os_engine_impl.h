@@ -39,11 +39,11 @@ inline int Fail(int code, const std::string& msg) {
 
 constexpr int kGoLogCap = 248;              // >= 2 * 11 * 11 + 4
 constexpr int kGoHeads = 122;               // stone counts 0 .. 11 * 11
-// go 12 x 12 .. 15 x 15 on the device (k_lsearch over B384 bitboards; node
-// nchild and the LDS action buffer are 8-bit, so <= 226 children).
-constexpr int kGoDeviceMaxSide = 15;
-constexpr int kGoLogCapBig = 2 * 15 * 15 + 4;
-constexpr int kGoHeadsBig = 15 * 15 + 1;
+// go 12 x 12 .. 19 x 19 on the device (k_lsearch over B384 bitboards, wide
+// nodes with 16-bit child counts, u16 actions in an HBM expansion buffer).
+constexpr int kGoDeviceMaxSide = 19;
+constexpr int kGoLogCapBig = 2 * 19 * 19 + 4;
+constexpr int kGoHeadsBig = 19 * 19 + 1;
 constexpr size_t kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
 constexpr int kDefaultBlock = 16;           // searches (lanes) per workgroup (lane layout)
 
@@ -76,6 +76,7 @@ struct DevArgs {
   uint64_t* lglog;        // [chunk][log cap] position logs
   uint32_t* lglink;       // [chunk][log cap] stone count + same-count links
   uint16_t* lheads;       // [chunk][kGoHeadsBig] bucket heads (boards > 11 x 11)
+  uint16_t* lact;         // [chunk][child_cap] expansion buffers (boards > 11 x 11)
   // outputs, indexed by global root
   SearchResult* results;
   int32_t max_children;
@@ -242,6 +243,8 @@ struct os_engine {
   int64_t chunk_roots = 0;
   uint32_t cap = 0;
   int node_bytes = 16;
+  bool node_double = false;  // Node<double>: f64 rewards
+  bool node_wide = false;    // Node<R, true>: 16-bit child counts (go > 11 x 11)
   int32_t max_children = 0;
   int32_t hash_stride = 1;
   bool import_state = false;
@@ -277,7 +280,7 @@ struct os_engine {
   int32_t az_requests = 0;  // os_az_set_requests (OS_AZ_REQUESTS_SEPARATE)
   bool az_fused = false;    // mode of the prepared batch
   osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw;
-  osx::DevBuf d_lpath, d_lheads;  // k_lsearch visit paths, big-board heads
+  osx::DevBuf d_lpath, d_lheads, d_lact;  // k_lsearch paths, big-board heads / actions
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
       d_rollout_out, d_dense_n, d_dense_w, d_sp_act, d_sp_len, d_sp_ret, d_sp_vis,
@@ -309,7 +312,7 @@ struct os_engine {
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
-                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath, &d_lheads};
+                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath, &d_lheads, &d_lact};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
   }

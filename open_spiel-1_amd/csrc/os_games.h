@@ -753,7 +753,13 @@ struct GoT {
       bool rb = false, rw = false;
       int num = 1;
       marked = marked | BB<B>::bit(p0);
-      uint64_t path0 = 0, path1 = 0, path2 = 0, path3 = 0;  // 2 bits per level
+      // 2 bits per DFS level, one word per 32 levels: as many levels as the
+      // board has points (B128: 128, B384: 384), words indexed by unrolled
+      // selects so they stay in registers.
+      constexpr int kNW = static_cast<int>(sizeof(B)) / 4;
+      uint64_t path[kNW];
+#pragma unroll
+      for (int q = 0; q < kNW; ++q) path[q] = 0;
       int depth = 0;  // stack size - 1
       int cur = p0, curd = 0;
       for (;;) {
@@ -762,7 +768,9 @@ struct GoT {
           if (depth == 0) break;
           --depth;
           const int w = depth >> 5, sh = 2 * (depth & 31);
-          const uint64_t pw = w == 0 ? path0 : (w == 1 ? path1 : (w == 2 ? path2 : path3));
+          uint64_t pw = 0;
+#pragma unroll
+          for (int q = 0; q < kNW; ++q) pw = w == q ? path[q] : pw;
           const int dir = static_cast<int>((pw >> sh) & 3);
           cur -= dir == 0 ? n : (dir == 1 ? 1 : (dir == 2 ? -1 : -n));
           curd = dir + 1;
@@ -783,10 +791,8 @@ struct GoT {
         // Slot `depth` <- d (it may hold a popped sibling's direction).
         const int w = depth >> 5, sh = 2 * (depth & 31);
         const uint64_t keep = ~(3ull << sh), m = static_cast<uint64_t>(d) << sh;
-        path0 = w == 0 ? ((path0 & keep) | m) : path0;
-        path1 = w == 1 ? ((path1 & keep) | m) : path1;
-        path2 = w == 2 ? ((path2 & keep) | m) : path2;
-        path3 = w == 3 ? ((path3 & keep) | m) : path3;
+#pragma unroll
+        for (int q = 0; q < kNW; ++q) path[q] = w == q ? ((path[q] & keep) | m) : path[q];
         ++depth;
         cur = q;
         curd = 0;

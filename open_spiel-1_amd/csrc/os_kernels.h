@@ -174,9 +174,13 @@ struct LsCaps<Go> {
   static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads * 64, log = kGoLogCap;
 };
 template <>
-struct LsCaps<GoBig> {
-  static constexpr int act = 226, zob = 2 * 225, heads = 1, log = kGoLogCapBig;
+struct LsCaps<GoBig> {  // actions up to 361: u16 expansion buffers in HBM
+  static constexpr int act = 1, zob = 2 * 361, heads = 1, log = kGoLogCapBig;
 };
+template <class G>
+struct LsWide : std::false_type {};  // Node<R, true>: 16-bit child counts
+template <>
+struct LsWide<GoBig> : std::true_type {};
 
 template <class G>
 struct LCtx {
@@ -249,16 +253,24 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
     ev.seed(a.eval_seeds[gr]);
   }
   StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
-  StridedPtr<uint8_t> act{acts + (threadIdx.x & 63), 64};
   auto ctx = LCtx<G>::make(a, gr, lr, heads);
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
   const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
-  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
-  SearchResult res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot,
-                                                   ev, path, act, a.path_cap);
+  using N = Node<R, LsWide<G>::value>;
+  N* nodes = static_cast<N*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  SearchResult res;
+  if constexpr (LsWide<G>::value) {
+    StridedPtr<uint16_t> act{a.lact + lr * a.child_cap, 1};
+    res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                                        act, a.path_cap);
+  } else {
+    StridedPtr<uint8_t> act{acts + (threadIdx.x & 63), 64};
+    res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                                        act, a.path_cap);
+  }
   res.rng_words = bot.words + ev.words;
   a.results[gr] = res;
-  const Node<R>& rn = nodes[0];
+  const N& rn = nodes[0];
   const int P0 = G::to_move(root);
   const int nc = rn.nchild;
   a.nchild[gr] = nc;
@@ -267,7 +279,7 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   a.root_out[gr] = out_sign<G>(rn.out, P0, a.cfg);
   const int64_t ob = gr * a.max_children;
   for (int k = 0; k < nc && k < a.max_children; ++k) {
-    const Node<R>& c = nodes[rn.first + k];
+    const N& c = nodes[rn.first + k];
     a.child_action[ob + k] = c.action;
     a.child_n[ob + k] = c.n;
     a.child_w[ob + k] = static_cast<double>(c.w);
@@ -959,7 +971,8 @@ template <class G, class R>
 int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
   if (a.shared_stream)
     return Fail(OS_ERR_UNSUPPORTED, "go's lane layout runs C++-policy bots (separate streams)");
-  if (a.child_cap > LsCaps<G>::act || 2 * a.cfg.rows * a.cfg.cols > LsCaps<G>::zob)
+  if ((!LsWide<G>::value && a.child_cap > LsCaps<G>::act) ||
+      2 * a.cfg.rows * a.cfg.cols > LsCaps<G>::zob)
     return Fail(OS_ERR_UNSUPPORTED, "go board too large for k_lsearch");
   for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
@@ -980,8 +993,7 @@ template <class G>
 int LaunchSearchOnly(os_engine* e, const DevArgs& a, hipStream_t stream) {
   if (e->params.layout != OS_LAYOUT_LANE || e->params.policy != OS_POLICY_CPP)
     return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs C++-policy searches on the lane layout");
-  return e->node_bytes == 16 ? LaunchLs<G, int32_t>(e, a, stream)
-                             : LaunchLs<G, double>(e, a, stream);
+  return e->node_double ? LaunchLs<G, double>(e, a, stream) : LaunchLs<G, int32_t>(e, a, stream);
 }
 
 template <class G, class R, int Policy>
@@ -1025,7 +1037,7 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
 
 template <class G>
 int LaunchForGame(os_engine* e, const DevArgs& a, hipStream_t stream) {
-  const bool dbl = e->node_bytes != static_cast<int>(sizeof(Node<int32_t>));
+  const bool dbl = e->node_double;
   if (e->params.policy == OS_POLICY_NUMPY) {
     return dbl ? LaunchSearch<G, double, kPolicyNumpy>(e, a, stream)
                : LaunchSearch<G, int32_t, kPolicyNumpy>(e, a, stream);

@@ -37,13 +37,15 @@ enum SearchStatus : int32_t {
   kGameOverflow = 4,    // self-play game longer than the trajectory buffer
 };
 
-template <class R>
+// W (wide): a 16-bit child count, for go above 15 x 15 (up to 362 children;
+// k_lsearch only).  Every other kernel keeps the 16-byte int32 node.
+template <class R, bool W = false>
 struct Node {
   uint32_t first;   // first child index (valid iff nchild > 0)
   int32_t n;        // explore_count
   R w;              // total_reward (int32 when n_rollouts == 1: exact)
   uint16_t action;
-  uint8_t nchild;
+  typename std::conditional<W, uint16_t, uint8_t>::type nchild;
   int8_t out;       // player-0 outcome, or kUnsolved
 };
 
@@ -93,8 +95,8 @@ OS_HD double outcome_for(int8_t out0, int player) {
 }
 
 // mcts.cc:113-123 CompareFinal(a, b) == "a < b".
-template <class R>
-OS_HD bool final_less(const Node<R>& a, int pa, const Node<R>& b, int pb) {
+template <class R, bool W>
+OS_HD bool final_less(const Node<R, W>& a, int pa, const Node<R, W>& b, int pb) {
   const double oa = a.out == kUnsolved ? 0.0 : outcome_for(a.out, pa);
   const double ob = b.out == kUnsolved ? 0.0 : outcome_for(b.out, pb);
   if (oa != ob) return oa < ob;
@@ -104,17 +106,17 @@ OS_HD bool final_less(const Node<R>& a, int pa, const Node<R>& b, int pb) {
 
 // CompareFinal / BestChild with the game's outcome decoding (OutValue: pig
 // with more than two players).
-template <class G, class R>
-OS_HD bool final_less_g(const Node<R>& a, const Node<R>& b, int p, const GameCfg& g) {
+template <class G, class R, bool W>
+OS_HD bool final_less_g(const Node<R, W>& a, const Node<R, W>& b, int p, const GameCfg& g) {
   const double oa = a.out == kUnsolved ? 0.0 : OutValue<G>::value(a.out, p, g);
   const double ob = b.out == kUnsolved ? 0.0 : OutValue<G>::value(b.out, p, g);
   if (oa != ob) return oa < ob;
   if (a.n != b.n) return a.n < b.n;
   return static_cast<double>(a.w) < static_cast<double>(b.w);
 }
-template <class G, class R>
-OS_HD int best_child_g(const Node<R>* nodes, int child_player, const GameCfg& g) {
-  const Node<R>& root = nodes[0];
+template <class G, class R, bool W>
+OS_HD int best_child_g(const Node<R, W>* nodes, int child_player, const GameCfg& g) {
+  const Node<R, W>& root = nodes[0];
   if (root.nchild == 0) return -1;
   int best = 0;
   for (int k = 1; k < root.nchild; ++k)
@@ -177,18 +179,18 @@ OS_HD int64_t GcStackReserve(int max_children, int depth = kMaxPath) {
 // such block, including blocks under an already-cleared ancestor (the
 // reference recurses before clearing).  Traversal order does not change the
 // result.  The DFS stack lives in the unused arena tail.
-template <class R>
-OS_HD int garbage_collect(Node<R>* nodes, uint32_t used, uint32_t cap, int limit,
+template <class R, bool W>
+OS_HD int garbage_collect(Node<R, W>* nodes, uint32_t used, uint32_t cap, int limit,
                           int* nodes_count) {
   uint32_t* stack = reinterpret_cast<uint32_t*>(nodes + used);
   const uint64_t stack_cap =
-      (static_cast<uint64_t>(cap - used) * sizeof(Node<R>)) / sizeof(uint32_t);
+      (static_cast<uint64_t>(cap - used) * sizeof(Node<R, W>)) / sizeof(uint32_t);
   uint64_t sp = 0;
   if (stack_cap < 1) return kGcStackOverflow;
   stack[sp++] = 0;
   while (sp > 0) {
     const uint32_t x = stack[--sp];
-    Node<R>& nx = nodes[x];
+    Node<R, W>& nx = nodes[x];
     const int nc = nx.nchild;
     if (nc == 0) continue;
     if (sp + nc > stack_cap) return kGcStackOverflow;
@@ -228,10 +230,10 @@ struct StridedPtr {
 // streams (the same object under kPolicyNumpy).  `actbuf` holds >=
 // max_children entries, `path` >= path_cap >= MaxGameLength + 1 entries
 // (pointers, or StridedPtr views of batch-SoA buffers).
-template <class G, class R, int Policy, class Rng, class PathA, class ActA, class Ctx>
+template <class G, class R, int Policy, class Rng, class PathA, class ActA, class Ctx, bool W>
 OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
                                const typename G::State& root,
-                               Ctx& ctx, Node<R>* nodes,
+                               Ctx& ctx, Node<R, W>* nodes,
                                uint32_t cap, Rng& bot, Rng& ev, PathA path,
                                ActA actbuf, int path_cap) {
   SearchResult res;
@@ -288,7 +290,7 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         const uint32_t first = used;
         used += nc;
         for (int k = 0; k < nc; ++k) {
-          Node<R>& c = nodes[first + k];
+          Node<R, W>& c = nodes[first + k];
           c.first = 0;
           c.n = 0;
           c.w = 0;
@@ -297,7 +299,7 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
           c.out = kUnsolved;
         }
         nodes[cur_idx].first = first;
-        nodes[cur_idx].nchild = static_cast<uint8_t>(nc);
+        nodes[cur_idx].nchild = static_cast<decltype(nodes[0].nchild)>(nc);
         path[depth].first = first;
         path[depth].nc = nc;
         nodes_count += nc;
@@ -319,8 +321,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         double best = -inf;
         chosen = 0;
         res.scanned += cur_nc;
-        Node<R> bc = nodes[cur_first];
-        auto consider = [&](const Node<R>& c, int k) {
+        Node<R, W> bc = nodes[cur_first];
+        auto consider = [&](const Node<R, W>& c, int k) {
           double v;
           if (c.out != kUnsolved) {
             v = outcome_for(c.out, cp);
@@ -342,8 +344,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         // four nodes on the lane layouts, the same first-maximum order.
         int k = 0;
         for (; k + 4 <= cur_nc; k += 4) {
-          const Node<R> c0 = nodes[cur_first + k], c1 = nodes[cur_first + k + 1];
-          const Node<R> c2 = nodes[cur_first + k + 2], c3 = nodes[cur_first + k + 3];
+          const Node<R, W> c0 = nodes[cur_first + k], c1 = nodes[cur_first + k + 1];
+          const Node<R, W> c2 = nodes[cur_first + k + 2], c3 = nodes[cur_first + k + 3];
           consider(c0, k);
           consider(c1, k + 1);
           consider(c2, k + 2);
@@ -411,7 +413,7 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         const int pl = d == 0 ? P0 : (P0 ^ ((d - 1) & 1));
         pe.w += pl == 0 ? rv0 : rv1;
         pe.n += 1;
-        Node<R>& nd = nodes[pe.idx];
+        Node<R, W>& nd = nodes[pe.idx];
         nd.n = pe.n;
         nd.w = pe.w;
         res.backed += 1;

@@ -180,10 +180,10 @@ class Game:
     return _TYPES[self._info.kind]
 
   # hex / go sides the device engine runs: every search up to 11 x 11 (B128
-  # bitboards); go up to 15 x 15 with C++-policy searches (k_lsearch over
+  # bitboards); go up to 19 x 19 with C++-policy searches (k_lsearch over
   # B384 bitboards).  Larger boards (up to 19 x 19) have the State API only.
   DEVICE_MAX_SIDE = 11
-  DEVICE_MAX_SIDE_GO_CPP = 15
+  DEVICE_MAX_SIDE_GO_CPP = 19
 
   def on_device(self, numpy_policy=False):
     """Whether the GPU engine can search this game (else: host State API);

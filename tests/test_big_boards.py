@@ -3,7 +3,7 @@
 State API (os_games.h HexT / GoT on B384 bitboards) follows the oracle move by
 move on random games (basic_tests.cc RandomSimTest shape: legal actions,
 current player, terminal, returns at every state; serialization round trips).
-The GPU engine runs hex up to 11 x 11 and go up to 15 x 15 (above 11 x 11:
+The GPU engine runs hex up to 11 x 11 and go up to 19 x 19 (above 11 x 11:
 C++-policy searches on the lane layout, k_lsearch over B384 bitboards, parity
 in test_gpu_big_go_search_matches_oracle); the GPU search refuses larger
 boards with ValueError at search time, and the Python MCTSBot (numpy policy)
@@ -27,7 +27,7 @@ def test_default_go_is_19x19():
   assert g.get_parameters()["board_size"] == 19
   assert g.num_distinct_actions() == 362 and g.max_game_length() == 722
   assert g.observation_tensor_shape() == [4, 19, 19]
-  assert not g.on_device()
+  assert g.on_device() and not g.on_device(numpy_policy=True)
   g13 = pyspiel.load_game("go(board_size=13)")
   assert g13.on_device() and not g13.on_device(numpy_policy=True)
   h = pyspiel.load_game("hex(board_size=13)")
@@ -86,11 +86,11 @@ def test_gpu_search_refuses_big_boards_and_auto_backend_uses_host_loop():
   with pytest.warns(RuntimeWarning, match="host CPU"):
     root = bot.mcts_search(g.new_initial_state())
   assert root.explore_count == 12 and len(root.children) == 170
-  g19 = pyspiel.load_game("go")  # above the device's 15 x 15: a loud error
-  cbot = pyspiel.MCTSBot(g19, pyspiel.RandomRolloutEvaluator(1, 1), 2.0, 10, 100, True, 1,
+  h13 = pyspiel.load_game("hex(board_size=13)")  # not on the device: a loud error
+  cbot = pyspiel.MCTSBot(h13, pyspiel.RandomRolloutEvaluator(1, 1), 2.0, 10, 100, True, 1,
                          False)
   with pytest.raises(ValueError):
-    cbot.step(g19.new_initial_state())
+    cbot.step(h13.new_initial_state())
 
 
 @pytest.mark.gpu
@@ -98,6 +98,9 @@ def test_gpu_search_refuses_big_boards_and_auto_backend_uses_host_loop():
     ("go(board_size=13)", 70, 60, 10, {}),
     ("go(board_size=12,komi=0.5)", 66, 80, 4, dict(n_rollouts=2, solve=False)),
     ("go(board_size=15)", 66, 40, 20, {}),
+    ("go", 66, 30, 8, {}),  # the default 19 x 19 (go.cc:45): 362 children, wide nodes
+    ("go(board_size=19,komi=0.5)", 20, 300, 30, dict(n_rollouts=2)),
+    ("go(handicap=4)", 40, 40, 0, {}),
     ("go(board_size=13)", 40, 50, 6, dict(child_selection=1)),  # PUCT
 ])
 def test_gpu_big_go_search_matches_oracle(require_gpu, gs, R, sims, plies, kw):
