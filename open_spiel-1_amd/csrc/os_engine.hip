@@ -217,13 +217,13 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
   if (p->layout != OS_LAYOUT_WAVE && p->layout != OS_LAYOUT_LANE &&
       p->layout != OS_LAYOUT_AUTO)
     return Fail(OS_ERR_INVALID, "unknown layout");
-  if (GoBigBoard(e->game.cfg)) {
-    // k_lsearch only: dynamic path / log capacities, 8-bit child counts.
+  if (BigBoard(e->game.cfg)) {
+    // k_lsearch only: dynamic path / log capacities, wide nodes.
     if (!search)
-      return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
+      return Fail(OS_ERR_UNSUPPORTED, "go / hex above 11 x 11 run searches only on the device");
     if (p->layout == OS_LAYOUT_WAVE || p->policy != OS_POLICY_CPP)
       return Fail(OS_ERR_UNSUPPORTED,
-                  "go above 11 x 11 runs C++-policy searches on the lane layout");
+                  "go / hex above 11 x 11 run C++-policy searches on the lane layout");
     return p->child_selection == OS_SELECT_UCT || p->child_selection == OS_SELECT_PUCT
                ? OS_OK : Fail(OS_ERR_INVALID, "unknown child_selection");
   }
@@ -254,7 +254,7 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
 // searches to fill the chip, so go takes it from 16384 roots.
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
   if (layout != OS_LAYOUT_AUTO) return layout;
-  if (cfg.kind == kPig || GoBigBoard(cfg)) return OS_LAYOUT_LANE;  // os_chance.h / k_lsearch
+  if (cfg.kind == kPig || BigBoard(cfg)) return OS_LAYOUT_LANE;  // os_chance.h / k_lsearch
   if (cfg.kind == kGo)
     return policy == OS_POLICY_CPP && R >= 16384 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
   if (cfg.kind == kHex)
@@ -262,18 +262,22 @@ int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t pol
   return OS_LAYOUT_WAVE;
 }
 
-// Per-search HBM buffers of the global-memory lane layout (k_lsearch, go):
-// visit path, position log + links (the expansion buffer is in LDS).
+// Per-search HBM buffers of the global-memory lane layout (k_lsearch: go, and
+// hex above 11 x 11): visit path, go's position log + links (+ bucket heads
+// above 11 x 11), the u16 expansion buffer above 11 x 11 (LDS otherwise).
 bool LaneGlobal(const os_engine* e) {
-  return e->game.cfg.kind == kGo && e->params.layout == OS_LAYOUT_LANE;
+  return (e->game.cfg.kind == kGo || BigBoard(e->game.cfg)) &&
+         e->params.layout == OS_LAYOUT_LANE;
 }
-int LaneLogCap(const GameCfg& c) { return GoBigBoard(c) ? kGoLogCapBig : kGoLogCap; }
+int LaneLogCap(const GameCfg& c) {
+  return c.kind != kGo ? 0 : (GoBigBoard(c) ? kGoLogCapBig : kGoLogCap);
+}
 size_t LaneGlobalBytes(const os_engine* e) {
   if (!LaneGlobal(e)) return 0;
+  const GameCfg& c = e->game.cfg;
   const size_t pe = e->node_double ? sizeof(PathEnt<double>) : sizeof(PathEnt<int32_t>);
-  return (e->game.cfg.max_game_length + 2) * pe +
-         static_cast<size_t>(LaneLogCap(e->game.cfg)) * 12 +
-         (GoBigBoard(e->game.cfg) ? (kGoHeadsBig + e->game.cfg.max_children + 1) * 2 : 0);
+  return (c.max_game_length + 2) * pe + static_cast<size_t>(LaneLogCap(c)) * 12 +
+         (GoBigBoard(c) ? kGoHeadsBig * 2 : 0) + (BigBoard(c) ? (c.max_children + 1) * 2 : 0);
 }
 
 // Nodes per page of the paged arena: room for 64 expansions of the widest
@@ -404,7 +408,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   // f64 node rewards when they are not integers: rollout means, or pig's
   // -1 / (n - 1) losses with more than two players (pig.cc:94-111).
   e->node_double = !(p->n_rollouts == 1 && cfg.pig_players <= 2);
-  e->node_wide = GoBigBoard(cfg);
+  e->node_wide = BigBoard(cfg);
   e->node_bytes = static_cast<int>(
       e->node_wide ? (e->node_double ? sizeof(Node<double, true>) : sizeof(Node<int32_t, true>))
                    : (e->node_double ? sizeof(Node<double>) : sizeof(Node<int32_t>)));
@@ -475,7 +479,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     if ((rc = e->d_lpath.ensure(C * (cfg.max_game_length + 2) * pe)) ||
         (rc = e->d_glog.ensure(C * lc * 8)) || (rc = e->d_glink.ensure(C * lc * 4)) ||
         (GoBigBoard(cfg) && (rc = e->d_lheads.ensure(C * kGoHeadsBig * 2))) ||
-        (GoBigBoard(cfg) && (rc = e->d_lact.ensure(C * (cfg.max_children + 1) * 2))))
+        (BigBoard(cfg) && (rc = e->d_lact.ensure(C * (cfg.max_children + 1) * 2))))
       return rc;
   }
   if ((rc = AllocArena(e))) return rc;
@@ -609,8 +613,8 @@ int ArenaCap(const os_engine* e, const os_mcts_params* p, uint32_t* cap_out) {
 int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* start_actions,
               const int64_t* start_offsets, const uint32_t* bot_seeds,
               const uint32_t* eval_seeds, int32_t max_len, int32_t record) {
-  if (GoBigBoard(e->game.cfg))
-    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
+  if (BigBoard(e->game.cfg))
+    return Fail(OS_ERR_UNSUPPORTED, "go / hex above 11 x 11 run searches only on the device");
   const bool with_visits = (record & OS_RECORD_VISITS) != 0;
   const bool with_obs = (record & OS_RECORD_OBSERVATIONS) != 0;
   const bool with_policy = (record & OS_RECORD_POLICY) != 0;
@@ -884,8 +888,8 @@ int AzStep(os_engine* e, hipStream_t stream) {
 // Uploads one root + n evaluator seeds for the rollout kernels.
 int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
                 const uint32_t* seeds) {
-  if (GoBigBoard(e->game.cfg))
-    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs searches only on the device");
+  if (BigBoard(e->game.cfg))
+    return Fail(OS_ERR_UNSUPPORTED, "go / hex above 11 x 11 run searches only on the device");
   int rc;
   const size_t sb = e->game.state_bytes;
   if ((rc = e->d_roots.ensure(sb))) return rc;
@@ -1087,14 +1091,10 @@ int os_engine_create(const char* game_string, int32_t device, os_engine** out) {
   std::string err = LoadHostGame(game_string, &e->game, &unsupported);
   if (!err.empty()) return Fail(unsupported ? OS_ERR_UNSUPPORTED : OS_ERR_INVALID, err);
   const GameCfg& cfg = e->game.cfg;
-  if (cfg.kind == kHex && cfg.rows > kB128Side)
+  if ((cfg.kind == kHex || cfg.kind == kGo) && cfg.rows > kGoDeviceMaxSide)
     return Fail(OS_ERR_UNSUPPORTED,
-                "the device engine runs hex up to 11 x 11 (B128 bitboards); larger "
-                "boards are supported by the State API only");
-  if (cfg.kind == kGo && cfg.rows > kGoDeviceMaxSide)
-    return Fail(OS_ERR_UNSUPPORTED,
-                "the device engine runs go up to 15 x 15 (lane-layout searches above "
-                "11 x 11); larger boards are supported by the State API only");
+                "the device engine runs hex / go up to 19 x 19 (lane-layout searches above "
+                "11 x 11)");
   int ndev = 0;
   hipError_t he = hipGetDeviceCount(&ndev);
   if (he != hipSuccess || ndev == 0)

@@ -338,10 +338,13 @@ extern GameLaunchers kBreakthroughLaunchers;
 extern GameLaunchers kHexLaunchers;
 extern GameLaunchers kGoLaunchers;
 extern GameLaunchers kGoBigLaunchers;
+extern GameLaunchers kHexBigLaunchers;
 extern GameLaunchers kPigLaunchers;
 
-// go above 11 x 11 runs lane-layout searches only (os_game_go_big.hip).
+// go / hex above 11 x 11 run lane-layout searches only (k_lsearch over B384
+// bitboards; os_game_go_big.hip, os_game_hex_big.hip).
 inline bool GoBigBoard(const GameCfg& c) { return c.kind == kGo && c.rows > 11; }
+inline bool BigBoard(const GameCfg& c) { return (c.kind == kGo || c.kind == kHex) && c.rows > 11; }
 
 inline const GameLaunchers* LaunchersFor(int32_t kind) {
   switch (kind) {
@@ -355,7 +358,8 @@ inline const GameLaunchers* LaunchersFor(int32_t kind) {
   return nullptr;
 }
 inline const GameLaunchers* LaunchersFor(const GameCfg& c) {
-  return GoBigBoard(c) ? &kGoBigLaunchers : LaunchersFor(c.kind);
+  if (BigBoard(c)) return c.kind == kGo ? &kGoBigLaunchers : &kHexBigLaunchers;
+  return LaunchersFor(c.kind);
 }
 
 }  // namespace osx

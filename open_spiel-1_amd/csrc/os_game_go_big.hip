@@ -1,4 +1,4 @@
-// go 12 x 12 .. 15 x 15 kernels of libos_mcts.so: lane-layout searches
+// go 12 x 12 .. 19 x 19 kernels of libos_mcts.so: lane-layout searches
 // (k_lsearch over B384 bitboards) only; see os_kernels.h.
 #include "os_kernels.h"
 

@@ -177,10 +177,16 @@ template <>
 struct LsCaps<GoBig> {  // actions up to 361: u16 expansion buffers in HBM
   static constexpr int act = 1, zob = 2 * 361, heads = 1, log = kGoLogCapBig;
 };
+template <>
+struct LsCaps<HexBig> {  // actions up to 360: u16 expansion buffers in HBM
+  static constexpr int act = 1, zob = 1, heads = 1, log = 1;
+};
 template <class G>
 struct LsWide : std::false_type {};  // Node<R, true>: 16-bit child counts
 template <>
 struct LsWide<GoBig> : std::true_type {};
+template <>
+struct LsWide<HexBig> : std::true_type {};
 
 template <class G>
 struct LCtx {
@@ -972,8 +978,8 @@ int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
   if (a.shared_stream)
     return Fail(OS_ERR_UNSUPPORTED, "go's lane layout runs C++-policy bots (separate streams)");
   if ((!LsWide<G>::value && a.child_cap > LsCaps<G>::act) ||
-      2 * a.cfg.rows * a.cfg.cols > LsCaps<G>::zob)
-    return Fail(OS_ERR_UNSUPPORTED, "go board too large for k_lsearch");
+      (G::State::kNeedsLog && 2 * a.cfg.rows * a.cfg.cols > LsCaps<G>::zob))
+    return Fail(OS_ERR_UNSUPPORTED, "board too large for k_lsearch");
   for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
     a.root_base = base;
@@ -988,11 +994,13 @@ int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
   return OS_OK;
 }
 
-// go above 11 x 11: lane-layout C++-policy searches only (os_game_go_big.hip).
+// go / hex above 11 x 11: lane-layout C++-policy searches only
+// (os_game_go_big.hip, os_game_hex_big.hip).
 template <class G>
 int LaunchSearchOnly(os_engine* e, const DevArgs& a, hipStream_t stream) {
   if (e->params.layout != OS_LAYOUT_LANE || e->params.policy != OS_POLICY_CPP)
-    return Fail(OS_ERR_UNSUPPORTED, "go above 11 x 11 runs C++-policy searches on the lane layout");
+    return Fail(OS_ERR_UNSUPPORTED,
+                "go / hex above 11 x 11 run C++-policy searches on the lane layout");
   return e->node_double ? LaunchLs<G, double>(e, a, stream) : LaunchLs<G, int32_t>(e, a, stream);
 }
 

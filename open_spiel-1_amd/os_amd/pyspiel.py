@@ -180,19 +180,17 @@ class Game:
     return _TYPES[self._info.kind]
 
   # hex / go sides the device engine runs: every search up to 11 x 11 (B128
-  # bitboards); go up to 19 x 19 with C++-policy searches (k_lsearch over
-  # B384 bitboards).  Larger boards (up to 19 x 19) have the State API only.
+  # bitboards); up to 19 x 19 (every board the games load) with C++-policy
+  # searches (k_lsearch over B384 bitboards).
   DEVICE_MAX_SIDE = 11
-  DEVICE_MAX_SIDE_GO_CPP = 19
+  DEVICE_MAX_SIDE_CPP = 19
 
   def on_device(self, numpy_policy=False):
     """Whether the GPU engine can search this game (else: host State API);
     numpy_policy: for the Python MCTSBot's RandomState streams."""
     k, n = self._info.kind, self._info.rows
-    if k == 3 or (k == 4 and numpy_policy):
-      return n <= Game.DEVICE_MAX_SIDE
-    if k == 4:
-      return n <= Game.DEVICE_MAX_SIDE_GO_CPP
+    if k in (3, 4):
+      return n <= (Game.DEVICE_MAX_SIDE if numpy_policy else Game.DEVICE_MAX_SIDE_CPP)
     return True
 
   def get_parameters(self):
