@@ -89,7 +89,8 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
                                       const typename G::State& root,
                                       typename G::Ctx& ctx, Node<R>* nodes, uint32_t cap,
                                       Rng& bot, Rng& ev, PathEnt<R>* path,
-                                      uint16_t* actbuf, int path_cap) {
+                                      uint16_t* actbuf, int path_cap,
+                                      uint32_t* pages = nullptr, uint32_t own_page = 0) {
   SearchResult res;
   res.status = kOk;
   res.sims = 0;
@@ -130,7 +131,8 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
         for (int k = 0; k < nc; ++k) actbuf[k] = static_cast<uint16_t>(l.kth(k));
         if (Policy == kPolicyCpp) CppShuffle(actbuf, nc, bot);
         else NpShuffle(actbuf, nc, bot);
-        if (used + static_cast<uint32_t>(nc) > cap) {
+        if (used + static_cast<uint32_t>(nc) > cap &&
+            !(pages && take_page(pages, own_page, &used, &cap))) {
           res.status = kArenaOverflow;
           goto done;
         }
@@ -259,7 +261,7 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
   }
 done:
   res.nodes = nodes_count;
-  res.used = used;
+  res.used = pages ? 1 + res.expanded : used;  // nodes allocated (mcts_search)
   return res;
 }
 

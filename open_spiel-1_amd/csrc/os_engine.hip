@@ -293,8 +293,9 @@ constexpr int64_t kPagedMinRoots = 64;  // below this the reservation is small
 //  * reserved: the exact worst case 1 + sims * max_children per root (one
 //    expansion per simulation at most; plus the GC stack when GC can fire),
 //    unless the caller caps it, with roots chunked to fit ~60% of HBM;
-//  * paged (arena_mode OS_ARENA_PAGED, wave layout, C++ policy, no GC, >= 64
-//    roots, and a hint from an earlier fetched run of the same shape): one pool of pages
+//  * paged (arena_mode OS_ARENA_PAGED; the wave layout's C++-policy UCT
+//    search or any lane-layout search; no GC, >= 64 roots, and a hint from an
+//    earlier fetched run of the same shape): one pool of pages
 //    for the whole batch, sized from the pages the earlier runs needed per
 //    root (x 1.25 + slack).  A batch that still runs out of pages is rerun on
 //    the reserved arena by the fetch (os_engine_arena_info counts it).
@@ -319,8 +320,13 @@ int SizeArena(os_engine* e, bool allow_paged) {
   e->pool_pages = 0;
   const uint32_t pn = PageNodes(cfg.max_children);
   const auto& h = e->arena_hint;
-  if (allow_paged && e->arena_mode == OS_ARENA_PAGED && p->layout == OS_LAYOUT_WAVE &&
-      p->policy == OS_POLICY_CPP && p->child_selection == OS_SELECT_UCT &&
+  // The wave layout pages its C++-policy UCT kernel only; the lane layouts'
+  // mcts_search takes pages under every policy and child selection.
+  const bool pageable_layout =
+      (p->layout == OS_LAYOUT_WAVE && p->policy == OS_POLICY_CPP &&
+       p->child_selection == OS_SELECT_UCT) ||
+      p->layout == OS_LAYOUT_LANE;
+  if (allow_paged && e->arena_mode == OS_ARENA_PAGED && pageable_layout &&
       !gc_possible && p->arena_nodes == 0 && R >= kPagedMinRoots &&
       h.sims == p->max_simulations && h.node_bytes == e->node_bytes && h.page_nodes == pn &&
       2 * static_cast<int64_t>(pn) <= worst) {
@@ -373,7 +379,7 @@ int AllocArena(os_engine* e) {
 // the pool: a page fills to at least page_nodes - max_children + 1 nodes
 // before a child block spills into the next.
 void UpdateArenaHint(os_engine* e) {
-  if (e->params.layout != OS_LAYOUT_WAVE || e->last_results.empty()) return;
+  if (e->last_results.empty()) return;
   const int mc = e->game.cfg.max_children;
   const uint32_t pn = PageNodes(mc);
   const int64_t eff = static_cast<int64_t>(pn) - mc + 1;
@@ -1221,22 +1227,71 @@ int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
   return OS_OK;
 }
 
-// Copies node i of a raw node array into the export arrays at slot o.
+// Copies node x into the export arrays at slot o.
 extern "C++" template <class N>
-static void ExportNodeT(const unsigned char* raw, uint32_t i, uint32_t o, uint32_t first,
-                        uint32_t* out_first, int32_t* n, double* w, int32_t* action,
-                        int32_t* nchild, int8_t* out0) {
-  const N& x = reinterpret_cast<const N*>(raw)[i];
-  n[o] = x.n; w[o] = x.w; action[o] = x.action; nchild[o] = x.nchild; out0[o] = x.out;
+static void ExportNodeT(const N& x, uint32_t o, uint32_t first, uint32_t* out_first, int32_t* n,
+                        double* w, int32_t* action, int32_t* nchild, int8_t* out0) {
+  n[o] = x.n; w[o] = static_cast<double>(x.w); action[o] = x.action; nchild[o] = x.nchild;
+  out0[o] = x.out;
   out_first[o] = first;
 }
-static void ExportNode(const unsigned char* raw, size_t nb, uint32_t i, uint32_t o,
-                       uint32_t first, uint32_t* out_first, int32_t* n, double* w,
-                       int32_t* action, int32_t* nchild, int8_t* out0) {
-  if (nb == sizeof(Node<int32_t>))
-    ExportNodeT<Node<int32_t>>(raw, i, o, first, out_first, n, w, action, nchild, out0);
-  else
-    ExportNodeT<Node<double>>(raw, i, o, first, out_first, n, w, action, nchild, out0);
+
+// Tree r of the last run as arrays in arena-index order.  Reserved arena: one
+// copy of the tree's `used` nodes.  Paged: the tree's child blocks lie on the
+// root's page and on pages taken later (higher page numbers, filled upward),
+// so index order is allocation order; walk the tree from the root, reading
+// each page once, and renumber the blocks in index order: the same arrays as
+// the reserved arena.
+extern "C++" template <class N>
+static int ExportTree(os_engine* e, int64_t r, uint32_t used, uint32_t* first, int32_t* n,
+                      double* w, int32_t* action, int32_t* nchild, int8_t* out0) {
+  unsigned char* const arena = static_cast<unsigned char*>(e->d_arena.p);
+  if (!e->paged) {
+    std::vector<N> raw(used);
+    HIP_TRY(hipMemcpy(raw.data(), arena + static_cast<size_t>(r) * e->cap * sizeof(N),
+                      used * sizeof(N), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < used; ++i)
+      ExportNodeT(raw[i], i, raw[i].first, first, n, w, action, nchild, out0);
+    return OS_OK;
+  }
+  const uint64_t pn = e->page_nodes;
+  const uint64_t base = static_cast<uint64_t>(r) * pn;  // node indices are relative to it
+  std::map<uint64_t, std::vector<N>> pages;
+  auto node_at = [&](uint64_t rel) -> const N* {
+    const uint64_t g = base + rel, pg = g / pn;
+    auto it = pages.find(pg);
+    if (it == pages.end()) {
+      std::vector<N> buf(pn);
+      if (hipMemcpy(buf.data(), arena + pg * pn * sizeof(N), pn * sizeof(N),
+                    hipMemcpyDeviceToHost) != hipSuccess)
+        return nullptr;
+      it = pages.emplace(pg, std::move(buf)).first;
+    }
+    return &it->second[g - pg * pn];
+  };
+  struct Blk { uint32_t rel, cnt; };
+  std::vector<Blk> blocks{{0u, 1u}};  // the root is a block of one
+  for (size_t b = 0; b < blocks.size(); ++b) {
+    for (uint32_t k = 0; k < blocks[b].cnt; ++k) {
+      const N* p = node_at(blocks[b].rel + k);
+      if (!p) return Fail(OS_ERR_DEVICE, "tree export copy failed");
+      if (p->nchild) blocks.push_back({p->first, static_cast<uint32_t>(p->nchild)});
+    }
+  }
+  std::sort(blocks.begin(), blocks.end(), [](const Blk& a, const Blk& b) { return a.rel < b.rel; });
+  std::unordered_map<uint32_t, uint32_t> renum;  // block start -> export index
+  uint32_t o = 0;
+  for (const Blk& b : blocks) { renum[b.rel] = o; o += b.cnt; }
+  if (o != used) return Fail(OS_ERR_DEVICE, "paged tree export: node count mismatch");
+  o = 0;
+  for (const Blk& b : blocks) {
+    for (uint32_t k = 0; k < b.cnt; ++k, ++o) {
+      const N* p = node_at(b.rel + k);
+      // A childless node keeps the reserved arena's first (0).
+      ExportNodeT(*p, o, p->nchild ? renum[p->first] : 0u, first, n, w, action, nchild, out0);
+    }
+  }
+  return OS_OK;
 }
 
 int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
@@ -1251,96 +1306,13 @@ int os_engine_tree(os_engine* e, int64_t r, int64_t* count, uint32_t* first,
   *count = used;
   if (!first) return OS_OK;
   HIP_TRY(hipSetDevice(e->device));
-  const size_t nb = e->node_bytes;
-  if (e->node_wide) {  // k_lsearch's wide nodes (go above 11 x 11): reserved arena
-    std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
-    HIP_TRY(hipMemcpy(raw.data(),
-                      static_cast<unsigned char*>(e->d_arena.p) +
-                          static_cast<size_t>(r) * e->cap * nb,
-                      raw.size(), hipMemcpyDeviceToHost));
-    for (uint32_t i = 0; i < used; ++i) {
-      if (e->node_double) {
-        using N = Node<double, true>;
-        ExportNodeT<N>(raw.data(), i, i, reinterpret_cast<const N*>(raw.data())[i].first, first,
-                       n, w, action, nchild, out0);
-      } else {
-        using N = Node<int32_t, true>;
-        ExportNodeT<N>(raw.data(), i, i, reinterpret_cast<const N*>(raw.data())[i].first, first,
-                       n, w, action, nchild, out0);
-      }
-    }
-    return OS_OK;
-  }
-  if (!e->paged) {
-    std::vector<unsigned char> raw(static_cast<size_t>(used) * nb);
-    HIP_TRY(hipMemcpy(raw.data(),
-                      static_cast<unsigned char*>(e->d_arena.p) +
-                          static_cast<size_t>(r) * e->cap * nb,
-                      raw.size(), hipMemcpyDeviceToHost));
-    for (uint32_t i = 0; i < used; ++i) {
-      const uint32_t f = nb == sizeof(Node<int32_t>)
-                             ? reinterpret_cast<const Node<int32_t>*>(raw.data())[i].first
-                             : reinterpret_cast<const Node<double>*>(raw.data())[i].first;
-      ExportNode(raw.data(), nb, i, i, f, first, n, w, action, nchild, out0);
-    }
-    return OS_OK;
-  }
-  // Paged: the tree's child blocks lie on the root's page and on pages taken
-  // later (higher page numbers, filled upward), so index order is allocation
-  // order.  Walk the tree from the root, reading each page once, and
-  // renumber the blocks in index order: the same arrays as the reserved arena.
-  const uint64_t pn = e->page_nodes;
-  const uint64_t base = static_cast<uint64_t>(r) * pn;  // node indices are relative to it
-  std::map<uint64_t, std::vector<unsigned char>> pages;
-  auto node_at = [&](uint64_t rel) -> const unsigned char* {
-    const uint64_t g = base + rel, pg = g / pn;
-    auto it = pages.find(pg);
-    if (it == pages.end()) {
-      std::vector<unsigned char> buf(pn * nb);
-      if (hipMemcpy(buf.data(), static_cast<unsigned char*>(e->d_arena.p) + pg * pn * nb,
-                    buf.size(), hipMemcpyDeviceToHost) != hipSuccess)
-        return nullptr;
-      it = pages.emplace(pg, std::move(buf)).first;
-    }
-    return it->second.data() + (g - pg * pn) * nb;
-  };
-  struct Blk { uint32_t rel, cnt; };
-  std::vector<Blk> blocks{{0u, 1u}};  // the root is a block of one
-  for (size_t b = 0; b < blocks.size(); ++b) {
-    for (uint32_t k = 0; k < blocks[b].cnt; ++k) {
-      const unsigned char* p = node_at(blocks[b].rel + k);
-      if (!p) return Fail(OS_ERR_DEVICE, "tree export copy failed");
-      uint32_t f;
-      uint8_t nc;
-      if (nb == sizeof(Node<int32_t>)) {
-        f = reinterpret_cast<const Node<int32_t>*>(p)->first;
-        nc = reinterpret_cast<const Node<int32_t>*>(p)->nchild;
-      } else {
-        f = reinterpret_cast<const Node<double>*>(p)->first;
-        nc = reinterpret_cast<const Node<double>*>(p)->nchild;
-      }
-      if (nc) blocks.push_back({f, nc});
-    }
-  }
-  std::sort(blocks.begin(), blocks.end(), [](const Blk& a, const Blk& b) { return a.rel < b.rel; });
-  std::unordered_map<uint32_t, uint32_t> renum;  // block start -> export index
-  uint32_t o = 0;
-  for (const Blk& b : blocks) { renum[b.rel] = o; o += b.cnt; }
-  if (o != used) return Fail(OS_ERR_DEVICE, "paged tree export: node count mismatch");
-  o = 0;
-  for (const Blk& b : blocks) {
-    for (uint32_t k = 0; k < b.cnt; ++k, ++o) {
-      const unsigned char* p = node_at(b.rel + k);
-      const bool i32 = nb == sizeof(Node<int32_t>);
-      const uint32_t f = i32 ? reinterpret_cast<const Node<int32_t>*>(p)->first
-                             : reinterpret_cast<const Node<double>*>(p)->first;
-      const uint8_t nc = i32 ? reinterpret_cast<const Node<int32_t>*>(p)->nchild
-                             : reinterpret_cast<const Node<double>*>(p)->nchild;
-      // A childless node keeps the reserved arena's first (0).
-      ExportNode(p, nb, 0, o, nc ? renum[f] : 0u, first, n, w, action, nchild, out0);
-    }
-  }
-  return OS_OK;
+  if (e->node_wide)  // k_lsearch's wide nodes (go / hex above 11 x 11)
+    return e->node_double
+               ? ExportTree<Node<double, true>>(e, r, used, first, n, w, action, nchild, out0)
+               : ExportTree<Node<int32_t, true>>(e, r, used, first, n, w, action, nchild, out0);
+  return e->node_double
+             ? ExportTree<Node<double>>(e, r, used, first, n, w, action, nchild, out0)
+             : ExportTree<Node<int32_t>>(e, r, used, first, n, w, action, nchild, out0);
 }
 
 int os_engine_set_arena_mode(os_engine* e, int32_t mode) {

@@ -25,13 +25,14 @@ template <class G, class R, int Policy, class Rng>
 __device__ SearchResult lane_search(const GameCfg& g, const SearchParams& sp,
                                     const typename G::State& root, typename G::Ctx& ctx,
                                     Node<R>* nodes, uint32_t cap, Rng& bot, Rng& ev,
-                                    PathEnt<R>* path, uint16_t* actbuf, int path_cap) {
+                                    PathEnt<R>* path, uint16_t* actbuf, int path_cap,
+                                    uint32_t* pages, uint32_t own_page) {
   if constexpr (HasChance<G>::value)
     return mcts_search_chance<G, R, Policy>(g, sp, root, ctx, nodes, cap, bot, ev, path,
-                                            actbuf, path_cap);
+                                            actbuf, path_cap, pages, own_page);
   else
     return mcts_search<G, R, Policy>(g, sp, root, ctx, nodes, cap, bot, ev, path, actbuf,
-                                     path_cap);
+                                     path_cap, pages, own_page);
 }
 
 
@@ -117,10 +118,12 @@ __global__ __launch_bounds__(64) void k_mcts(DevArgs a) {
   SearchResult res;
   if (Policy == kPolicyNumpy && a.shared_stream)
     res = lane_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot,
-                                    path, actbuf, a.path_cap);
+                                    path, actbuf, a.path_cap, a.pages,
+                                    static_cast<uint32_t>(lr));
   else
     res = lane_search<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev,
-                                    path, actbuf, a.path_cap);
+                                    path, actbuf, a.path_cap, a.pages,
+                                    static_cast<uint32_t>(lr));
   res.rng_words = bot.words + ((Policy == kPolicyNumpy && a.shared_stream) ? 0u : ev.words);
   a.results[gr] = res;
   const Node<R>& rn = nodes[0];
@@ -268,11 +271,11 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   if constexpr (LsWide<G>::value) {
     StridedPtr<uint16_t> act{a.lact + lr * a.child_cap, 1};
     res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
-                                        act, a.path_cap);
+                                        act, a.path_cap, a.pages, static_cast<uint32_t>(lr));
   } else {
     StridedPtr<uint8_t> act{acts + (threadIdx.x & 63), 64};
     res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
-                                        act, a.path_cap);
+                                        act, a.path_cap, a.pages, static_cast<uint32_t>(lr));
   }
   res.rng_words = bot.words + ev.words;
   a.results[gr] = res;

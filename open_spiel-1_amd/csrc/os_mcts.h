@@ -226,16 +226,40 @@ struct StridedPtr {
   OS_HD T& operator[](int i) const { return p[static_cast<int64_t>(i) * stride]; }
 };
 
+// Page-pool descriptor of the paged arena (os_engine.hip AllocArena), u32
+// words: pages taken by this launch, nodes per page, pages in the pool, first
+// page handed out dynamically (the searches' own pages come first).
+constexpr int kPgTaken = 0, kPgNodes = 1, kPgPool = 2, kPgFirstDynamic = 3;
+
+// The next page of the pool for search `own_page` whose arena `nodes` starts
+// at its own page: the child block goes to the start of that page, node
+// indices stay relative to the search's first page.  false when the pool is
+// exhausted (the batch is then rerun on the reserved arena).
+OS_HD bool take_page(uint32_t* pg, uint32_t own_page, uint32_t* used, uint32_t* cap) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t np = atomicAdd(pg + kPgTaken, 1u) + pg[kPgFirstDynamic];
+#else
+  const uint32_t np = pg[kPgTaken]++ + pg[kPgFirstDynamic];
+#endif
+  if (np >= pg[kPgPool]) return false;
+  *used = (np - own_page) * pg[kPgNodes];
+  *cap = *used + pg[kPgNodes];
+  return true;
+}
+
 // One complete search from `root`.  `bot` and `ev` are the two MT19937
 // streams (the same object under kPolicyNumpy).  `actbuf` holds >=
 // max_children entries, `path` >= path_cap >= MaxGameLength + 1 entries
-// (pointers, or StridedPtr views of batch-SoA buffers).
+// (pointers, or StridedPtr views of batch-SoA buffers).  `pages` (optional)
+// is the page pool's descriptor: a child block that does not fit in `cap`
+// then goes to the next free page (`own_page` = this search's first page).
 template <class G, class R, int Policy, class Rng, class PathA, class ActA, class Ctx, bool W>
 OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
                                const typename G::State& root,
                                Ctx& ctx, Node<R, W>* nodes,
                                uint32_t cap, Rng& bot, Rng& ev, PathA path,
-                               ActA actbuf, int path_cap) {
+                               ActA actbuf, int path_cap, uint32_t* pages = nullptr,
+                               uint32_t own_page = 0) {
   SearchResult res;
   res.status = kOk;
   res.sims = 0;
@@ -283,7 +307,8 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         for (int k = 0; k < nc; ++k) actbuf[k] = static_cast<uint16_t>(l.kth(k));
         if (Policy == kPolicyCpp) CppShuffle(actbuf, nc, bot);
         else NpShuffle(actbuf, nc, bot);
-        if (used + static_cast<uint32_t>(nc) > cap) {
+        if (used + static_cast<uint32_t>(nc) > cap &&
+            !(pages && take_page(pages, own_page, &used, &cap))) {
           res.status = kArenaOverflow;
           goto done;
         }
@@ -467,7 +492,9 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
   }
 done:
   res.nodes = nodes_count;
-  res.used = used;
+  // Nodes allocated (== the last used slot on the reserved arena; on the
+  // paged arena `used` is an index into a later page).
+  res.used = pages ? 1 + res.expanded : used;
   return res;
 }
 

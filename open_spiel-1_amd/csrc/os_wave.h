@@ -1282,7 +1282,7 @@ __device__ __forceinline__ Node<int32_t> load_node(const Node<int32_t>* p) {
 // k_wsearch leaves the descriptor's address in the kPageDescLds bytes of LDS
 // just below `path` (kPageable searches only): read on that rare path, it
 // holds no scalar registers across the search, which is at its SGPR budget.
-enum { kPgTaken = 0, kPgNodes = 1, kPgPool = 2, kPgFirstDynamic = 3 };
+// (kPgTaken ... kPgFirstDynamic: os_mcts.h.)
 constexpr int kPageDescLds = 16;
 
 // LegalActions()[k] for lane k (k < count; other lanes get garbage) in the

@@ -26,18 +26,18 @@ def _batch(E, gs, R, sims, plies, seed=1000):
   return acts, offs, bs, bs + np.uint32(1 << 20)
 
 
-def _run(eng, batch, sims):
+def _run(eng, batch, sims, **params):
   acts, offs, bs, es = batch
-  eng.prepare(acts, offs, bs, es, uct_c=2.0, max_simulations=sims)
+  eng.prepare(acts, offs, bs, es, uct_c=2.0, max_simulations=sims, **params)
   eng.run_async()
   return eng.fetch(), eng.arena_info()
 
 
-def _check_oracle(E, gs, eng, out, batch, sims, roots=16):
+def _check_oracle(E, gs, eng, out, batch, sims, roots=16, puct=False):
   acts, offs, bs, es = batch
   ref = O.Game(gs).mcts_batch(acts[:offs[roots]], offs[:roots + 1], bs[:roots], es[:roots],
                               uct_c=2.0, max_simulations=sims,
-                              max_children=eng.max_children, threads=8)
+                              max_children=eng.max_children, threads=8, puct=puct)
   bad = [k for k in E.OUTPUT_KEYS if not np.array_equal(out[k][:roots], ref[k])]
   assert not bad, bad
 
@@ -142,3 +142,55 @@ def test_root_sums_after_pool_overflow(E):
   assert eng.arena_info()["reruns"] == 1
   assert np.array_equal(vis, want) and s == int(out["root_n"].sum())
   np.testing.assert_array_equal(rew, w.cpu().numpy())
+
+
+# The lane layouts' searches (os_mcts.h mcts_search, os_chance.h) take pages
+# per lane: k_lsearch for go (narrow nodes at 9 x 9, wide above 11 x 11) and
+# hex above 11 x 11, k_mcts for the rest (pig's chance search included), under
+# UCT and PUCT.  sims is chosen so that two pages fit the worst case.
+@pytest.mark.parametrize("gs,R,sims,plies,puct", [
+    ("go(board_size=9)", 64, 256, 4, False),
+    ("go(board_size=9)", 64, 256, 4, True),
+    ("go(board_size=13)", 64, 256, 4, False),
+    ("hex(board_size=13)", 64, 256, 4, False),
+    ("connect_four", 128, 400, 6, False),
+    ("pig", 64, 256, 0, False),
+])
+def test_lane_layout_paged_equals_reserved(E, gs, R, sims, plies, puct):
+  from os_amd import _lib
+  kw = dict(layout=_lib.LAYOUT_LANE,
+            child_selection=_lib.SELECT_PUCT if puct else _lib.SELECT_UCT)
+  eng = E.Engine(gs)
+  eng.set_arena_mode("paged")
+  batch = _batch(E, gs, R, sims, plies)
+  ref, info0 = _run(eng, batch, sims, **kw)
+  assert info0["paged"] == 0
+  got, info = _run(eng, batch, sims, **kw)
+  assert info["paged"] == 1 and info["reruns"] == 0
+  assert info["arena_bytes"] < info["reserved_bytes"]
+  assert info["pages_used"] <= info["pool_pages_or_chunk_roots"]
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+  _check_oracle(E, gs, eng, got, batch, sims, roots=8, puct=puct)
+  eng2 = E.Engine(gs)
+  _run(eng2, batch, sims, **kw)
+  for r in (0, R - 1):
+    a, b = eng.tree(r), eng2.tree(r)
+    for k in a:
+      np.testing.assert_array_equal(a[k], b[k], err_msg="root %d %s" % (r, k))
+
+
+def test_lane_layout_pool_overflow_reruns_reserved(E):
+  from os_amd import _lib
+  gs, R, sims = "connect_four", 128, 400
+  eng = E.Engine(gs)
+  eng.set_arena_mode("paged")
+  acts, offs = E.roots_from_histories([[0, 1, 0, 1, 0, 1]] * R)
+  bs = np.arange(R, dtype=np.uint32)
+  late = (acts, offs, bs, bs + np.uint32(1 << 20))
+  _run(eng, late, sims, layout=_lib.LAYOUT_LANE)
+  assert _run(eng, late, sims, layout=_lib.LAYOUT_LANE)[1]["paged"] == 1
+  early = _batch(E, gs, R, sims, 0, seed=5000)
+  got, info = _run(eng, early, sims, layout=_lib.LAYOUT_LANE)
+  assert info["reruns"] == 1 and info["overflowed_searches"] > 0
+  _check_oracle(E, gs, eng, got, early, sims)
