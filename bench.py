@@ -647,7 +647,8 @@ def bench_az(args, ctx, layout):
   obs_size = int(np.prod(search.obs_shape))
   net = _az_network(obs_size, A, torch, ctx.dev)
   kw = dict(puct=True, max_simulations=sims, uct_c=c, dirichlet_alpha=alpha,
-            dirichlet_epsilon=eps, stream=ctx.stream, requests=args.az_requests)
+            dirichlet_epsilon=eps, stream=ctx.stream, requests=args.az_requests,
+            block_size=args.block)
   parity = None
   if ctx.rank == 0 and args.parity_roots > 0:  # exact toy evaluator on a prefix vs the oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -704,6 +705,7 @@ def bench_az(args, ctx, layout):
                         "game": game, "searches_per_gpu": R, "sims_per_search": sims,
                         "parallelism": "dp%d (independent searches)" % ctx.world,
                         "layout": "lane (continuation in HBM)",
+                        "searches_per_wave": args.block or 64,
                         "evaluator_requests": args.az_requests,
                         "rounds": "hip graph replay" if args.az_graph else "eager",
                         "sims_per_step_per_gpu": sims_step,

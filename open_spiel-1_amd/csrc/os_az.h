@@ -118,8 +118,12 @@ OS_HD void az_request(const GameCfg& g, const typename G::State& s, int kind, co
                       int obs_size, int num_actions, typename G::Ctx& ctx) {
   *io.kind = kind;
   const int cells = g.rows * g.cols;
+  const int planes = obs_size / cells;
   const int p = G::to_move(s);
-  for (int i = 0; i < obs_size; ++i) io.obs[i] = G::obs(s, g, p, i / cells, i % cells);
+  // Cell-major walk of the CHW tensor: the cell's contents are decoded once
+  // for all its planes (no per-element division by the cell count).
+  for (int c = 0; c < cells; ++c)
+    for (int pl = 0; pl < planes; ++pl) io.obs[pl * cells + c] = G::obs(s, g, p, pl, c);
   for (int a = 0; a < num_actions; ++a) io.legal[a] = 0;
   const typename G::Legal l = G::legal(s, g, ctx);
   for (int k = 0; k < l.count; ++k) io.legal[l.kth(k)] = 1;

@@ -1175,7 +1175,9 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.best_action = d.best_action;
   HIP_TRY(hipMemsetAsync(e->az_pending, 0, sizeof(int32_t), stream));
   if (e->num_roots == 0) return OS_OK;
-  const int bs = 64;
+  // Searches per workgroup (one wave): os_mcts_params.block_size, 64 by
+  // default.  Fewer lanes per wave spread a small batch over more SIMDs.
+  const int bs = e->params.block_size > 0 ? std::min(e->params.block_size, 64) : 64;
   hipLaunchKernelGGL(k_az_step<G>, dim3(static_cast<unsigned>((e->num_roots + bs - 1) / bs)),
                      dim3(bs), 0, stream, a);
   HIP_TRY(hipGetLastError());

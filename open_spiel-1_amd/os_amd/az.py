@@ -56,7 +56,7 @@ class ExternalEvaluatorSearch:
   def run(self, root_actions, root_offsets, bot_seeds, evaluator, puct=True,
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
           dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False,
-          bot_rng=None, requests="fused", graph=False, graph_batch=8):
+          bot_rng=None, requests="fused", graph=False, graph_batch=8, block_size=0):
     """Runs every search to completion; returns the os_mcts_batch outputs.
 
     The evaluator may be called once more after the last step, with every
@@ -68,6 +68,7 @@ class ExternalEvaluatorSearch:
     dirichlet_alpha / dirichlet_epsilon are the MCTSBot constructor's
     (mcts.h:152-159): root priors become (1 - eps) * p + eps * Dir(alpha)
     noise drawn from the bot's rng before the root's shuffle (mcts.cc:265-273).
+    block_size: searches per k_az_step workgroup (one wave; 64 when 0).
     time_steps: record a HIP event pair around every k_az_step launch on the
     launch stream (`step_ms()` then sums them).
 
@@ -91,7 +92,7 @@ class ExternalEvaluatorSearch:
     value = torch.zeros(R, dtype=torch.float64, device=dev)
     pending = torch.zeros(1, dtype=torch.int32, device=dev)
     p = E.make_params(uct_c=uct_c, max_simulations=max_simulations,
-                      max_memory_mb=max_memory_mb, solve=solve)
+                      max_memory_mb=max_memory_mb, solve=solve, block_size=block_size)
     acts = _lib.i64(root_actions)
     if requests not in _REQUESTS:
       raise ValueError("requests must be 'fused' or 'separate'")
