@@ -948,17 +948,18 @@ extern "C" {
 const char* os_last_error(void) { return g_err.c_str(); }
 
 int os_debug_phase_cycles(uint64_t* out, int32_t n) {
-#if OS_PHASE_TIMING
-  if (!out || n < kNumPhases) return Fail(OS_ERR_INVALID, "need kNumPhases slots");
-  // Each game's kernels live in their own code object: sum the counters.
-  std::vector<uint64_t> acc(kNumPhases, 0), one(kNumPhases, 0);
+#if OS_PHASE_TIMING || OS_WAVE_TIMES
+  if (!out || n < kDbgSlots) return Fail(OS_ERR_INVALID, "need kDbgSlots slots");
+  // Each game's kernels live in their own code object: sum the counters (the
+  // wave-time slots of the games that did not run are zero).
+  std::vector<uint64_t> acc(kDbgSlots, 0), one(kDbgSlots, 0);
   for (int k = kTicTacToe; k <= kPig; ++k) {
     const int rc = LaunchersFor(k)->phase_cycles(one.data(), true);
     if (rc) return rc;
-    for (int i = 0; i < kNumPhases; ++i) acc[i] += one[i];
+    for (int i = 0; i < kDbgSlots; ++i) acc[i] += one[i];
   }
-  std::memcpy(out, acc.data(), sizeof(uint64_t) * kNumPhases);
-  return kNumPhases;
+  std::memcpy(out, acc.data(), sizeof(uint64_t) * kDbgSlots);
+  return kDbgSlots;
 #else
   (void)out;
   (void)n;

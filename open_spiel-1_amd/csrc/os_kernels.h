@@ -37,8 +37,8 @@ __device__ SearchResult lane_search(const GameCfg& g, const SearchParams& sp,
 
 
 
-#if OS_PHASE_TIMING
-static __device__ uint64_t g_phase_cycles[kNumPhases];  // diagnostic build only; internal linkage: one per game TU
+#if OS_PHASE_TIMING || OS_WAVE_TIMES
+static __device__ uint64_t g_phase_cycles[kDbgSlots];  // diagnostic build only; internal linkage: one per game TU
 #endif
 
 
@@ -357,6 +357,9 @@ template <class G, class R, int Policy, bool kPaged, bool kPuct>
 __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int64_t lr = blockIdx.x;
   if (lr >= a.num_roots) return;
+#if OS_WAVE_TIMES
+  const uint64_t wt_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const int64_t gr = a.root_base + lr;
   const int l = lane_id();
   extern __shared__ __align__(16) unsigned char smem[];
@@ -401,9 +404,9 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   if constexpr (std::is_same<G, Go>::value) ctx.sub = ph.c;
 #endif
   SearchResult res = shared
-      ? wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE>(
+      ? wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE, OS_PACE != 0>(
             a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path, a.path_cap, ph, lcache)
-      : wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE>(
+      : wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE, OS_PACE != 0>(
             a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path, a.path_cap, ph, lcache);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
@@ -412,6 +415,15 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
     for (int i = 0; i < kNumPhases; ++i)
       atomicAdd(reinterpret_cast<unsigned long long*>(&g_phase_cycles[i]),
                 static_cast<unsigned long long>(ph.c[i]));
+#endif
+#if OS_WAVE_TIMES
+  if (l == 0 && lr < kWaveTimesMax) {
+    uint64_t* wt = g_phase_cycles + kNumPhases + 3 * lr;
+    wt[0] = wt_start;
+    wt[1] = __builtin_amdgcn_s_memrealtime();
+    wt[2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF804)) |
+            (static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32);
+  }
 #endif
   __threadfence_block();
   const Node<R> rn = nodes[0];
@@ -1222,14 +1234,14 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   return OS_OK;
 }
 
-#if OS_PHASE_TIMING
+#if OS_PHASE_TIMING || OS_WAVE_TIMES
 static int PhaseCycles(uint64_t* out, bool clear) {  // static: per game TU
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(uint64_t) * kNumPhases));
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_cycles), sizeof(uint64_t) * kDbgSlots));
   if (clear) {
-    std::vector<uint64_t> zero(kNumPhases, 0);
+    std::vector<uint64_t> zero(kDbgSlots, 0);
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_cycles), zero.data(),
-                              sizeof(uint64_t) * kNumPhases));
+                              sizeof(uint64_t) * kDbgSlots));
   }
   return OS_OK;
 }

@@ -76,7 +76,30 @@
 #define OS_AB_HEX 0
 #endif
 
+// Issue priority by progress (results unchanged): the wave searches of a
+// launch start together and share each SIMD four ways, and the hardware
+// arbitrates issue by priority, then age, so without help the youngest waves
+// (the last roots) starve and finish last while the SIMD idles around them.
+// Every OS_PACE_EVERY simulations a search compares its own simulation count
+// with the mean over the searches resident at that moment (one packed
+// launch-wide counter: resident searches << 44 | their simulations) and sets
+// its priority (s_setprio 0..3) by how far behind or ahead of the mean it is,
+// with bands of max_simulations / OS_PACE_BAND.  C2: 9.26 -> 7.2 ms.
+#ifndef OS_PACE
+#define OS_PACE 1
+#endif
+#ifndef OS_PACE_EVERY
+#define OS_PACE_EVERY 32
+#endif
+#ifndef OS_PACE_BAND
+#define OS_PACE_BAND 32
+#endif
+
 namespace osm {
+
+#if OS_PACE
+static __device__ unsigned long long g_pace;  // internal linkage: one per game TU
+#endif
 
 enum PhaseId { kPhSelect = 0, kPhExpand, kPhRollout, kPhBackup, kPhSolver, kPhTail,
                kPhTwist, kPhTotal,
@@ -86,6 +109,14 @@ enum PhaseId { kPhSelect = 0, kPhExpand, kPhRollout, kPhBackup, kPhSolver, kPhTa
 struct PhaseCycles {
   uint64_t c[kNumPhases];
 };
+// Diagnostic build (-DOS_WAVE_TIMES=1): each wave search also records
+// (s_memrealtime at start, at end, HW_ID | XCC_ID << 32) after the phase
+// counters, one triple per root (first kWaveTimesMax roots).
+#ifndef OS_WAVE_TIMES
+#define OS_WAVE_TIMES 0
+#endif
+constexpr int kWaveTimesMax = 16384;
+constexpr int kDbgSlots = kNumPhases + (OS_WAVE_TIMES ? 3 * kWaveTimesMax : 0);
 #if OS_PHASE_TIMING
 #define OS_PH_NOW() __builtin_amdgcn_s_memtime()
 #define OS_PH_ADD(acc, t0) ((acc) += __builtin_amdgcn_s_memtime() - (t0))
@@ -119,6 +150,49 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 // An instrumentation counter kept in lane 0 of a VGPR rather than in an
 // SGPR: the wave kernels are SGPR-bound (the state, the tree walk and both
 // MT streams are scalar), and a spilled SGPR costs far more than one VALU op.
+// The pacing counter of one wave (see OS_PACE): `progress` is the work the
+// wave has done (simulations), `band` the gap that moves it one priority
+// level.
+struct Pacer {
+  static constexpr int kShift = 44;
+  unsigned long long added = 0;  // this wave's share of the counter
+  uint32_t reported = 0;
+  __device__ __forceinline__ void begin() {
+#if OS_PACE
+    added = 1ull << kShift;
+    if (lane_id() == 0) atomicAdd(&g_pace, added);
+#endif
+  }
+  __device__ __forceinline__ void update(uint32_t progress, int64_t band) {
+#if OS_PACE
+    const unsigned long long d = progress - reported;
+    reported = progress;
+    added += d;
+    unsigned long long c = 0;
+    if (lane_id() == 0) c = atomicAdd(&g_pace, d);
+    c = rl64(c, 0) + d;
+    const int64_t active = static_cast<int64_t>(c >> kShift);
+    const int64_t sum = static_cast<int64_t>(c & ((1ull << kShift) - 1));
+    // (mean - progress) * active against band * active
+    const int64_t gap = sum - static_cast<int64_t>(progress) * active;
+    band *= active;
+    if (gap > band) __builtin_amdgcn_s_setprio(3);
+    else if (gap > 0) __builtin_amdgcn_s_setprio(2);
+    else if (gap > -band) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#else
+    (void)progress;
+    (void)band;
+#endif
+  }
+  __device__ __forceinline__ void end() {
+#if OS_PACE
+    if (lane_id() == 0) atomicAdd(&g_pace, 0ull - added);
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  }
+};
+
 struct LaneCount {
   uint32_t v;
   __device__ void reset() { v = 0; }
@@ -1393,7 +1467,7 @@ struct NodeCache {
 // PUCTValue (sp.log_lut then holds sqrt(N)); kCache > 0: `lcache` (LDS)
 // holds the first kCache nodes (NodeCache).
 template <class G, class R, int Policy, bool kPageable = false, bool kPuct = false,
-          int kCache = 0, class C>
+          int kCache = 0, bool kPace = false, class C>
 __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     const typename G::State& root, C& ctx,
                                     Node<R>* nodes, uint32_t cap, WaveMt& bot,
@@ -1451,7 +1525,11 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   LanePath<R> lp;
   if (kLP && path_cap > 64) path_cap = 64;
 
+  Pacer pacer;
+  if (kPace) pacer.begin();
   for (int sim = 0; sim < sp.max_simulations; ++sim) {
+    if (kPace && (sim & (OS_PACE_EVERY - 1)) == 0 && sim > 0)
+      pacer.update(static_cast<uint32_t>(sim), sp.max_simulations / OS_PACE_BAND);
     uint64_t t_ph = OS_PH_NOW();
     typename G::State s = root;
     ctx.reset();
@@ -1897,6 +1975,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     OS_PH_ADD(ph.c[kPhTail], t_ph);
   }
 done:
+  if (kPace) pacer.end();
   OS_PH_ADD(ph.c[kPhTotal], t_begin);
   res.scanned = c_scanned.get();
   res.backed = c_backed.get();
