@@ -88,6 +88,14 @@
 #ifndef OS_PACE
 #define OS_PACE 1
 #endif
+// OS_SCREEN_LOG (integer-reward UCT with the f32 screen): 1 takes the
+// screen's log(N) from v_log_f32 of the parent count (no per-lane log-table
+// gather on the selection chain; the exact f64 log(N) is read only when the
+// screen falls back), reduces the screen by integer keys (DPP folded into
+// v_max_i32) and bounds the near-tie band with v_sqrt_f32.
+#ifndef OS_SCREEN_LOG
+#define OS_SCREEN_LOG 1
+#endif
 #ifndef OS_PACE_EVERY
 #define OS_PACE_EVERY 32
 #endif
@@ -753,6 +761,69 @@ __device__ __forceinline__ int uct_argmax_screen(const Node<int32_t>& c0, bool i
   return ballot(near) ? -1 : j;
 }
 
+// Order-preserving int32 key of a non-NaN f32 (an involution: the same map
+// decodes), so the screen's wave maximum runs on integers and DPP folds into
+// v_max_i32 (no canonicalising v_max_f32 per step).  -0 and +0 get different
+// keys; the near-tie test below still sends any such pair to the exact path.
+__device__ __forceinline__ int32_t f32_key(float a) {
+  const int32_t b = __float_as_int(a);
+  return b ^ ((b >> 31) & 0x7FFFFFFF);
+}
+__device__ __forceinline__ float key_f32(int32_t k) {
+  return __int_as_float(k ^ ((k >> 31) & 0x7FFFFFFF));
+}
+template <int Ctrl, int RowMask = 0xf>
+__device__ __forceinline__ int32_t dpp_max_i32(int32_t v) {
+  return max(v, __builtin_amdgcn_update_dpp(static_cast<int32_t>(0x80000000u), v, Ctrl,
+                                            RowMask, 0xf, false));
+}
+template <int Lanes>
+__device__ __forceinline__ int32_t wave_max_key(int32_t v) {
+  v = dpp_max_i32<0xB1>(v);                   // quad_perm [1,0,3,2]
+  if (Lanes > 2) v = dpp_max_i32<0x4E>(v);    // quad_perm [2,3,0,1]
+  if (Lanes > 4) v = dpp_max_i32<0x141>(v);   // row_half_mirror
+  if (Lanes > 8) v = dpp_max_i32<0x140>(v);   // row_mirror
+  if (Lanes > 16) {
+    v = dpp_max_i32<0x142, 0xa>(v);  // row_bcast15 -> rows 1, 3
+    v = dpp_max_i32<0x143, 0xc>(v);  // row_bcast31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+  }
+  return __builtin_amdgcn_readfirstlane(v);
+}
+// uct_argmax_screen with the parent term lf = log(N) in f32 from v_log_f32
+// (within 4 ulp of log(N); tests/test_uct_screen.py bounds the screen with that
+// input error), the integer-key maximum and a v_sqrt_f32 band (the band is
+// 8E, four times the 2E the argument needs, so its own rounding is immaterial).
+template <int Lanes, bool TwoSlots>
+__device__ __forceinline__ int uct_argmax_screen_lf(const Node<int32_t>& c0, bool in0,
+                                                    const Node<int32_t>& c1, bool in1, int cp,
+                                                    float lf, double uct_c) {
+  const float cf = static_cast<float>(uct_c);
+  const float a0 = uct_screen_value(c0, in0, cp, lf, cf);
+  const float a1 = TwoSlots ? uct_screen_value(c1, in1, cp, lf, cf) : -__builtin_huge_valf();
+  const int32_t k0 = f32_key(a0), k1 = f32_key(a1);
+  const int32_t mk = wave_max_key<Lanes>(TwoSlots ? max(k0, k1) : k0);
+  const uint64_t t0 = ballot(k0 == mk);
+  const int j = t0 ? static_cast<int>(ctz64(t0)) : 64 + static_cast<int>(ctz64(ballot(k1 == mk)));
+  const bool hi = TwoSlots && j >= 64;  // wave-uniform
+  const int src = j & 63;
+  const int32_t nj = rli(hi ? c1.n : c0.n, src), wj = rli(hi ? c1.w : c0.w, src);
+  const int32_t oj = rli(static_cast<int32_t>(hi ? c1.out : c0.out), src);
+  const float e2 = (1.0f + fabsf(cf) * __builtin_amdgcn_sqrtf(lf)) * 0x1p-17f;  // 2E', lf >= 0
+  const float lo = key_f32(mk) - e2;
+  const bool same0 = c0.n == nj && c0.w == wj && static_cast<int32_t>(c0.out) == oj;
+  bool near = in0 && a0 >= lo && !same0;
+  if (TwoSlots) {
+    const bool same1 = c1.n == nj && c1.w == wj && static_cast<int32_t>(c1.out) == oj;
+    near = near || (in1 && a1 >= lo && !same1);
+  }
+  return ballot(near) ? -1 : j;
+}
+// log(n) in f32 for the screen: v_log_f32 (log2, 1 ulp) times ln 2.
+__device__ __forceinline__ float screen_log(int32_t n) {
+  return __builtin_amdgcn_logf(static_cast<float>(n)) * 0x1.62e430p-1f;
+}
+
 // Games whose rollout draws use WaveMt::uniform_small (|LegalActions| <= 7,
 // C++ policy): the evaluator stream then needs use7 = 1.
 template <class G>
@@ -1406,8 +1477,8 @@ struct WaveApply<ConnectFour> {
     put(s.bb, p, mine);
     s.moves++;
     if (mv & ConnectFour::kTopRow) s.legal &= ~(1u << col);
-    const int j = lane_id() & 3;
-    const uint32_t d = j == 0 ? 1u : (j == 1 ? 7u : (j == 2 ? 6u : 8u));
+    // shift 1, 7, 6, 8 for lane & 3 (one byte extract, no exec-mask branch)
+    const uint32_t d = (0x08060701u >> (8 * (lane_id() & 3))) & 0xFFu;
     const uint64_t m = mine & (mine >> d);
     if (ballot((m & (m >> (2 * d))) != 0)) s.outcome = p;
     else if (s.moves == 42) s.outcome = 2;
@@ -1522,6 +1593,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
   double rlg0 = 0.0, rlg1 = 0.0;
   int root_k = 0;
   constexpr bool kLP = OS_LANE_PATH && LanePathGame<G>::value;
+  // cur_logN is then only read on the screen's fallback, loaded there.
+  constexpr bool kLazyLog = OS_SCREEN_LOG && OS_UCT_SCREEN && sizeof(R) == 4 && !kPuct &&
+                            (OS_UCT_SCREEN == 2 || !WW::kTwoSlots);
   LanePath<R> lp;
   if (kLP && path_cap > 64) path_cap = 64;
 
@@ -1689,10 +1763,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           const Node<R>* src = nc_.block(cur_first, cur_nc) ? nc_.c : nodes;
           if (nc_.block(cur_first, cur_nc)) c0 = load_node(nc_.c + cur_first + (in0 ? l : 0));
           else c0 = load_node(nodes + cur_first + (in0 ? l : 0));
-          lg0 = sp.log_lut[c0.n];
+          if (!kLazyLog) lg0 = sp.log_lut[c0.n];
           if (in1) {
             c1 = load_node(src + cur_first + l + 64);
-            lg1 = sp.log_lut[c1.n];
+            if (!kLazyLog) lg1 = sp.log_lut[c1.n];
           }
         }
         if constexpr (kPuct) {
@@ -1716,12 +1790,17 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         } else {
           chosen = -1;
 #if OS_UCT_SCREEN
-          if constexpr (sizeof(R) == 4 && (OS_UCT_SCREEN == 2 || !WW::kTwoSlots))
+          if constexpr (kLazyLog)
+            chosen = uct_argmax_screen_lf<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
+                                                                     screen_log(cur_n), sp.uct_c);
+          else if constexpr (sizeof(R) == 4 && (OS_UCT_SCREEN == 2 || !WW::kTwoSlots))
             chosen = uct_argmax_screen<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
                                                                   cur_logN, sp.uct_c);
 #endif
         }
         }
+        if (kLazyLog && chosen < 0)  // the exact log(N) for the f64 scan
+          cur_logN = depth == 0 ? root_logN : sp.log_lut[cur_n];
         if (!kPuct && chosen < 0) {
           const double v0 = uct_value_sel(c0, in0, cp, cur_logN, sp.uct_c);
           const double v1 = WW::kTwoSlots ? uct_value_sel(c1, in1, cp, cur_logN, sp.uct_c) : -inf;
@@ -1741,7 +1820,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         } else {
           c_w = static_cast<R>(rld(static_cast<double>(bc.w), src));
         }
-        cur_logN = rld(hi ? lg1 : lg0, src);
+        if (!kLazyLog) cur_logN = rld(hi ? lg1 : lg0, src);
       }
 #if OS_WAVE_APPLY
       WaveApply<G>::apply(s, g, ctx, static_cast<int>(c_action));

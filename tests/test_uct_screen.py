@@ -23,10 +23,10 @@ def _ulp_nudge(x, k):
   return x
 
 
-def _screen_values(n, w, log_n, c, rcp_ulp, sqrt_ulp):
+def _screen_values(n, w, log_n, c, rcp_ulp, sqrt_ulp, log_ulp=0):
   r = _ulp_nudge(F(1.0) / n.astype(F), rcp_ulp)
   q = (w.astype(F) * r).astype(F)
-  t = (F(log_n) * r).astype(F)
+  t = (_ulp_nudge(F(log_n), log_ulp) * r).astype(F)
   s = _ulp_nudge(np.sqrt(t).astype(F), sqrt_ulp)
   return (q + (F(c) * s).astype(F)).astype(F)
 
@@ -45,8 +45,46 @@ def test_f32_screen_within_bound(c, parent):
   e = (1.0 + abs(c) * np.sqrt(max(log_n, 0.0))) * 2.0 ** -20
   for ru in (-1, 0, 1):
     for su in (-1, 0, 1):
-      a = _screen_values(n, w, log_n, c, ru, su).astype(np.float64)
-      assert np.max(np.abs(a - v)) <= e
+      # log(N) as rounded from the f64 table (0), or from v_log_f32 * ln 2
+      # (OS_SCREEN_LOG: within 4 ulp, see test_log_f32_within_4_ulp)
+      for lu in ((-4, 0, 4) if parent > 1 else (0,)):  # log2(1) = 0 exactly
+        a = _screen_values(n, w, log_n, c, ru, su, lu).astype(np.float64)
+        assert np.max(np.abs(a - v)) <= e
+
+
+def _log_f32_model(n, log2_ulp, prod_round=True):
+  """v_log_f32 (log2 within 1 ulp) times ln 2 rounded to f32."""
+  l2 = _ulp_nudge(np.log2(n.astype(np.float64)).astype(F), log2_ulp)
+  return (l2 * F(float.fromhex("0x1.62e430p-1"))).astype(F)
+
+
+@pytest.mark.gpu
+def test_device_log2_f32_within_model():
+  # v_log_f32 on the device (torch.log2 of f32 lowers to it for normal inputs)
+  # is within 1 ulp of log2 and exact at 1; with the ln 2 product, within 4 ulp
+  # of log(N) -- the input error test_f32_screen_within_bound allows.
+  import torch
+  n = torch.arange(1, 1 << 20, dtype=torch.float32, device="cuda")
+  l2 = torch.log2(n).cpu().numpy()
+  nn = np.arange(1, 1 << 20, dtype=np.int64)
+  exact2 = np.log2(nn.astype(np.float64))
+  assert l2[0] == 0.0
+  ulp2 = np.spacing(np.maximum(exact2, 1.0).astype(F)).astype(np.float64)
+  assert np.max(np.abs(l2.astype(np.float64) - exact2) / ulp2) <= 1.0
+  got = (l2 * F(float.fromhex("0x1.62e430p-1"))).astype(np.float64)[1:]
+  exact = np.log(nn[1:].astype(np.float64))
+  assert np.max(np.abs(got - exact) / np.spacing(exact.astype(F)).astype(np.float64)) <= 4.0
+
+
+def test_log_f32_within_4_ulp():
+  # The screen's log(N) under OS_SCREEN_LOG: 1 ulp of v_log_f32, the f32 ln 2
+  # constant and the product's rounding stay within 4 ulp of log(N).
+  n = np.arange(2, 1 << 20, dtype=np.int64)
+  exact = np.log(n.astype(np.float64))
+  for u in (-1, 0, 1):
+    got = _log_f32_model(n, u).astype(np.float64)
+    ulp = np.spacing(exact.astype(F)).astype(np.float64)
+    assert np.max(np.abs(got - exact) / ulp) <= 4.0
 
 
 def test_identical_children_give_identical_f32_values():
