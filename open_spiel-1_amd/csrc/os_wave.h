@@ -274,9 +274,13 @@ struct WaveMt {
   // The pair (cur, nxt) of every lane is read once per window, so
   // uniform_lanes() needs no cross-lane shuffle per draw (small7() reads the
   // pairs once per window and shuffles instead).
+  // Every lane reads (lanes past the block re-read its last word) and selects,
+  // so the LDS reads need no exec-mask branch.
   __device__ void load_window(int i) {
-    cur = i < kMtN ? MtStream::temper(s[i]) : 0u;
-    nxt = !use7 && i + 1 < kMtN ? MtStream::temper(s[i + 1]) : 0u;
+    const uint32_t w0 = MtStream::temper(s[i < kMtN ? i : kMtN - 1]);
+    const uint32_t w1 = MtStream::temper(s[i + 1 < kMtN ? i + 1 : kMtN - 1]);
+    cur = i < kMtN ? w0 : 0u;
+    nxt = !use7 && i + 1 < kMtN ? w1 : 0u;
   }
   __device__ int export_pos() const { return base >= kMtN ? kMtN : base + pos; }
 
@@ -289,17 +293,15 @@ struct WaveMt {
     const uint64_t t0 = OS_PH_NOW();
 #endif
     for (int c = 0; c < kMtN; c += 64) {
-      const int i = c + l;
-      uint32_t v = 0;
-      const bool act = i < kMtN;
-      if (act) {
-        const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
-        const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
-        const uint32_t y = (s[i] & 0x80000000u) | (s[i1] & 0x7fffffffu);
-        v = s[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
+      // Lanes past the block (last chunk only) compute on a clamped index and
+      // do not store: no exec-mask branch around the reads.
+      const int i = c + l < kMtN ? c + l : kMtN - 1;
+      const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+      const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+      const uint32_t y = (s[i] & 0x80000000u) | (s[i1] & 0x7fffffffu);
+      const uint32_t v = s[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
       __builtin_amdgcn_wave_barrier();
-      if (act) s[i] = v;
+      if (c + 64 <= kMtN || c + l < kMtN) s[i] = v;  // wave-uniform except the last chunk
       __builtin_amdgcn_wave_barrier();
     }
 #if OS_PHASE_TIMING
@@ -938,7 +940,10 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
     const uint32_t c = static_cast<uint32_t>(l & 7);
     const uint64_t occ = s.bb[0] | s.bb[1];
     const bool col = c < 7;
-    const uint32_t hc = col ? popc64((occ >> (7 * c)) & 0x3full) : 0u;
+    // every lane counts (lane 7 reads the unused bits above column 6); the
+    // select keeps the count free of an exec-mask branch
+    const uint32_t hc0 = popc64((occ >> (7 * c)) & 0x3full);
+    const uint32_t hc = col ? hc0 : 0u;
     const bool lgl = col && ((s.legal >> c) & 1u);
     const uint32_t rank = static_cast<uint32_t>(__builtin_popcount(s.legal & ((1u << c) - 1u)));
     heights = rl32(row_scan_add(hc << (4 * c)), 7);
