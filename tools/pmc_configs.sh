@@ -15,5 +15,20 @@ for c in $CFGS; do
     bash "$R/tools/pmc.sh" "$P1" "$P2" FETCH_SIZE WRITE_SIZE || exit 1
   rm -rf "$R/gpurun_out/pmc_$c"
   mv "$R/gpurun_out/pmc" "$R/gpurun_out/pmc_$c"
+  if [ -n "$PMC_SUMMARY" ]; then
+    # Summarise on the box and keep only the counter CSVs (the traces of the
+    # many-launch configs would exceed what gpurun copies back).
+    case $c in
+      c2|c3|c4) K=k_wsearch ;; c5) K=k_rollouts ;; sp) K=k_wselfplay ;;
+      az) K=k_az_step ;; g9) K=k_lsearch ;;
+    esac
+    case $c in
+      c2|sp|az) G=connect_four ;; c3) G=breakthrough ;; c4) G=hex ;; c5|g9) G=go ;;
+    esac
+    python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/pmc_$c" $K $G \
+      "$R/gpurun_out/pmc_rec_$c.json" > /dev/null || exit 1
+    find "$R/gpurun_out/pmc_$c" -type f ! -name "run_counter_collection.csv" ! -name "*.log" -delete
+    gzip -f "$R/gpurun_out/pmc_$c"/p*/run_counter_collection.csv
+  fi
   echo "pmc $c done"
 done
