@@ -1628,6 +1628,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     bot.uniformize();
 #endif
     // ---- selection / expansion ----
+    bool pending_expand = false;
     for (;;) {
 #if OS_UNI_SEL == 1
       s = make_uniform(s);
@@ -1640,12 +1641,130 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       depth = __builtin_amdgcn_readfirstlane(depth);
 #endif
       if (G::terminal(s, g) || cur_n <= 0) break;
+      // The node to expand ends the descent (its first child is fresh): the
+      // expansion runs after the loop, so the per-level loop carries only
+      // the selection (no merge of the two paths' values every level).
+      if (cur_nc == 0) {
+        pending_expand = true;
+        break;
+      }
       int chosen;
       uint32_t c_action, c_first;
       int32_t c_n;
       int c_nc;
       R c_w;
-      if (cur_nc == 0) {
+      // Lane k scores child k (and k + 64); each lane also fetches
+      // log(n) of its own child, which is log(N_parent) one level down if
+      // that child is chosen, so the next level needs no dependent load.
+      const int cp = P0 ^ (depth & 1);
+      c_scanned.add(cur_nc);
+      Node<R> c0 = zero_node, c1 = zero_node;
+      double lg0 = 0.0, lg1 = 0.0;
+      const bool in0 = l < cur_nc, in1 = WW::kTwoSlots && l + 64 < cur_nc;
+      if (depth == 0) {  // root children: register-resident, no loads
+        // Lanes past the last child hold zero_node in the mirror (every
+        // write to it keeps that), so no exec mask is needed here.
+        c0 = rc0;
+        lg0 = rlg0;
+        if (in1) {
+          c1 = rc1;
+          lg1 = rlg1;
+        }
+      } else {
+        // Every lane loads (lanes past the last child re-read child 0, so
+        // no exec-mask branch); their values are masked by in0 / in1.
+        // A block of the cached top levels comes from LDS (wave-uniform).
+        const Node<R>* src = nc_.block(cur_first, cur_nc) ? nc_.c : nodes;
+        if (nc_.block(cur_first, cur_nc)) c0 = load_node(nc_.c + cur_first + (in0 ? l : 0));
+        else c0 = load_node(nodes + cur_first + (in0 ? l : 0));
+        if (!kLazyLog) lg0 = sp.log_lut[c0.n];
+        if (in1) {
+          c1 = load_node(src + cur_first + l + 64);
+          if (!kLazyLog) lg1 = sp.log_lut[c1.n];
+        }
+      }
+      if constexpr (kPuct) {
+        // PUCTValue (mcts.cc:102-111): unvisited children are not +inf, so
+        // every child is scored in f64 (cur_logN holds sqrt(N) here).
+        const double cprior = puct_prior_term(sp.uct_c, cur_nc);
+        const double v0 = puct_value_sel(c0, in0, cp, cur_logN, cprior);
+        const double v1 =
+            WW::kTwoSlots ? puct_value_sel(c1, in1, cp, cur_logN, cprior) : -inf;
+        chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
+      } else {
+      // An unvisited unsolved child scores +inf, above every finite UCT
+      // value and solver outcome, so the first one in index order wins the
+      // strict '>' scan outright: one ballot instead of the f64 UCT values
+      // and the wave max.
+      const uint64_t f0 = ballot(in0 && c0.out == kUnsolved && c0.n == 0);
+      const uint64_t f1 =
+          WW::kTwoSlots ? ballot(in1 && c1.out == kUnsolved && c1.n == 0) : 0ull;
+      if (f0 | f1) {
+        chosen = f0 ? ctz64(f0) : 64 + ctz64(f1);
+      } else {
+        chosen = -1;
+#if OS_UCT_SCREEN
+        if constexpr (kLazyLog)
+          chosen = uct_argmax_screen_lf<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
+                                                                   screen_log(cur_n), sp.uct_c);
+        else if constexpr (sizeof(R) == 4 && (OS_UCT_SCREEN == 2 || !WW::kTwoSlots))
+          chosen = uct_argmax_screen<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
+                                                                cur_logN, sp.uct_c);
+#endif
+      }
+      }
+      if (kLazyLog && chosen < 0)  // the exact log(N) for the f64 scan
+        cur_logN = depth == 0 ? root_logN : sp.log_lut[cur_n];
+      if (!kPuct && chosen < 0) {
+        const double v0 = uct_value_sel(c0, in0, cp, cur_logN, sp.uct_c);
+        const double v1 = WW::kTwoSlots ? uct_value_sel(c1, in1, cp, cur_logN, sp.uct_c) : -inf;
+        chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
+      }
+      if (depth == 0) root_k = chosen;
+      const int src = chosen & 63;
+      const bool hi = WW::kTwoSlots && chosen >= 64;  // wave-uniform
+      const Node<R> bc = hi ? c1 : c0;
+      c_action = rl32(bc.action, src);
+      c_first = rl32(bc.first, src);
+      c_n = rli(bc.n, src);
+      c_nc = rli(bc.nchild, src);
+      if (sizeof(R) == 4) {
+        const int32_t wi = rli(static_cast<int32_t>(bc.w), src);
+        c_w = static_cast<R>(wi);
+      } else {
+        c_w = static_cast<R>(rld(static_cast<double>(bc.w), src));
+      }
+      if (!kLazyLog) cur_logN = rld(hi ? lg1 : lg0, src);
+#if OS_WAVE_APPLY
+      WaveApply<G>::apply(s, g, ctx, static_cast<int>(c_action));
+#else
+      G::apply(s, g, ctx, static_cast<int>(c_action));
+#endif
+      if (++depth >= path_cap) {
+        res.status = kPathOverflow;
+        goto done;
+      }
+      cur_idx = cur_first + chosen;
+      cur_first = c_first;
+      cur_n = c_n;
+      cur_nc = c_nc;
+      if constexpr (kLP) {
+        lp.set(depth, cur_idx, c_first, c_n, c_nc, c_w);
+      } else if (l == 0) {
+        PathEnt<R>& pe = path[depth];
+        pe.idx = cur_idx;
+        pe.first = c_first;
+        pe.n = c_n;
+        pe.nc = c_nc;
+        pe.w = c_w;
+      }
+    }
+    if (pending_expand) {
+      int chosen;
+      uint32_t c_action, c_first;
+      int32_t c_n;
+      int c_nc;
+      R c_w;
         const uint64_t t_ex = OS_PH_NOW();
         const typename G::Legal lg = G::legal(s, g, ctx);
         const int nc = lg.count;
@@ -1743,90 +1862,6 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         c_nc = 0;
         c_w = 0;
         OS_PH_ADD(ph.c[kPhExpand], t_ex);
-      } else {
-        // Lane k scores child k (and k + 64); each lane also fetches
-        // log(n) of its own child, which is log(N_parent) one level down if
-        // that child is chosen, so the next level needs no dependent load.
-        const int cp = P0 ^ (depth & 1);
-        c_scanned.add(cur_nc);
-        Node<R> c0 = zero_node, c1 = zero_node;
-        double lg0 = 0.0, lg1 = 0.0;
-        const bool in0 = l < cur_nc, in1 = WW::kTwoSlots && l + 64 < cur_nc;
-        if (depth == 0) {  // root children: register-resident, no loads
-          // Lanes past the last child hold zero_node in the mirror (every
-          // write to it keeps that), so no exec mask is needed here.
-          c0 = rc0;
-          lg0 = rlg0;
-          if (in1) {
-            c1 = rc1;
-            lg1 = rlg1;
-          }
-        } else {
-          // Every lane loads (lanes past the last child re-read child 0, so
-          // no exec-mask branch); their values are masked by in0 / in1.
-          // A block of the cached top levels comes from LDS (wave-uniform).
-          const Node<R>* src = nc_.block(cur_first, cur_nc) ? nc_.c : nodes;
-          if (nc_.block(cur_first, cur_nc)) c0 = load_node(nc_.c + cur_first + (in0 ? l : 0));
-          else c0 = load_node(nodes + cur_first + (in0 ? l : 0));
-          if (!kLazyLog) lg0 = sp.log_lut[c0.n];
-          if (in1) {
-            c1 = load_node(src + cur_first + l + 64);
-            if (!kLazyLog) lg1 = sp.log_lut[c1.n];
-          }
-        }
-        if constexpr (kPuct) {
-          // PUCTValue (mcts.cc:102-111): unvisited children are not +inf, so
-          // every child is scored in f64 (cur_logN holds sqrt(N) here).
-          const double cprior = puct_prior_term(sp.uct_c, cur_nc);
-          const double v0 = puct_value_sel(c0, in0, cp, cur_logN, cprior);
-          const double v1 =
-              WW::kTwoSlots ? puct_value_sel(c1, in1, cp, cur_logN, cprior) : -inf;
-          chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
-        } else {
-        // An unvisited unsolved child scores +inf, above every finite UCT
-        // value and solver outcome, so the first one in index order wins the
-        // strict '>' scan outright: one ballot instead of the f64 UCT values
-        // and the wave max.
-        const uint64_t f0 = ballot(in0 && c0.out == kUnsolved && c0.n == 0);
-        const uint64_t f1 =
-            WW::kTwoSlots ? ballot(in1 && c1.out == kUnsolved && c1.n == 0) : 0ull;
-        if (f0 | f1) {
-          chosen = f0 ? ctz64(f0) : 64 + ctz64(f1);
-        } else {
-          chosen = -1;
-#if OS_UCT_SCREEN
-          if constexpr (kLazyLog)
-            chosen = uct_argmax_screen_lf<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
-                                                                     screen_log(cur_n), sp.uct_c);
-          else if constexpr (sizeof(R) == 4 && (OS_UCT_SCREEN == 2 || !WW::kTwoSlots))
-            chosen = uct_argmax_screen<WW::kLanes, WW::kTwoSlots>(c0, in0, c1, in1, cp,
-                                                                  cur_logN, sp.uct_c);
-#endif
-        }
-        }
-        if (kLazyLog && chosen < 0)  // the exact log(N) for the f64 scan
-          cur_logN = depth == 0 ? root_logN : sp.log_lut[cur_n];
-        if (!kPuct && chosen < 0) {
-          const double v0 = uct_value_sel(c0, in0, cp, cur_logN, sp.uct_c);
-          const double v1 = WW::kTwoSlots ? uct_value_sel(c1, in1, cp, cur_logN, sp.uct_c) : -inf;
-          chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
-        }
-        if (depth == 0) root_k = chosen;
-        const int src = chosen & 63;
-        const bool hi = WW::kTwoSlots && chosen >= 64;  // wave-uniform
-        const Node<R> bc = hi ? c1 : c0;
-        c_action = rl32(bc.action, src);
-        c_first = rl32(bc.first, src);
-        c_n = rli(bc.n, src);
-        c_nc = rli(bc.nchild, src);
-        if (sizeof(R) == 4) {
-          const int32_t wi = rli(static_cast<int32_t>(bc.w), src);
-          c_w = static_cast<R>(wi);
-        } else {
-          c_w = static_cast<R>(rld(static_cast<double>(bc.w), src));
-        }
-        if (!kLazyLog) cur_logN = rld(hi ? lg1 : lg0, src);
-      }
 #if OS_WAVE_APPLY
       WaveApply<G>::apply(s, g, ctx, static_cast<int>(c_action));
 #else
