@@ -5,6 +5,7 @@
 #   tools/pmc_configs.sh [configs...]        (default: c2 c4)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 CFGS=${*:-c2 c4}
+PMC_SUMMARY=${PMC_SUMMARY-1}  # summarise on the box (traces of many-launch configs exceed the copy-back)
 P1="SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
 P2="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD"
 for c in $CFGS; do
