@@ -715,7 +715,10 @@ def bench_az(args, ctx, layout):
                         "units_per_launch": requests / max(launches, 1)})
   line["az"] = {"launches_per_step": launches, "requests_per_step": requests,
                 "k_az_step_ms_total": step_ms,
-                "k_az_step_share_of_step": step_ms / (elapsed / max(args.steps, 1) * 1e3)}
+                "k_az_step_share_of_step": step_ms / (elapsed / max(args.steps, 1) * 1e3),
+                # the search alone (k_az_step time, no network): the figure
+                # comparable with cpu_baseline, whose evaluator is free
+                "search_only_sims_per_s": sims_step / max(step_ms * 1e-3, 1e-12)}
   line["roofline"] = _roofline("k_az_step", game, alg / max(launches, 1), kernel_ms,
                                requests / max(launches, 1), "request")
   cpu = None
