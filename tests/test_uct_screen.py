@@ -95,3 +95,27 @@ def test_identical_children_give_identical_f32_values():
   w = np.array([2, 2, 2], np.int64)
   a = _screen_values(n, w, np.log(40.0), 2.0, 0, 0)
   assert a[0] == a[1] == a[2]
+
+
+def _f32_key(a):
+  """csrc/os_wave.h f32_key: b ^ ((b >> 31) & 0x7FFFFFFF) on the int32 bits."""
+  b = np.asarray(a, F).view(np.int32)
+  return b ^ ((b >> 31) & np.int32(0x7FFFFFFF))
+
+
+def test_f32_key_orders_like_floats_and_decodes():
+  # The screen's integer-key wave maximum (OS_SCREEN_LOG) relies on the key
+  # being strictly monotone in the float value (non-NaN, -0 below +0) and on
+  # the same map decoding it (key_f32).
+  rng = np.random.default_rng(7)
+  vals = np.concatenate([
+      rng.standard_normal(20000).astype(F) * F(100),
+      np.array([-np.inf, np.inf, 0.0, -0.0, 1e-45, -1e-45, 3.4e38, -3.4e38, 1.0, -1.0], F),
+      (rng.random(2000).astype(F) - F(0.5)) * F(1e-38)])
+  keys = _f32_key(vals)
+  order_f = np.argsort(vals, kind="stable")
+  sv, sk = vals[order_f], keys[order_f]
+  neq = sv[1:] != sv[:-1]  # equal floats: only -0 / +0 here, whose keys differ
+  assert np.all((np.diff(sk.astype(np.int64)) > 0)[neq])           # strictly monotone
+  assert _f32_key(F(-0.0)) < _f32_key(F(0.0))
+  assert _f32_key(keys.view(F)).view(np.int32).tolist() == vals.view(np.int32).tolist()
