@@ -88,6 +88,10 @@ def parse():
   ap.add_argument("--cpu-seconds", type=float, default=12.0,
                   help="target CPU-baseline sample duration")
   ap.add_argument("--parity-roots", type=int, default=32)
+  ap.add_argument("--no-parity-sweep", dest="parity_sweep", action="store_false",
+                  help="c2: skip the bit-exact sweep over the other kernels (C3/C4/C5 "
+                       "shapes, go lane layout, PUCT, numpy policy, chance nodes), run "
+                       "after the timed region")
   ap.add_argument("--az-graph", type=int, default=1,
                   help="az: replay each evaluator round as one captured HIP graph (1) "
                        "or launch it op by op (0)")
@@ -333,6 +337,7 @@ def bench_search(args, ctx, layout):
   stats = eng.stats()
 
   parity = None
+  ref = None
   if ctx.rank == 0 and args.parity_roots > 0:
     og = _oracle(game)
     pr = min(args.parity_roots, R)
@@ -343,10 +348,17 @@ def bench_search(args, ctx, layout):
 
   elapsed, kernel_ms = ctx.timed(lambda: eng.run_async(handle), args.steps)
   total_sims = ctx.total(sims_per_step * args.steps)
-  eng.fetch()
+  out_timed = eng.fetch()  # the last TIMED run's results
   arena = eng.arena_info()
   if arena["reruns"] != arena0["reruns"] or eng.last_sims() != sims_per_step:
     raise RuntimeError("a timed run overflowed the page pool: %r" % (arena,))
+  if ref is not None:
+    bad = [k for k in E.OUTPUT_KEYS if not np.array_equal(out_timed[k][:pr], ref[k])]
+    parity["timed_run_bit_exact"] = not bad
+    parity["timed_run_mismatch_fields"] = bad
+  sweep = None
+  if (ctx.rank == 0 and args.config == "c2" and args.parity_sweep and not ctx.rehearse):
+    sweep = parity_sweep(ctx)
 
   cpu = None
   if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
@@ -370,6 +382,8 @@ def bench_search(args, ctx, layout):
   line["roofline"] = _roofline(kern, game, alg_bytes, kernel_ms, sims_per_step, "sim")
   line["cpu_baseline"] = cpu
   line["parity"] = parity
+  if sweep is not None:
+    line["parity_sweep"] = sweep
   line["tree_stats"] = stats
   line["arena"] = dict(arena, mode=arena_mode)
   return line
@@ -392,9 +406,8 @@ def bench_root_parallel(args, ctx, layout):
 
   def step():
     v, w = be.run_root_parallel()
-    if ctx.world > 1:
-      ctx.dist.all_reduce(v)
-      ctx.dist.all_reduce(w)
+    if ctx.world > 1:  # one f64[2A] message (os_amd/dist.py)
+      v, w = D._all_reduce_root_sums(v, w, None)
     return v, w
 
   be.eng.set_arena_mode("reserved" if args.arena == "reserved" else "paged")
@@ -456,9 +469,9 @@ def bench_root_parallel(args, ctx, layout):
                         "workload": "%s initial position, %d trees x %d sims per GPU, "
                                     "action-indexed root visits all-reduced" % (game, T, sims),
                         "game": game, "trees_per_gpu": T, "sims_per_tree": sims,
-                        "parallelism": "root-parallel x%d (RCCL all_reduce int64[%d] + "
-                                       "f64[%d] per step)" % (ctx.world, be.num_actions,
-                                                              be.num_actions),
+                        "parallelism": "root-parallel x%d (one RCCL all_reduce of "
+                                       "f64[%d] = visits + rewards per step)"
+                                       % (ctx.world, 2 * be.num_actions),
                         "layout": lay, "sims_per_step_per_gpu": sims_per_step})
   line["roofline"] = _roofline(KERNEL[lay], game, alg_bytes, kernel_ms, sims_per_step, "sim")
   line["arena"] = dict(arena, mode=arena_mode)
@@ -728,6 +741,180 @@ def bench_az(args, ctx, layout):
   line["parity"] = parity
   line["tree_stats"] = st
   return line
+
+
+# ---------------------------------------------------------------------------
+# parity sweep: every kernel of the library, bit-exact against the oracle
+def parity_sweep(ctx):
+  """Runs after the C2 timed region on rank 0 (never timed): one reduced-size
+  case per kernel / layout / policy the library ships, each compared
+  bit-exactly with the oracle (mcts.cc:325-428 searches,
+  :42-71 playouts).  The sizes keep the whole sweep to seconds, while the
+  launches keep each config's full width where that is what a kernel's
+  indexing depends on (C3's 65536 searches on the paged arena, C4's 8192
+  trees, C5's 2^20 playouts).  Returns {case: {...,"bit_exact": bool}} plus
+  "all_bit_exact"."""
+  from os_amd import _lib
+  from os_amd import engine as E
+  torch = ctx.torch
+  res = {}
+  t_start = time.perf_counter()
+
+  def cmp(got, ref, keys=E.OUTPUT_KEYS, rows=None):
+    sel = (lambda a: a) if rows is None else (lambda a: a[rows])
+    return [k for k in keys if not np.array_equal(sel(got[k]), ref[k])]
+
+  def case(name, fn):
+    t0 = time.perf_counter()
+    try:
+      r = fn()
+    except Exception as e:  # a failing case is reported, not hidden
+      r = {"bit_exact": False, "error": "%s: %s" % (type(e).__name__, e)}
+    r["seconds"] = round(time.perf_counter() - t0, 3)
+    res[name] = r
+
+  def seeds(R, mul=1, add=0):
+    b = np.arange(R, dtype=np.uint32) * np.uint32(mul) + np.uint32(add)
+    return b, b + np.uint32(EVAL_OFFSET)
+
+  def c3():
+    # C3 shape: 65536 breakthrough 8x8 roots on the paged arena (the pool
+    # sized by a first reserved run), 256 sims (a page must fit twice in the
+    # worst-case reservation for paging to apply); first and last 64 roots.
+    gs, R, sims = "breakthrough(rows=8,columns=8)", 65536, 256
+    acts, offs = E.make_roots(gs, R, seed_base=1000, max_plies=6)
+    bs, es = seeds(R)
+    eng = E.Engine(gs, device=ctx.local)
+    kw = dict(uct_c=2.0, max_simulations=sims)
+    eng.set_arena_mode("paged")
+    eng.prepare(acts, offs, bs, es, **kw)
+    eng.run_async(ctx.handle)
+    eng.fetch()
+    eng.prepare(acts, offs, bs, es, **kw)
+    eng.run_async(ctx.handle)
+    got = eng.fetch()
+    info = eng.arena_info()
+    og = _oracle(gs)
+    rows = np.r_[0:64, R - 64:R]
+    sub_offs = np.concatenate([offs[:65], offs[R - 63:R + 1] - offs[R - 64] + offs[64]])
+    sub_acts = np.concatenate([acts[:offs[64]], acts[offs[R - 64]:offs[R]]])
+    ref = og.mcts_batch(sub_acts, sub_offs, bs[rows], es[rows], max_children=eng.max_children,
+                        threads=host_cores()[0], **kw)
+    bad = cmp(got, ref, rows=rows)
+    eng.close()
+    return {"roots": R, "sims": sims, "roots_checked": 128, "paged": bool(info["paged"]),
+            "reruns": info["reruns"], "bit_exact": not bad and bool(info["paged"]),
+            "mismatch_fields": bad}
+
+  def c4():
+    # C4 shape: 8192 hex-11 trees on the initial position (paged), 256 sims;
+    # device action-indexed root sums vs the fetched children, 16-tree prefix.
+    gs, T, sims = "hex(board_size=11)", 8192, 256
+    eng = E.Engine(gs, device=ctx.local)
+    A = eng.num_distinct_actions
+    bs, es = seeds(T)
+    acts, offs = np.zeros(0, np.int64), np.zeros(T + 1, np.int64)
+    kw = dict(uct_c=2.0, max_simulations=sims)
+    eng.set_arena_mode("paged")
+    eng.prepare(acts, offs, bs, es, **kw)
+    eng.run_async(ctx.handle)
+    eng.fetch()
+    eng.prepare(acts, offs, bs, es, **kw)
+    eng.run_async(ctx.handle)
+    v = torch.empty(A, dtype=torch.int64, device=ctx.dev)
+    w = torch.empty(A, dtype=torch.float64, device=ctx.dev)
+    eng.root_sums_async(A, v.data_ptr(), w.data_ptr(), ctx.handle)
+    got = eng.fetch()
+    paged = bool(eng.arena_info()["paged"])
+    lv, lw = np.zeros(A, np.int64), np.zeros(A, np.float64)
+    for r in range(T):
+      nc = int(got["nchild"][r])
+      np.add.at(lv, got["child_action"][r, :nc], got["child_n"][r, :nc])
+      np.add.at(lw, got["child_action"][r, :nc], got["child_w"][r, :nc])
+    sums_ok = (np.array_equal(v.cpu().numpy(), lv) and np.array_equal(w.cpu().numpy(), lw))
+    ref = _oracle(gs).mcts_batch(acts, offs[:17], bs[:16], es[:16],
+                                 max_children=eng.max_children, threads=host_cores()[0], **kw)
+    bad = cmp(got, ref, rows=slice(0, 16))
+    eng.close()
+    return {"trees": T, "sims": sims, "trees_checked": 16, "paged": paged,
+            "root_sums_equal_children": bool(sums_ok),
+            "bit_exact": not bad and bool(sums_ok), "mismatch_fields": bad}
+
+  def c5():
+    gs, N = "go(board_size=9)", 1 << 20
+    eng = E.Engine(gs, device=ctx.local)
+    s = np.arange(N, dtype=np.uint32)
+    eng.rollouts_prepare([], s)
+    eng.rollouts_run_async(ctx.handle)
+    c = torch.empty(3, dtype=torch.int64, device=ctx.dev)
+    eng.rollouts_outcomes_async(c.data_ptr(), ctx.handle)
+    ret = eng.rollouts_fetch()
+    pick = np.arange(0, N, N // 4096, dtype=np.int64)[:4096]
+    ref = _oracle(gs).rollouts([], s[pick])
+    r0 = ret[:, 0]
+    counts = [int((r0 > 0).sum()), int((r0 < 0).sum()), int((r0 == 0).sum())]
+    cok = c.cpu().tolist() == counts
+    eng.close()
+    return {"playouts": N, "playouts_checked": 4096, "device_counts_equal_returns": cok,
+            "bit_exact": bool(np.array_equal(ret[pick], ref)) and cok}
+
+  def search(gs, R, sims, plies, layout, seed_mul=1, **kw):
+    def fn():
+      acts, offs = E.make_roots(gs, R, seed_base=4242, max_plies=plies)
+      bs, es = seeds(R, seed_mul, 1)
+      eng = E.Engine(gs, device=ctx.local)
+      got = eng.mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
+                           layout=layout, **kw)
+      puct = kw.pop("child_selection", 0) == _lib.SELECT_PUCT
+      ref = _oracle(gs).mcts_batch(acts, offs, bs, es, uct_c=2.0, max_simulations=sims,
+                                   max_children=eng.max_children, threads=host_cores()[0],
+                                   puct=puct, **kw)
+      bad = cmp(got, ref)
+      eng.close()
+      return {"roots": R, "sims": sims, "bit_exact": not bad, "mismatch_fields": bad}
+    return fn
+
+  def numpy_policy(gs, histories, sims):
+    # python/algorithms/mcts.py semantics: one RandomState shared by the bot
+    # and its evaluator (mcts_test.py:41-54), continued across the search.
+    def fn():
+      eng = E.Engine(gs, device=ctx.local)
+      og = _oracle(gs)
+      bad = []
+      for i, h in enumerate(histories):
+        seed = 17 + i
+        _, key, pos, _, _ = np.random.RandomState(seed).get_state()
+        got, (k2, p2), _ = eng.mcts_stateful(h, (key, pos), None, uct_c=2.0,
+                                             max_simulations=sims, policy=_lib.POLICY_NUMPY)
+        ref = og.mcts_numpy(h, seed, uct_c=2.0, max_simulations=sims)
+        rs = np.random.RandomState()
+        rs.set_state(("MT19937", k2, p2, 0, 0.0))
+        bad += cmp(got, ref)
+        if rs.randint(0, 2 ** 32, dtype=np.uint32) != ref["next_word"][0]:
+          bad.append("random_state_after")
+      eng.close()
+      return {"searches": len(histories), "sims": sims, "bit_exact": not bad,
+              "mismatch_fields": sorted(set(bad))}
+    return fn
+
+  W, L = _lib.LAYOUT_WAVE, _lib.LAYOUT_LANE
+  PUCT = _lib.SELECT_PUCT
+  case("c3_breakthrough_65536_paged", c3)
+  case("c4_hex11_8192_root_sums", c4)
+  case("c5_go9_2^20_playouts", c5)
+  case("go9_lane_layout", search("go(board_size=9)", 72, 160, 8, L))
+  case("go9_wave_layout", search("go(board_size=9)", 8, 96, 8, W))
+  case("tic_tac_toe_wave", search("tic_tac_toe", 64, 1000, 4, W))
+  case("connect_four_lane", search("connect_four", 64, 1024, 8, L))
+  case("puct_connect_four_wave", search("connect_four", 64, 512, 8, W, child_selection=PUCT))
+  case("puct_hex5_lane", search("hex(board_size=5)", 64, 400, 6, L, child_selection=PUCT,
+                                n_rollouts=2, solve=False))
+  case("numpy_policy_connect_four", numpy_policy("connect_four", [[], [3, 3, 2], [0, 6]], 500))
+  case("numpy_policy_go9", numpy_policy("go(board_size=9)", [[], [40]], 120))
+  case("pig_3p_chance", search("pig(players=3)", 64, 300, 6, L))
+  res["all_bit_exact"] = all(v.get("bit_exact") for v in res.values() if isinstance(v, dict))
+  res["seconds"] = round(time.perf_counter() - t_start, 2)
+  return res
 
 
 # ---------------------------------------------------------------------------

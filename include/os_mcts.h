@@ -136,7 +136,9 @@ typedef struct {
   int32_t child_selection;      /* OS_SELECT_UCT (mcts.cc:89-100) or OS_SELECT_PUCT
                                    (mcts.cc:102-111; MCTSBot child_selection_policy,
                                    mcts.h:152-159; mcts.py child_selection_fn) */
-  int32_t reserved;             /* 0 */
+  int32_t reserved;             /* must be 0: every call taking params returns
+                                   OS_ERR_INVALID otherwise, so a binding built
+                                   against a shorter struct fails loudly */
 } os_mcts_params;
 
 /* Batched independent searches: MCTSBot::MCTSearch (mcts.cc:325-428) on every
@@ -423,6 +425,13 @@ int64_t os_make_roots(const os_game* game, int64_t num_roots, uint32_t seed_base
  * (advanced in place); returns the index of the first outcome whose
  * [sum, sum + probs[k]) holds z, or < 0 on error. */
 int32_t os_sample_action(const double* probs, int32_t n, uint32_t* key, int32_t* pos);
+
+/* sizeof of the named ABI struct ("os_mcts_params", "os_game_info",
+ * "os_selfplay_options") as this library was built, or OS_ERR_INVALID for an
+ * unknown name: lets a binding (ctypes, cgo, JNI) check its own layout once at
+ * load time.  No reference counterpart (pybind11 checks types at compile
+ * time, pyspiel.cc:499-524). */
+int64_t os_abi_struct_size(const char* name);
 
 /* Library/kernel build info string (arch, build flags). */
 const char* os_build_info(void);

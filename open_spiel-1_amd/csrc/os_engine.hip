@@ -208,6 +208,11 @@ bool ReplayRoot(const HostGame& g, const int64_t* a, int64_t n, HostState* s,
 
 int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true) {
   if (!p) return Fail(OS_ERR_INVALID, "null params");
+  // A binding built against an older, shorter os_mcts_params leaves whatever
+  // follows its struct here: refuse it instead of reading it as a policy.
+  if (p->reserved != 0)
+    return Fail(OS_ERR_INVALID, "os_mcts_params.reserved must be 0 (struct size mismatch? "
+                                "see os_abi_struct_size)");
   if (p->max_simulations < 0) return Fail(OS_ERR_INVALID, "max_simulations < 0");
   if (p->n_rollouts < 1) return Fail(OS_ERR_INVALID, "n_rollouts must be >= 1");
   if (p->policy != OS_POLICY_CPP && p->policy != OS_POLICY_NUMPY)
@@ -965,6 +970,15 @@ int os_debug_phase_cycles(uint64_t* out, int32_t n) {
   (void)n;
   return Fail(OS_ERR_UNSUPPORTED, "built without -DOS_PHASE_TIMING=1");
 #endif
+}
+
+int64_t os_abi_struct_size(const char* name) {
+  if (!name) return Fail(OS_ERR_INVALID, "null name");
+  const std::string n(name);
+  if (n == "os_mcts_params") return sizeof(os_mcts_params);
+  if (n == "os_game_info") return sizeof(os_game_info);
+  if (n == "os_selfplay_options") return sizeof(os_selfplay_options);
+  return Fail(OS_ERR_INVALID, "unknown ABI struct " + n);
 }
 
 const char* os_build_info(void) {

@@ -306,18 +306,15 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
 // Wave-per-search kernel (default layout): one 64-lane workgroup per search.
 template <class G>
 struct WaveCtxMaker {
-  __device__ static NoCtx make(const DevArgs&, int64_t, uint64_t*) { return NoCtx(); }
+  __device__ static NoCtx make(const DevArgs&, int64_t) { return NoCtx(); }
 };
 template <>
 struct WaveCtxMaker<Go> {
-  __device__ static GoWaveCtx make(const DevArgs& a, int64_t gr, uint64_t* log) {
+  __device__ static GoWaveCtx make(const DevArgs& a, int64_t gr) {
     GoWaveCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
     c.n_base = a.root_nhash[gr];
-    c.log = log;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
     c.init_filters();
     return c;
   }
@@ -333,7 +330,6 @@ template <class G, class R>
 __host__ __device__ constexpr size_t WaveLdsBytes(int path_cap) {
   return static_cast<size_t>(2 * kMtN * 4) + kPageDescLds +
          static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
-         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0) +
          static_cast<size_t>(OS_NODE_CACHE) * sizeof(Node<R>) + 16;
 }
 
@@ -364,14 +360,11 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int l = lane_id();
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
-  // [MT bot | MT evaluator | page descriptor address | path | go log]
+  // [MT bot | MT evaluator | page descriptor address | path | node cache]
   PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4 + kPageDescLds);
-  const size_t glog_off =
-      (2 * kMtN * 4 + kPageDescLds + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7);
-  uint64_t* glog = reinterpret_cast<uint64_t*>(smem + glog_off);
-  // [... | node cache], 16-byte aligned
   Node<R>* lcache = reinterpret_cast<Node<R>*>(
-      smem + ((glog_off + (G::State::kNeedsLog ? kGoLogCap * 8 + 8 : 0) + 15) & ~size_t(15)));
+      smem + ((2 * kMtN * 4 + kPageDescLds + a.path_cap * sizeof(PathEnt<R>) + 15) &
+              ~size_t(15)));
   if (l == 0)
     *reinterpret_cast<uint64_t*>(smem + 2 * kMtN * 4) = reinterpret_cast<uintptr_t>(a.pages);
   const bool shared = Policy == kPolicyNumpy && a.shared_stream;
@@ -397,7 +390,7 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   }
   const typename G::State root =
       make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
-  typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr, glog);
+  typename WaveCtxOf<G>::type ctx = WaveCtxMaker<G>::make(a, gr);
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   PhaseCycles ph = {};  // paged: the root's page is page lr = blockIdx.x
 #if OS_PHASE_TIMING
@@ -462,38 +455,40 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
 
 template <class G>
 struct SpCtx {  // games without a history context
-  __device__ static NoCtx make(const SpArgs&, int64_t, uint64_t*) { return NoCtx(); }
+  __device__ static NoCtx make(const SpArgs&, int64_t) { return NoCtx(); }
   __device__ static void commit(NoCtx&, const SpArgs&, int64_t) {}
 };
 template <>
 struct SpCtx<Go> {
-  __device__ static GoWaveCtx make(const SpArgs& a, int64_t gg, uint64_t* log) {
+  __device__ static GoWaveCtx make(const SpArgs& a, int64_t gg) {
     GoWaveCtx c;
     c.zob = a.zob;
     c.base = a.hist + gg * a.hash_stride;
     c.n_base = a.hist_n[gg];
-    c.log = log;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
     c.init_filters();
     return c;
   }
-  // The move just applied logged its position (go.cc:199-208): append it to
-  // the game history that the next searches treat as "before the root".
+  // The move just applied logged its position (go.cc:199-208): it joins the
+  // game history that the next searches treat as "before the root" (already
+  // in the lanes' slots; stored to the history for the host).
   __device__ static void commit(GoWaveCtx& c, const SpArgs& a, int64_t gg) {
     uint64_t* h = a.hist + gg * a.hash_stride;
-    if (lane_id() == 0)
-      for (int i = 0; i < c.n_log && c.n_base + i < a.hash_stride; ++i) h[c.n_base + i] = c.log[i];
+    const int l = lane_id();
+    const uint64_t sl[4] = {c.s0, c.s1, c.s2, c.s3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 64 * j + l;
+      if (i >= c.n_base && i < c.n && i < a.hash_stride) h[i] = sl[j];
+    }
     __threadfence_block();
-    c.n_base = c.n_base + c.n_log < a.hash_stride ? c.n_base + c.n_log : a.hash_stride;
-    c.init_filters();
+    c.n_base = c.n < a.hash_stride ? c.n : a.hash_stride;
+    c.reset();
   }
 };
 
 template <class G, class R>
 __host__ __device__ constexpr size_t SelfPlayLdsBytes(int path_cap) {
-  return static_cast<size_t>(4 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
-         (G::State::kNeedsLog ? static_cast<size_t>(kGoLogCap) * 8 + 8 : 0);
+  return static_cast<size_t>(4 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>);
 }
 
 // AlphaZero's move choice (alpha_zero.cc:77-95) from the root's children
@@ -547,8 +542,6 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
   PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 4 * kMtN * 4);
-  uint64_t* glog = reinterpret_cast<uint64_t*>(
-      smem + ((4 * kMtN * 4 + a.path_cap * sizeof(PathEnt<R>) + 7) & ~size_t(7)));
   WaveMt b0, b1, ev, act;
   b0.s = mt;
   b1.s = mt + kMtN;
@@ -575,7 +568,7 @@ __global__ __launch_bounds__(64) void k_wselfplay(SpArgs a) {
     if (u < a.cutoff_probability) cutoff = a.cutoff_value;
   }
   typename G::State s = make_uniform(static_cast<const typename G::State*>(a.starts)[gg]);
-  typename WaveCtxOf<G>::type ctx = SpCtx<G>::make(a, gg, glog);
+  typename WaveCtxOf<G>::type ctx = SpCtx<G>::make(a, gg);
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lg * static_cast<int64_t>(a.cap);
   PhaseCycles ph = {};
   SearchResult tot;
@@ -832,18 +825,15 @@ struct RollCtx<Go> {
 
 template <class G>
 struct WaveRollCtx {
-  __device__ static NoCtx make(const RollArgs&, uint64_t*) { return NoCtx(); }
+  __device__ static NoCtx make(const RollArgs&) { return NoCtx(); }
 };
 template <>
 struct WaveRollCtx<Go> {
-  __device__ static GoWaveCtx make(const RollArgs& a, uint64_t* log) {
+  __device__ static GoWaveCtx make(const RollArgs& a) {
     GoWaveCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
-    c.log = log;
-    c.n_log = 0;
-    c.cap = kGoLogCap;
     c.init_filters();
     return c;
   }
@@ -855,14 +845,13 @@ __global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
   const int64_t i = blockIdx.x;
   if (i >= a.n) return;
   __shared__ uint32_t mt[kMtN];
-  __shared__ uint64_t glog[G::State::kNeedsLog ? kGoLogCap : 1];
   WaveMt ev;
   ev.s = mt;
   ev.use7 = SmallAbsl<G>::value ? 1 : 0;
   if (lane_id() == 0) mt_seed(mt, a.seeds[i]);
   __syncthreads();
   ev.init_seeded();
-  typename WaveCtxOf<G>::type ctx = WaveRollCtx<G>::make(a, glog);
+  typename WaveCtxOf<G>::type ctx = WaveRollCtx<G>::make(a);
   const typename G::State root = make_uniform(*static_cast<const typename G::State*>(a.root));
   double s0 = 0.0, s1 = 0.0;
   for (int k = 0; k < a.n_rollouts; ++k) {

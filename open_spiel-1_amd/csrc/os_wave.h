@@ -14,7 +14,10 @@
 //   * backup: lane d updates path node d (mcts.cc:351-357) in one step; the
 //     MCTS-Solver max^n backup (:359-395) walks up serially, each level's
 //     children outcomes read and reduced across lanes;
-//   * go superko: the hash history lives in LDS and is compared 64 at a time.
+//   * go: the superko set lives in the lanes (four entries per lane, one
+//     compare + ballot per move); rollouts keep chain labels on the lanes
+//     (lane l: points l, l + 64), so a chain is one compare + ballot, not a
+//     flood (go_rollout_wave).
 // The semantics are those of os_mcts.h::mcts_search (checked bit-exact
 // against the oracle by tests/test_gpu_parity.py).
 #ifndef OS_WAVE_H_
@@ -442,65 +445,67 @@ struct WaveMt {
   }
 };
 
-// Go superko context for one search per wave: the per-simulation hash log in
-// LDS, compared 64 entries at a time.  Candidates as in GoCtx (os_games.h):
-// only entries logged before the most recent capture can repeat a position.
+// Go superko context for one search per wave (go.cc:199-208).  The whole set
+// -- the positions before the root (base) followed by those logged since --
+// lives in the lanes: entry i in lane i % 64 of slot i / 64, up to kCap
+// entries (a game of n x n <= 11 x 11 logs at most 2 n^2 + 1 <= 243).  A new
+// position is compared with every candidate at once (four 64-bit compares and
+// one ballot).  Candidates: the base, and entries logged before the most recent
+// capture -- without a capture the stone count only grows, so no later
+// position can repeat (the same rule as GoCtx, os_games.h).
 struct GoWaveCtx {
 #if OS_PHASE_TIMING
   uint64_t* sub;  // PhaseCycles::c of the search (go breakdown)
 #endif
+  static constexpr int kCap = 256;
   const uint64_t* zob;
-  const uint64_t* base;   // hashes before the root (global)
+  const uint64_t* base;   // hashes before the root (global), copied into the slots
   int32_t n_base;
-  uint64_t* log;          // LDS
-  int32_t n_log;
-  int32_t cand_end;
-  int32_t cap;
-  Filter256 filt;
-  Filter256 cand_filt;
-  Filter256 base_filt;
+  int32_t n;              // entries held (base included)
+  int32_t cand_end;       // entries [0, cand_end) can repeat a new position
+  uint64_t s0, s1, s2, s3;  // per lane: entries lane, lane + 64, + 128, + 192
 
   __device__ void reset() {
-    n_log = 0;
-    cand_end = 0;
-    filt = base_filt;
-    cand_filt = base_filt;
+    n = n_base;
+    cand_end = n_base;
   }
+  // Copies the base into the slots (every lane loads its four entries).
   __device__ void init_filters() {
-    base_filt.clear();
-    for (int i = 0; i < n_base; ++i) base_filt.add(GoCtx::fbit(base[i]));
+    const int l = lane_id();
+    n_base = n_base < kCap ? n_base : kCap;
+    s0 = l < n_base ? base[l] : 0ull;
+    s1 = l + 64 < n_base ? base[l + 64] : 0ull;
+    s2 = l + 128 < n_base ? base[l + 128] : 0ull;
+    s3 = l + 192 < n_base ? base[l + 192] : 0ull;
     reset();
   }
-  __device__ bool candidate(uint64_t h) const {
-    if (!cand_filt.has(GoCtx::fbit(h))) return false;
-    const int l = lane_id();
-    for (int i = 0; i < n_base; i += 64) {
-      const bool hit = i + l < n_base && base[i + l] == h;
-      if (ballot(hit)) return true;
-    }
-    for (int i = 0; i < cand_end; i += 64) {
-      const bool hit = i + l < cand_end && log[i + l] == h;
-      if (ballot(hit)) return true;
-    }
-    return false;
+  __device__ uint64_t entry(int i) const {
+    const int j = i >> 6, q = i & 63;
+    const uint64_t v = j == 0 ? s0 : (j == 1 ? s1 : (j == 2 ? s2 : s3));
+    return rl64(v, q);
   }
   __device__ bool insert(uint64_t h, bool captured, int stones) {
     (void)stones;
 #if OS_PHASE_TIMING
     const uint64_t t0 = OS_PH_NOW();
 #endif
-    if (captured) {
-      cand_end = n_log;
-      cand_filt = filt;
+    if (captured) cand_end = n;
+    bool dup = false;
+    if (cand_end > 0) {
+      const int l = lane_id();
+      const bool hit = (l < cand_end && s0 == h) | (l + 64 < cand_end && s1 == h) |
+                       (l + 128 < cand_end && s2 == h) | (l + 192 < cand_end && s3 == h);
+      dup = ballot(hit) != 0;
     }
-    const bool dup = candidate(h);
-    if (!dup) {
-      if (n_log < cap) {
-        if (lane_id() == 0) log[n_log] = h;
-        __builtin_amdgcn_wave_barrier();
-        ++n_log;
-      }
-      filt.add(GoCtx::fbit(h));
+    if (!dup && n < kCap) {
+      const int l = lane_id();
+      const int j = n >> 6;
+      const bool me = l == (n & 63);
+      s0 = me && j == 0 ? h : s0;
+      s1 = me && j == 1 ? h : s1;
+      s2 = me && j == 2 ? h : s2;
+      s3 = me && j == 3 ? h : s3;
+      ++n;
     }
 #if OS_PHASE_TIMING
     OS_PH_ADD(sub[kPhGoInsert], t0);
@@ -1344,6 +1349,176 @@ __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev)
   return r;
 }
 
+// ---------------------------------------------------------------------------
+// go playouts with chain labels on the lanes (RandomRolloutEvaluator::Evaluate,
+// mcts.cc:42-71, on go.cc / go_board.cc rules; same moves and the same words
+// drawn as GoT::apply in a scalar loop).
+//
+// Lane l holds the labels of points l and l + 64.  Every stone carries the
+// label of its chain, and a chain's label is one of its own stones, so labels
+// of live chains are distinct and a chain is ONE compare + ballot
+// (`chain(L) & colour`) instead of a flood whose iterations grow with the
+// chain's diameter.  Placing a stone relabels the own chains it joins to the
+// new point; captured stones keep stale labels, which the colour mask drops
+// (a stale label names an empty point, never a live chain's stone).
+#ifndef OS_GO_LANES
+#define OS_GO_LANES 1
+#endif
+
+struct GoLabels {
+  int32_t l0, l1;  // per lane: labels of points lane, lane + 64
+  __device__ int at(int q) const { return q < 64 ? rli(l0, q) : rli(l1, q - 64); }
+  __device__ B128 chain(int lab) const { return b128(ballot(l0 == lab), ballot(l1 == lab)); }
+  __device__ void relabel(int from, int to) {
+    l0 = l0 == from ? to : l0;
+    l1 = l1 == from ? to : l1;
+  }
+  __device__ void set(int q, int lab) {
+    const int l = lane_id();
+    l0 = q == l ? lab : l0;
+    l1 = q == l + 64 ? lab : l1;
+  }
+  __device__ void assign(B128 ch, int lab) {
+    const int l = lane_id();
+    l0 = ((ch.lo >> l) & 1) ? lab : l0;
+    l1 = ((ch.hi >> l) & 1) ? lab : l1;
+  }
+  // Labels of every chain of s (each labelled by its lowest point).
+  __device__ void init(const Go::State& s, const GameCfg& g) {
+    l0 = l1 = -1;
+    B128 todo = s.bw[0] | s.bw[1];
+    while (any(todo)) {
+      const int q = lowest(todo);
+      const B128 col = test(s.bw[0], q) ? s.bw[0] : s.bw[1];
+      const B128 ch = Go::flood(bit128(q), col, g);
+      todo = todo & ~ch;
+      assign(ch, q);
+    }
+  }
+};
+
+// LegalActions()[k] from the legal mask on the lanes: the lane holding the
+// k-th set bit sees exactly k set bits below it (mbcnt); pass is last.
+__device__ __forceinline__ int go_kth_lanes(B128 mask, int k, int pass) {
+  const int c0 = popc64(mask.lo);
+  if (k >= c0 + popc64(mask.hi)) return pass;
+  const bool hi = k >= c0;
+  const uint64_t w = hi ? mask.hi : mask.lo;
+  const uint32_t kk = static_cast<uint32_t>(hi ? k - c0 : k);
+  const int l = lane_id();
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+      static_cast<uint32_t>(w >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(w), 0u));
+  const uint64_t b = ballot(((w >> l) & 1) && below == kk);
+  return (hi ? 64 : 0) + ctz64(b);
+}
+
+// GoT::apply (go_board.cc:217-299 via go.cc:124-216) with chains from labels.
+__device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, GoWaveCtx& ctx,
+                                               GoLabels& lab, int a) {
+  using M = CfgMasks<B128>;
+  const int c = s.to_play;
+  const int pass = g.rows * g.cols;
+  s.flags = static_cast<uint8_t>((s.flags & Go::kSuperko) |
+                                 ((s.flags & Go::kLastPass) ? Go::kPrevPass : 0));
+  if (a == pass) {
+    s.ko = -1;
+    s.flags |= Go::kLastPass;
+  } else {
+    const B128 pb = bit128(a);
+    const B128 nb = Go::nbr4(pb, g);
+    const B128 own0 = pick(s.bw, c);
+    const B128 own = own0 | pb;
+    B128 opp = pick(s.bw, 1 - c);
+    const bool enemy_eye = !any(nb & ~opp);
+    s.hash ^= ctx.zob[2 * a + c];
+    B128 E = M::board(g) & ~(own | opp);
+    // The own chains next to a join the new stone's chain, labelled a.
+    B128 on_own = nb & own0;
+    while (any(on_own)) {
+      const int L = lab.at(lowest(on_own));
+      on_own = on_own & ~lab.chain(L);
+      lab.relabel(L, a);
+    }
+    lab.set(a, a);
+    int captured = 0;
+    int cap_pt = -1;
+    B128 atari = s.atari;
+    B128 capd = b128(0, 0);
+    B128 on = nb & opp;
+    while (any(on)) {
+      const int q = lowest(on);
+      const B128 ch = lab.chain(lab.at(q)) & opp;
+      on = on & ~ch;
+      const B128 libs = Go::nbr4(ch, g) & E;
+      if (!any(libs)) {
+        opp = opp & ~ch;
+        E = E | ch;
+        capd = capd | ch;
+        captured += popc(ch);
+        cap_pt = q;
+        B128 rem = ch;
+        while (any(rem)) {
+          const int x = lowest(rem);
+          rem = rem & ~bit128(x);
+          s.hash ^= ctx.zob[2 * x + (1 - c)];
+        }
+      }
+      atari = (atari & ~ch) | sel128(popc(libs) == 1, ch, b128(0, 0));
+    }
+    B128 todo = pb | (Go::nbr4(capd, g) & own);
+    while (any(todo)) {
+      const B128 ch = lab.chain(lab.at(lowest(todo))) & own;
+      todo = todo & ~ch;
+      atari = (atari & ~ch) | sel128(popc(Go::nbr4(ch, g) & E) == 1, ch, b128(0, 0));
+    }
+    s.atari = atari;
+    s.bw[0] = c ? opp : own;
+    s.bw[1] = c ? own : opp;
+    s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
+    if (!ctx.insert(s.hash, captured > 0, popc(own) + popc(opp))) s.flags |= Go::kSuperko;
+  }
+  s.to_play = static_cast<uint8_t>(1 - c);
+  s.moves++;
+}
+
+template <int Policy, class Rng>
+__device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rng& ev) {
+  s = make_uniform(s);
+  ev.uniformize();
+  GoLabels lab;
+  lab.init(s, g);
+  const int pass = g.rows * g.cols;
+  for (;;) {
+    if (Go::terminal(s, g)) break;
+#if OS_PHASE_TIMING
+    const uint64_t t0 = OS_PH_NOW();
+#endif
+    const Go::Legal l = Go::legal(s, g, ctx);
+    uint32_t k;
+    if (Policy == kPolicyCpp)
+      k = ev.uniform_lanes(static_cast<uint32_t>(l.count));
+    else
+      k = NpChoice(ev, static_cast<uint32_t>(l.count));
+    const int act = go_kth_lanes(l.mask, static_cast<int>(k), pass);
+#if OS_PHASE_TIMING
+    const uint64_t t1 = OS_PH_NOW();
+    OS_PH_ADD(ctx.sub[kPhGoLegal], t0);
+#endif
+    go_apply_lanes(s, g, ctx, lab, act);
+#if OS_PHASE_TIMING
+    OS_PH_ADD(ctx.sub[kPhGoApply], t1);
+#endif
+  }
+#if OS_PHASE_TIMING
+  const uint64_t t2 = OS_PH_NOW();
+  const int r0 = Go::ret0(s, g, ctx);
+  OS_PH_ADD(ctx.sub[kPhGoScore], t2);
+  return r0;
+#else
+  return Go::ret0(s, g, ctx);
+#endif
+}
+
 template <class G, int Policy, class Rng, class C>
 __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& ev) {
   if constexpr (std::is_same<G, Breakthrough>::value) {
@@ -1354,6 +1529,9 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
   if constexpr (Policy == kPolicyCpp && SmallAbsl<G>::value) {
     if (ev.use7) return c4_rollout_lanes(s, ctx, ev);
   }
+#if OS_GO_LANES
+  if constexpr (std::is_same<G, Go>::value) return go_rollout_wave<Policy>(s, g, ctx, ev);
+#endif
   if constexpr (Policy == kPolicyCpp && std::is_same<G, Hex>::value) {
     // n >= 3: on n <= 2 the reference's wrap filter (hex.cc:206-222) leaves
     // filled boards without a winner, so the end-of-fill argument fails.

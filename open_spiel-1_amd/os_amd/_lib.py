@@ -95,6 +95,7 @@ _P = _vp  # pointers passed as raw addresses (numpy .ctypes.data)
 
 _sig("os_last_error", _cp, [])
 _sig("os_build_info", _cp, [])
+_sig("os_abi_struct_size", _i64, [_cp])
 _sig("os_debug_phase_cycles", ctypes.c_int, [_P, _i32])
 _sig("os_game_load", ctypes.c_int, [_cp, ctypes.POINTER(_vp)])
 _sig("os_game_free", None, [_vp])
@@ -179,6 +180,20 @@ _sig("os_engine_node_bytes", _i32, [_vp])
 _sig("os_engine_state_bytes", _i32, [_vp])
 _sig("os_make_roots", _i64, [_vp, _i64, _u32, _i32, _P, _P])
 _sig("os_sample_action", _i32, [_P, _i32, _P, _P])
+
+
+def _check_abi_layout():
+  """The library reports the struct sizes it was built with: a stale build or
+  binding fails at import instead of misreading parameters."""
+  for name, cls in (("os_mcts_params", MctsParams), ("os_game_info", GameInfo),
+                    ("os_selfplay_options", SelfPlayOptions)):
+    n = lib.os_abi_struct_size(name.encode())
+    if n != ctypes.sizeof(cls):
+      raise ImportError("%s: libos_mcts.so has %d bytes, the ctypes binding %d "
+                        "(rebuild the library)" % (name, n, ctypes.sizeof(cls)))
+
+
+_check_abi_layout()
 
 
 class SpielError(RuntimeError):

@@ -9,8 +9,8 @@ semantics (each tree is one bit-exact `MCTSBot::MCTSearch`, mcts.cc:325-428):
   be gathered to every rank with one all_gather.
 * `root_parallel` (C4): every rank grows T trees on the SAME position, tree
   t of rank g seeded (g*T + t, g*T + t + 2^20).  Root child visits/rewards are
-  summed action-indexed on the device, then ONE all-reduce (RCCL over xGMI on
-  the GPU; gloo in the CPU tests) combines them.  The result equals the sum of
+  summed action-indexed on the device, then ONE all-reduce of one f64[2A]
+  message (RCCL over xGMI on the GPU; gloo in the CPU tests) combines them.  The result equals the sum of
   the W*T single-tree reference searches, whatever W is.
 * `sharded_playouts` (C5): global playouts [0, N) split into contiguous blocks,
   evaluator seed = global playout id; per-rank outcome counts (p0 wins, p1 wins,
@@ -102,9 +102,24 @@ def root_parallel(backend, history, trees_per_rank, group=None, **params):
   visits, rewards = backend.root_sums(np.asarray(history, np.int64), ids,
                                       ids + np.uint32(EVAL_SEED_OFFSET), **params)
   if world > 1:
-    dist.all_reduce(visits, group=group)
-    dist.all_reduce(rewards, group=group)
+    visits, rewards = _all_reduce_root_sums(visits, rewards, group)
   return visits, rewards
+
+
+def _all_reduce_root_sums(visits, rewards, group):
+  """ONE all-reduce of the concatenated f64[2A] (visits, rewards) message.
+
+  The exchange is ~2 KB and latency-bound on xGMI, so one collective per step
+  instead of two halves the step's fixed cost.  Visit counts travel as f64 and
+  come back exact (every partial sum is an integer below 2^53: 8 ranks x 8192
+  trees x 2048 sims ~ 1.3e8); rewards are the f64 sums they were before.
+  """
+  import torch
+  import torch.distributed as dist
+  A = visits.numel()
+  msg = torch.cat((visits.to(torch.float64), rewards))
+  dist.all_reduce(msg, group=group)
+  return msg[:A].to(torch.int64), msg[A:]
 
 
 def sharded_playouts(backend, history, total, group=None, n_rollouts=1):

@@ -143,44 +143,83 @@ def _outcome_vector(code, nplayers):
   return [0.0] * nplayers
 
 
-def tree_to_search_nodes(flat, state, game, root_action=None):
-  """Materialises the engine's flat arena (os_engine_tree) as SearchNodes.
+class _TreeView(object):
+  """The engine's flat arena of one search (os_engine_tree) plus what node
+  construction needs; shared by every lazy node of that tree."""
+  __slots__ = ("first", "n", "w", "action", "nchild", "out0", "p0", "chance", "nplayers")
 
-  Node players follow from depth where turns alternate; in games with chance
-  nodes (pig) they are read off the replayed states (a chance node's children
-  have player PlayerId.CHANCE and the outcome probabilities as priors).
-  Other priors are the uniform 1/|legal| of RandomRolloutEvaluator.prior;
-  outcomes are [v, -v] vectors as the reference stores Returns().
+  def __init__(self, flat, state, game):
+    self.first, self.n, self.w = flat["first"], flat["n"], flat["w"]
+    self.action, self.nchild, self.out0 = flat["action"], flat["nchild"], flat["out0"]
+    self.p0 = state.current_player()
+    self.chance = (game.get_type().chance_mode !=
+                   pyspiel.GameType.ChanceMode.DETERMINISTIC)
+    self.nplayers = game.num_players()
+
+
+class _LazySearchNode(SearchNode):
+  """A SearchNode whose `children` are built from the flat arena on first
+  access, so a caller that reads only the root (or `best_child()`) does not
+  pay for the whole tree (thousands of nodes per search)."""
+  __slots__ = ("_view", "_idx", "_depth", "_state", "_parent_state", "_kids")
+
+  def __init__(self, view, idx, depth, action, player, prior, parent_state=None,
+               state=None):
+    # SearchNode.__init__ is not called: `children` is the lazy property below.
+    self.action, self.player, self.prior = action, player, prior
+    self._view, self._idx, self._depth = view, idx, depth
+    self._state, self._parent_state, self._kids = state, parent_state, None
+    self.explore_count = int(view.n[idx])
+    self.total_reward = float(view.w[idx])
+    o = int(view.out0[idx])
+    self.outcome = None if o == 2 else _outcome_vector(o, view.nplayers)
+
+  def _node_state(self):
+    if self._state is None:
+      self._state = self._parent_state.child(self.action)
+    return self._state
+
+  @property
+  def children(self):
+    if self._kids is None:
+      v, idx = self._view, self._idx
+      nc = int(v.nchild[idx])
+      base = int(v.first[idx])
+      kids = []
+      if nc:
+        acts = v.action[base:base + nc].tolist()
+        if v.chance:
+          st = self._node_state()
+          child_player = st.current_player()
+          probs = dict(st.chance_outcomes()) if st.is_chance_node() else {}
+          kids = [_LazySearchNode(v, base + k, self._depth + 1, a, child_player,
+                                  probs.get(a, 1.0 / nc), parent_state=st)
+                  for k, a in enumerate(acts)]
+        else:
+          child_player = v.p0 ^ (self._depth & 1)
+          kids = [_LazySearchNode(v, base + k, self._depth + 1, a, child_player, 1.0 / nc)
+                  for k, a in enumerate(acts)]
+      self._kids = kids
+    return self._kids
+
+  @children.setter
+  def children(self, value):
+    self._kids = value
+
+
+def tree_to_search_nodes(flat, state, game, root_action=None):
+  """The engine's flat arena (os_engine_tree) as a SearchNode tree.
+
+  Nodes are materialised lazily, level by level as `children` is read.  Node
+  players follow from depth where turns alternate; in games with chance nodes
+  (pig) they are read off the replayed states (a chance node's children have
+  player PlayerId.CHANCE and the outcome probabilities as priors).  Other
+  priors are the uniform 1/|legal| of RandomRolloutEvaluator.prior; outcomes
+  are [v, -v] vectors as the reference stores Returns().
   """
-  nplayers = game.num_players()
-  first, n, w = flat["first"], flat["n"], flat["w"]
-  action, nchild, out0 = flat["action"], flat["nchild"], flat["out0"]
-  p0 = state.current_player()
-  chance = (game.get_type().chance_mode !=
-            pyspiel.GameType.ChanceMode.DETERMINISTIC)
-  root = SearchNode(root_action, p0, 1)
-  stack = [(0, root, 0, state if chance else None)]
-  while stack:
-    idx, node, depth, st = stack.pop()
-    node.explore_count = int(n[idx])
-    node.total_reward = float(w[idx])
-    if out0[idx] != 2:
-      node.outcome = _outcome_vector(int(out0[idx]), nplayers)
-    nc = int(nchild[idx])
-    if nc:
-      base = int(first[idx])
-      acts = [int(action[base + k]) for k in range(nc)]
-      if chance:
-        child_player = st.current_player()
-        probs = dict(st.chance_outcomes()) if st.is_chance_node() else {}
-        node.children = [SearchNode(a, child_player, probs.get(a, 1.0 / nc))
-                         for a in acts]
-      else:
-        child_player = p0 ^ (depth & 1)
-        node.children = [SearchNode(a, child_player, 1.0 / nc) for a in acts]
-      for k, c in enumerate(node.children):
-        stack.append((base + k, c, depth + 1, st.child(c.action) if chance else None))
-  return root
+  view = _TreeView(flat, state, game)
+  return _LazySearchNode(view, 0, 0, root_action, view.p0, 1,
+                         state=state if view.chance else None)
 
 
 class MCTSBot(pyspiel.Bot):
@@ -224,6 +263,12 @@ class MCTSBot(pyspiel.Bot):
 
   def step_with_policy(self, state):
     t0 = time.time()
+    if self._use_gpu() and not self.verbose:
+      # The engine's BestChild (mcts.py sort_key order, first maximum) is all a
+      # step needs: no tree export, no SearchNode objects.
+      chosen = int(self._run_gpu(state)[0]["best_action"][0])
+      return [(a, 1.0 if a == chosen else 0.0)
+              for a in state.legal_actions(state.current_player())], chosen
     root = self.mcts_search(state)
     best = root.best_child()
     if self.verbose:
@@ -247,10 +292,11 @@ class MCTSBot(pyspiel.Bot):
   def step(self, state):
     return self.step_with_policy(state)[1]
 
+  def _use_gpu(self):
+    return self.backend == "hip" or (self.backend == "auto" and self._gpu_eligible())
+
   def mcts_search(self, state):
-    use_gpu = self.backend == "hip" or (self.backend == "auto" and
-                                        self._gpu_eligible())
-    if use_gpu:
+    if self._use_gpu():
       return self._search_gpu(state)
     if self.backend == "auto" and not self._warned_host:
       # Never a silent CPU search: say once why this bot runs on the host.
@@ -264,13 +310,19 @@ class MCTSBot(pyspiel.Bot):
 
   # ---- GPU path -------------------------------------------------------------
   def _search_gpu(self, state):
+    _, eng = self._run_gpu(state)
+    return tree_to_search_nodes(eng.tree(0), state, self._game)
+
+  def _run_gpu(self, state):
+    """One search on the device continuing the RandomState streams; returns
+    (root outputs, engine holding the tree)."""
     eng = pyspiel._engine_for(self._game)
     bot_rs = self._random_state
     ev_rs = self.evaluator._random_state
     shared = ev_rs is bot_rs
     b = bot_rs.get_state()
     e = None if shared else ev_rs.get_state()
-    _, nb, ne = eng.mcts_stateful(
+    out, nb, ne = eng.mcts_stateful(
         state.history(), (b[1], b[2]), None if shared else (e[1], e[2]),
         uct_c=self.uct_c, max_simulations=self.max_simulations,
         n_rollouts=self.evaluator.n_rollouts, solve=self.solve,
@@ -280,7 +332,7 @@ class MCTSBot(pyspiel.Bot):
     bot_rs.set_state(("MT19937", nb[0], nb[1], b[3], b[4]))
     if not shared:
       ev_rs.set_state(("MT19937", ne[0], ne[1], e[3], e[4]))
-    return tree_to_search_nodes(eng.tree(0), state, self._game)
+    return out, eng
 
   # ---- generic host path (user evaluators / selection functions) ------------
   def _descend(self, root, state):

@@ -555,23 +555,82 @@ class MCTSBot(Bot):
     self._select = (_lib.SELECT_PUCT if child_selection_policy == ChildSelectionPolicy.PUCT
                     else _lib.SELECT_UCT)
 
-  def mcts_search(self, state):
-    from .mcts import SearchNode, tree_to_search_nodes
+  def _run(self, state):
     eng = _engine_for(self._game)
     o, self._state, self._evaluator._state = eng.mcts_stateful(
         state.history(), self._state, self._evaluator._state,
         uct_c=self.uct_c, max_simulations=self.max_simulations,
         n_rollouts=self._evaluator.n_rollouts, max_memory_mb=self.max_memory_mb,
         solve=self.solve, policy=_lib.POLICY_CPP, child_selection=self._select)
-    del o, SearchNode
+    return o, eng
+
+  def mcts_search(self, state):
+    """MCTSearch (mcts.cc:325-428): the root of the search tree (its nodes are
+    built from the device arena as they are read)."""
+    from .mcts import tree_to_search_nodes
+    _, eng = self._run(state)
     return tree_to_search_nodes(eng.tree(0), state, self._game, root_action=-1)
 
   def step(self, state):
-    root = self.mcts_search(state)
-    if not root.children:
+    """MCTSBot::Step (mcts.cc:219-248): BestChild's action, taken from the
+    engine (no tree is exported unless `verbose`)."""
+    import time
+    t0 = time.time()
+    o, eng = self._run(state)
+    if o["nchild"][0] <= 0:
       raise SpielError("MCTSBot: root has no children")
-    return root.best_child().action
+    best = int(o["best_action"][0])
+    if self.verbose:
+      self._print_verbose(state, eng, o, time.time() - t0, best)
+    return best
+
+  _SEARCH_NODE_BYTES = 80  # sizeof(SearchNode) in the reference build (SURVEY §8a M1)
+
+  def _print_verbose(self, state, eng, o, seconds, best):
+    """The report MCTSBot::Step writes to stderr when verbose (mcts.cc:226-245;
+    SearchNode::ToString / ChildrenStr :143-175)."""
+    import sys
+    from .mcts import tree_to_search_nodes
+    root = tree_to_search_nodes(eng.tree(0), state, self._game, root_action=-1)
+    nodes = int(o["nodes"][0])
+    n = root.explore_count
+    err = sys.stderr
+    err.write("Finished %d sims in %.3f secs, %.1f sims/s, tree size: %d nodes / %d mb.\n"
+              % (n, seconds, n / max(seconds, 1e-12), nodes,
+                 nodes * self._SEARCH_NODE_BYTES // (1 << 20)))
+    err.write("Root:\n%s\n" % _node_string(root, state))
+    err.write("Children:\n%s\n" % _children_string(root, state))
+    chosen = next(c for c in root.children if c.action == best)
+    if chosen.children:
+      err.write("Children of chosen:\n%s\n" % _children_string(chosen, state.child(best)))
+    err.flush()
 
   def step_with_policy(self, state):
     a = self.step(state)
     return [(a, 1.0)], a
+
+
+def _node_string(node, state):
+  """SearchNode::ToString(state) (mcts.cc:162-175): `state` is the node's
+  parent position, whose ActionToString names the node's action."""
+  name = ("none" if node.action is None or node.action == -1
+          else state.action_to_string(node.player, node.action))
+  value = node.total_reward / node.explore_count if node.explore_count else 0.0
+  if node.outcome is None:
+    outcome = "none"
+  else:
+    outcome = "%4.1f" % node.outcome[0 if node.player == PlayerId.CHANCE else node.player]
+  return ("%6s: player: %d, prior: %5.3f, value: %6.3f, sims: %5d, outcome: %s, "
+          "%3d children" % (name, node.player, node.prior, value, node.explore_count,
+                            outcome, len(node.children)))
+
+
+def _children_string(node, state):
+  """SearchNode::ChildrenStr (mcts.cc:143-160): children best-first by
+  CompareFinal (outcome, explore_count, total_reward), one line each."""
+  def key(c):
+    proven = 0.0 if c.outcome is None else c.outcome[0 if c.player == PlayerId.CHANCE
+                                                     else c.player]
+    return (proven, c.explore_count, c.total_reward)
+  ordered = sorted(node.children, key=key, reverse=True)
+  return "".join(_node_string(c, state) + "\n" for c in ordered)

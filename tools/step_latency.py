@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""One-root `step` latency of the drop-in bots, per game.
+
+For each game, from the initial position, at the reference's simulation
+count (1000, python/examples/mcts.py and SURVEY §8d C1):
+  cpp_step_ms     pyspiel.MCTSBot.step (C++ MCTSBot semantics), wall
+  py_step_ms      open_spiel.python.algorithms.mcts.MCTSBot.step (numpy), wall
+  kernel_ms       the same search's device time alone: os_engine_run_async
+                  bracketed by HIP events on the launch stream
+  host_overhead   cpp_step_ms - kernel_ms, and its fraction of kernel_ms
+  oracle_1core_ms the oracle MCTSBot (reference-faithful restatement of
+                  mcts.cc) for the same search on one host core
+Writes JSON + a markdown table to --out (default profiles/r04/step_latency).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "open_spiel-1_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GAMES = ["tic_tac_toe", "connect_four", "breakthrough", "hex", "go(board_size=9)",
+         "pig"]
+
+
+def _median_ms(fn, reps):
+  ts = []
+  for _ in range(reps):
+    t0 = time.perf_counter()
+    fn()
+    ts.append((time.perf_counter() - t0) * 1e3)
+  return float(np.median(ts)), ts
+
+
+def measure(gs, sims, reps, torch):
+  import pyspiel
+  from open_spiel.python.algorithms import mcts
+  from os_amd import engine as E
+  import oracle_lib as O
+  game = pyspiel.load_game(gs)
+  st = game.new_initial_state()
+  if st.is_chance_node():
+    st.apply_action(st.legal_actions()[0])
+  hist = st.history()
+  # the drop-in bots (first call warms the engine and its arena)
+  cbot = pyspiel.MCTSBot(game, pyspiel.RandomRolloutEvaluator(1, 7), 2.0, sims, 1000, True, 3,
+                         False)
+  cbot.step(st)
+  cpp_ms, _ = _median_ms(lambda: cbot.step(st), reps)
+  rs = np.random.RandomState(3)
+  pbot = mcts.MCTSBot(game, 2.0, sims, mcts.RandomRolloutEvaluator(1, rs), random_state=rs,
+                      solve=True, backend="hip")
+  pbot.step(st)
+  py_ms, _ = _median_ms(lambda: pbot.step(st), reps)
+  # the kernel alone: the same search through the device-resident pipeline
+  eng = E.Engine(game.game_string if hasattr(game, "game_string") else gs)
+  acts = np.array(hist, np.int64)
+  offs = np.array([0, len(hist)], np.int64)
+  eng.prepare(acts, offs, [3], [7], uct_c=2.0, max_simulations=sims)
+  stream = torch.cuda.current_stream()
+  ks = []
+  for _ in range(reps + 1):
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    eng.run_async(stream.cuda_stream)
+    e1.record(stream)
+    e1.synchronize()
+    ks.append(e0.elapsed_time(e1))
+  eng.fetch()
+  kernel_ms = float(np.median(ks[1:]))
+  # oracle, one core
+  og = O.Game(gs)
+  osecs = []
+  for _ in range(max(3, reps // 2)):
+    s, _n = og.time_mcts_batch(acts, offs, np.array([3], np.uint32), np.array([7], np.uint32),
+                               max_simulations=sims, threads=1)
+    osecs.append(s * 1e3)
+  return {"game": gs, "sims": sims, "cpp_step_ms": cpp_ms, "py_step_ms": py_ms,
+          "kernel_ms": kernel_ms, "host_overhead_ms": cpp_ms - kernel_ms,
+          "host_overhead_frac": (cpp_ms - kernel_ms) / kernel_ms,
+          "py_overhead_frac": (py_ms - kernel_ms) / kernel_ms,
+          "oracle_1core_ms": float(np.median(osecs)),
+          "gpu_over_oracle": float(np.median(osecs)) / cpp_ms}
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--sims", type=int, default=1000)
+  ap.add_argument("--reps", type=int, default=10)
+  ap.add_argument("--games", default=",".join(GAMES))
+  ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04", "step_latency"))
+  args = ap.parse_args()
+  import torch
+  torch.cuda.init()
+  rows = []
+  for gs in args.games.split(","):
+    r = measure(gs, args.sims, args.reps, torch)
+    rows.append(r)
+    print(json.dumps(r), flush=True)
+  os.makedirs(args.out, exist_ok=True)
+  with open(os.path.join(args.out, "step_latency.json"), "w") as f:
+    json.dump(rows, f, indent=1)
+  with open(os.path.join(args.out, "step_latency.md"), "w") as f:
+    f.write("| game | sims | pyspiel.MCTSBot.step ms | mcts.MCTSBot.step ms | kernel ms | "
+            "host overhead | oracle 1 core ms | oracle / GPU step |\n|---|---|---|---|---|---|---|---|\n")
+    for r in rows:
+      f.write("| %s | %d | %.3f | %.3f | %.3f | %.3f ms (%.1f%%) | %.2f | %.2f |\n" % (
+          r["game"], r["sims"], r["cpp_step_ms"], r["py_step_ms"], r["kernel_ms"],
+          r["host_overhead_ms"], 100 * r["host_overhead_frac"], r["oracle_1core_ms"],
+          r["gpu_over_oracle"]))
+
+
+if __name__ == "__main__":
+  main()
