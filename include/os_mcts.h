@@ -262,6 +262,12 @@ int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos);
 #define OS_AZ_REQUESTS_SEPARATE 0
 #define OS_AZ_REQUESTS_FUSED 1
 int os_az_set_requests(os_engine* e, int32_t mode);
+/* Kernel of the next os_az_prepare*: OS_LAYOUT_WAVE (one wavefront per search:
+ * coalesced child scans, lane-parallel expansion / backup / request writes),
+ * OS_LAYOUT_LANE (one lane per search; the only one that garbage-collects,
+ * mcts.cc:402-424) or OS_LAYOUT_AUTO (default: wave unless the node budget can
+ * be reached).  Same results either way. */
+int os_az_set_layout(os_engine* e, int32_t layout);
 /* The Dirichlet noise os_az_prepare draws for one fresh MCTSBot(seed) at a
  * root with `count` legal actions: out[count] (normalised, legal-action
  * order); returns the MT19937 words consumed (< 0 on error).  Exposed so the

@@ -877,6 +877,18 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     HIP_TRY(hipMemcpy(e->d_az_pos.p, bot_pos, static_cast<size_t>(R) * 4, hipMemcpyHostToDevice));
   }
   e->az_puct = puct ? 1 : 0;
+  {
+    // One wave per search unless GC could fire (k_waz_step has no GC; the
+    // lane kernel runs mcts.cc:402-424 exactly) or the caller asks for lanes.
+    const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+    const int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * e->game.cfg.max_children;
+    const bool gc_possible = max_nodes > 1 && worst >= max_nodes;
+    if (e->az_layout == OS_LAYOUT_WAVE && gc_possible)
+      return Fail(OS_ERR_UNSUPPORTED,
+                  "the wave external-evaluator layout does not garbage-collect: raise "
+                  "max_memory_mb or use OS_LAYOUT_LANE");
+    e->az_wave = e->az_layout == OS_LAYOUT_WAVE || (e->az_layout == OS_LAYOUT_AUTO && !gc_possible);
+  }
   e->az_kind = kind;
   e->az_obs = obs;
   e->az_legal = legal;
@@ -1384,6 +1396,14 @@ int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,
   return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, nullptr, dirichlet_alpha,
                    dirichlet_epsilon, dev_kind, dev_obs, dev_legal, dev_prior, dev_value,
                    dev_pending, bot_keys ? bot_keys : nullptr, bot_pos);
+}
+
+int os_az_set_layout(os_engine* e, int32_t layout) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (layout != OS_LAYOUT_WAVE && layout != OS_LAYOUT_LANE && layout != OS_LAYOUT_AUTO)
+    return Fail(OS_ERR_INVALID, "unknown layout");
+  e->az_layout = layout;
+  return OS_OK;
 }
 
 int os_az_set_requests(os_engine* e, int32_t mode) {

@@ -279,6 +279,8 @@ struct os_engine {
   bool az_import = false;  // os_az_prepare_stateful
   int32_t az_requests = 0;  // os_az_set_requests (OS_AZ_REQUESTS_SEPARATE)
   bool az_fused = false;    // mode of the prepared batch
+  int32_t az_layout = OS_LAYOUT_AUTO;  // os_az_set_layout
+  bool az_wave = false;     // the prepared batch runs k_waz_step (one wave per search)
   osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw;
   osx::DevBuf d_lpath, d_lheads, d_lact;  // k_lsearch paths, big-board heads / actions
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,

@@ -790,6 +790,478 @@ __global__ __launch_bounds__(64) void k_az_step(AzArgs a) {
 }
 
 
+// ---------------------------------------------------------------------------
+// Wave-per-search external-evaluator step (os_az.h semantics; SURVEY §8f rank
+// 2).  k_az_step runs one search per LANE with its whole continuation read
+// and written per lane -- 16384 searches fill 256 waves, one per CU, each
+// lane's chain of dependent HBM accesses exposed.  Here one WAVE advances one
+// search, as k_wsearch does: the child scan is one coalesced load (lane k <->
+// child k) and a DPP argmax, the expansion's shuffle runs on the lanes, the
+// backup updates every path node at once (lane d <-> depth d), and the request
+// (observation tensor, legal mask) is written by all lanes.  Between launches
+// the continuation stays in the same AzSlot<G> (state, counters, path, go's
+// positions since the root) and the bot rng in its HBM row in numpy form
+// (WaveMtRow).  GC (mcts.cc:402-424) is not implemented here: the host runs
+// k_az_step whenever the node budget could be reached.  Bit-exact with
+// az_step (tests/test_az.py, both layouts).
+template <class G>
+struct WazCtx {
+  __device__ static NoCtx make(const AzArgs&, int64_t) { return NoCtx(); }
+  __device__ static void load_tail(NoCtx&, const AzSlot<G>&) {}
+  __device__ static void save_tail(const NoCtx&, AzSlot<G>&) {}
+};
+template <>
+struct WazCtx<Go> {
+  __device__ static GoWaveCtx make(const AzArgs& a, int64_t r) {
+    GoWaveCtx c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + r * a.hash_stride;
+    c.n_base = a.root_nhash[r];
+    c.init_filters();
+    return c;
+  }
+  // The pending simulation's positions since the root follow the base.
+  __device__ static void load_tail(GoWaveCtx& c, const AzSlot<Go>& sl) {
+    const int nl = __builtin_amdgcn_readfirstlane(sl.glog.n_log);
+    const int l = lane_id();
+    uint64_t* sv[4] = {&c.s0, &c.s1, &c.s2, &c.s3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 64 * j + l;
+      const bool in = i >= c.n_base && i < c.n_base + nl && i < GoWaveCtx::kCap;
+      const uint64_t v = in ? sl.glog.log[i - c.n_base] : 0ull;
+      *sv[j] = in ? v : *sv[j];
+    }
+    c.n = c.n_base + nl < GoWaveCtx::kCap ? c.n_base + nl : GoWaveCtx::kCap;
+    // Every held entry stays a candidate (a superset of the capture rule's:
+    // positions after the last capture cannot repeat anyway).
+    c.cand_end = c.n;
+  }
+  __device__ static void save_tail(const GoWaveCtx& c, AzSlot<Go>& sl) {
+    const int l = lane_id();
+    const uint64_t sv[4] = {c.s0, c.s1, c.s2, c.s3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 64 * j + l;
+      if (i >= c.n_base && i < c.n && i - c.n_base < kAzLogCap) sl.glog.log[i - c.n_base] = sv[j];
+    }
+    if (l == 0) sl.glog.n_log = c.n - c.n_base;
+  }
+};
+
+// Path of the pending simulation on the lanes: entry d in lane d % 64 of slot d / 64.
+struct WazPath {
+  uint32_t p0, p1, p2, p3;
+  __device__ uint32_t at(int d) const {
+    const int j = d >> 6, q = d & 63;
+    return rl32(j == 0 ? p0 : (j == 1 ? p1 : (j == 2 ? p2 : p3)), q);
+  }
+  __device__ void set(int d, uint32_t v) {
+    const int j = d >> 6;
+    const bool me = lane_id() == (d & 63);
+    p0 = me && j == 0 ? v : p0;
+    p1 = me && j == 1 ? v : p1;
+    p2 = me && j == 2 ? v : p2;
+    p3 = me && j == 3 ? v : p3;
+  }
+};
+
+template <class G, bool kPuct>
+__global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
+  const int64_t r = blockIdx.x;
+  if (r >= a.num_roots) return;
+  const int l = lane_id();
+  __shared__ uint32_t mt_lds[kMtN];
+  AzSlot<G>& sl = static_cast<AzSlot<G>*>(a.slots)[r];
+  int stage = __builtin_amdgcn_readfirstlane(sl.stage);
+  if (stage == kAzDone) {
+    if (l == 0) a.kind[r] = kAzNone;
+    return;
+  }
+  const GameCfg& g = a.cfg;
+  const SearchParams& sp = a.sp;
+  const typename G::State root = make_uniform(static_cast<const typename G::State*>(a.roots)[r]);
+  const int P0 = G::to_move(root);
+  const int A = a.num_actions;
+  Node<double>* nodes = a.arena + r * static_cast<int64_t>(a.cap);
+  double* prior = a.priors + r * static_cast<int64_t>(a.cap);
+  double* raw = a.raw ? a.raw + r * static_cast<int64_t>(a.cap) : nullptr;
+  const double* pin = a.prior_in + r * static_cast<int64_t>(A);
+  const uint32_t cap = a.cap;
+  const double inf = __builtin_huge_val();
+  typename WaveCtxOf<G>::type ctx = WazCtx<G>::make(a, r);
+#if OS_PHASE_TIMING
+  PhaseCycles ph_unused = {};
+  if constexpr (std::is_same<G, Go>::value) ctx.sub = ph_unused.c;
+#endif
+  WaveMtRow bot;
+  typename G::State s;
+  int sim, depth, nodes_count;
+  uint32_t used;
+  SearchResult res;
+  WazPath path;
+  path.p0 = path.p1 = path.p2 = path.p3 = 0;
+  if (stage == kAzStart) {
+    int p = kMtN;
+    bool in_lds = false;
+    if (a.import_mt) {
+      p = a.mt_pos_in[r];
+    } else {
+      if (l == 0) mt_seed(mt_lds, a.bot_seeds[r]);  // init_genrand: twisted at the first draw
+      __syncthreads();
+      in_lds = true;
+    }
+    bot.init_row(a.mt + r * kMtN, mt_lds, p, in_lds);
+    if (l == 0) {
+      Node<double> z;
+      z.first = 0; z.n = 0; z.w = 0.0; z.action = 0; z.nchild = 0; z.out = kUnsolved;
+      nodes[0] = z;
+      prior[0] = 1.0;  // SearchNode(kInvalidAction, player_id, 1) (mcts.cc:328)
+    }
+    __threadfence_block();
+    sim = 0;
+    depth = 0;
+    nodes_count = 1;
+    used = 1;
+    res.status = kOk;
+    res.sims = res.nodes = res.gc_runs = res.max_depth = 0;
+    res.used = res.scanned = res.backed = res.expanded = res.solver_scanned = 0;
+    res.rng_words = res.pad = 0;
+    s = root;
+  } else {
+    bot.init_row(a.mt + r * kMtN, mt_lds, __builtin_amdgcn_readfirstlane(sl.mt_idx), false);
+    s = make_uniform(sl.s);
+    sim = __builtin_amdgcn_readfirstlane(sl.sim);
+    depth = __builtin_amdgcn_readfirstlane(sl.depth);
+    nodes_count = __builtin_amdgcn_readfirstlane(sl.nodes_count);
+    used = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sl.used)));
+    res = make_uniform(sl.res);
+    path.p0 = sl.path[l];
+    if (depth >= 64) path.p1 = sl.path[64 + l];
+    if (depth >= 128) path.p2 = sl.path[128 + l];
+    if (depth >= 192) path.p3 = sl.path[192 + l];
+    WazCtx<G>::load_tail(ctx, sl);
+  }
+  int phase;  // 0 new simulation, 1 descend, 2 expand with priors, 3 value ready, -1 stop
+  double v0 = 0.0;
+  bool solved = false;
+  bool from_raw = false;  // phase 2 takes the parked priors of a fused request
+  uint32_t parked_first = 0;
+  int request = kAzNone;
+  // The node being descended from / expanded: index and its (first, n, nchild).
+  uint32_t cur_x = 0, cur_first = 0;
+  int32_t cur_n = 0;
+  int cur_nc = 0;
+
+  auto legal_lanes = [&](const typename G::Legal& lg, LaneArr& acts) {
+    const int nc = lg.count;
+    const int k0 = WaveKth<G>::kth(lg, l);
+    acts.a0 = l < nc ? static_cast<uint32_t>(k0) : 0u;
+    acts.a1 = l + 64 < nc ? static_cast<uint32_t>(lg.kth(l + 64)) : 0u;
+  };
+  auto reload_cur = [&](uint32_t x) {
+    const Node<double> nx = nodes[x];
+    cur_x = x;
+    cur_first = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nx.first)));
+    cur_n = __builtin_amdgcn_readfirstlane(nx.n);
+    cur_nc = __builtin_amdgcn_readfirstlane(nx.nchild);
+  };
+
+  if (stage == kAzStart) {
+    phase = 0;
+  } else if (stage == kAzWaitPrior) {
+    phase = 2;
+    reload_cur(path.at(depth));
+  } else {
+    v0 = a.value_in[r];
+    phase = 3;
+    if (raw != nullptr) {
+      // Park the leaf's priors (legal order) where its children will live.
+      const typename G::Legal lg = G::legal(s, g, ctx);
+      const int nc = lg.count;
+      if (used + static_cast<uint32_t>(nc) > cap) {
+        res.status = kArenaOverflow;
+        phase = -1;
+      } else {
+        LaneArr acts;
+        legal_lanes(lg, acts);
+        if (l < nc) raw[used + l] = pin[acts.a0];
+        if (l + 64 < nc) raw[used + l + 64] = pin[acts.a1];
+        if (l == 0) nodes[path.at(depth)].first = used;
+        used += nc;
+        __threadfence_block();
+      }
+    }
+  }
+  for (;;) {
+    if (phase < 0) break;
+    if (phase == 0) {
+      if (sim >= sp.max_simulations) break;
+      s = root;
+      ctx.reset();
+      depth = 0;
+      path.set(0, 0u);
+      reload_cur(0);
+      phase = 1;
+    }
+    if (phase == 2) {
+      // Prior of the pending node (legal order), shuffled with the bot rng
+      // like std::shuffle over (action, prior) pairs (mcts.cc:275-282).
+      const typename G::Legal lg = G::legal(s, g, ctx);
+      const int nc = lg.count;
+      if (!from_raw && used + static_cast<uint32_t>(nc) > cap) {
+        res.status = kArenaOverflow;
+        break;
+      }
+      const bool noisy = cur_x == 0 && a.noise != nullptr;
+      if (noisy) {  // dirichlet_noise consumed these words of rng_ (mcts.cc:265-267)
+        const int skip = a.noise_skip[r];
+        for (int i = 0; i < skip; ++i) bot.next();
+      }
+      LaneArr acts, perm;
+      legal_lanes(lg, acts);
+      perm.a0 = static_cast<uint32_t>(l);
+      perm.a1 = static_cast<uint32_t>(l + 64);
+      wave_shuffle<kPolicyCpp>(perm, nc, bot);
+      const uint32_t first = from_raw ? parked_first : used;
+      const double* noise = a.noise ? a.noise + r * a.noise_stride : nullptr;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = l + 64 * h;
+        const int j = static_cast<int>(h == 0 ? perm.a0 : perm.a1);
+        const uint32_t x0 = static_cast<uint32_t>(__shfl(static_cast<int>(acts.a0), j & 63));
+        const uint32_t x1 = static_cast<uint32_t>(__shfl(static_cast<int>(acts.a1), j & 63));
+        const int act = static_cast<int>(j < 64 ? x0 : x1);
+        if (k < nc) {
+          const double p = from_raw ? raw[first + j] : pin[act];
+          Node<double> c;
+          c.first = 0; c.n = 0; c.w = 0.0; c.action = static_cast<uint16_t>(act);
+          c.nchild = 0; c.out = kUnsolved;
+          nodes[first + k] = c;
+          // (1 - eps) * p + eps * noise, separately rounded (mcts.cc:269-271)
+          prior[first + k] = noisy ? (1.0 - a.noise_eps) * p + a.noise_eps * noise[j] : p;
+        }
+      }
+      if (l == 0) {
+        nodes[cur_x].first = first;
+        nodes[cur_x].nchild = static_cast<uint8_t>(nc);
+      }
+      __threadfence_block();
+      if (!from_raw) used += nc;
+      from_raw = false;
+      nodes_count += nc;
+      res.expanded += nc;
+      cur_first = first;
+      cur_nc = nc;
+      phase = 1;
+    }
+    if (phase == 1) {
+      for (;;) {
+        if (G::terminal(s, g) || cur_n <= 0) break;
+        if (cur_nc == 0 && raw != nullptr && cur_first != 0) {
+          from_raw = true;  // parked by this node's fused request: expand now
+          parked_first = cur_first;
+          break;
+        }
+        if (cur_nc == 0) {
+          request = kAzPrior;
+          break;
+        }
+        // ---- selection: lane k scores child k (and k + 64) ----
+        const int cp = P0 ^ (depth & 1);
+        const bool in0 = l < cur_nc, in1 = l + 64 < cur_nc;
+        const Node<double> c0 = nodes[cur_first + (in0 ? l : 0)];
+        const Node<double> c1 = nodes[cur_first + (in1 ? l + 64 : 0)];
+        double v0s, v1s;
+        if constexpr (kPuct) {  // mcts.cc:102-111
+          const double sqrtN = __builtin_sqrt(static_cast<double>(cur_n));
+          const double pr0 = prior[cur_first + (in0 ? l : 0)];
+          const double pr1 = prior[cur_first + (in1 ? l + 64 : 0)];
+          const double q0 = c0.n != 0 ? c0.w / static_cast<double>(c0.n) : 0.0;
+          const double q1 = c1.n != 0 ? c1.w / static_cast<double>(c1.n) : 0.0;
+          double u0 = q0 + sp.uct_c * pr0 * sqrtN / static_cast<double>(c0.n + 1);
+          double u1 = q1 + sp.uct_c * pr1 * sqrtN / static_cast<double>(c1.n + 1);
+          u0 = c0.out != kUnsolved ? outcome_for(c0.out, cp) : u0;
+          u1 = c1.out != kUnsolved ? outcome_for(c1.out, cp) : u1;
+          v0s = in0 ? u0 : -inf;
+          v1s = in1 ? u1 : -inf;
+        } else {  // mcts.cc:89-100
+          const double logN = sp.log_lut[cur_n];
+          v0s = uct_value_sel(c0, in0, cp, logN, sp.uct_c);
+          v1s = uct_value_sel(c1, in1, cp, logN, sp.uct_c);
+        }
+        const int chosen = wave_argmax2<64, true>(v0s, v1s);
+        res.scanned += cur_nc;
+        const int src = chosen & 63;
+        const Node<double> bc = chosen >= 64 ? c1 : c0;
+        const int act = static_cast<int>(rl32(bc.action, src));
+        const uint32_t ci = cur_first + static_cast<uint32_t>(chosen);
+        cur_x = ci;
+        cur_first = rl32(bc.first, src);
+        cur_n = rli(bc.n, src);
+        cur_nc = rli(bc.nchild, src);
+        G::apply(s, g, ctx, act);
+        if (++depth >= kMaxPath) {
+          res.status = kPathOverflow;
+          break;
+        }
+        path.set(depth, ci);
+      }
+      if (res.status != kOk) break;
+      if (from_raw) {
+        phase = 2;
+        continue;
+      }
+      if (request != kAzNone) break;
+      if (depth > res.max_depth) res.max_depth = depth;
+      if (G::terminal(s, g)) {
+        const int r0 = G::ret0(s, g, ctx);
+        if (l == 0) nodes[cur_x].out = static_cast<int8_t>(r0);
+        __threadfence_block();
+        solved = sp.solve != 0;
+        v0 = static_cast<double>(r0);
+        phase = 3;
+      } else {
+        request = raw != nullptr ? kAzBoth : kAzValue;
+        break;
+      }
+    }
+    if (phase == 3) {
+      // ---- backup (mcts.cc:351-357): lane d updates path node d ----
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = 64 * j + l;
+        const uint32_t x = j == 0 ? path.p0 : (j == 1 ? path.p1 : (j == 2 ? path.p2 : path.p3));
+        if (d <= depth) {
+          const int pl = d == 0 ? P0 : (P0 ^ ((d - 1) & 1));
+          Node<double>& nd = nodes[x];
+          nd.w = nd.w + (pl == 0 ? v0 : -v0);
+          nd.n = nd.n + 1;
+        }
+      }
+      __threadfence_block();
+      res.backed += depth + 1;
+      // ---- MCTS-Solver (mcts.cc:359-395), from the leaf's parent upward ----
+      if (solved) {
+        for (int d = depth; d >= 0; --d) {
+          const uint32_t x = path.at(d);
+          const Node<double> nd = nodes[x];
+          const int nc = __builtin_amdgcn_readfirstlane(nd.nchild);
+          if (nc <= 0) continue;
+          const uint32_t f = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nd.first)));
+          const int cpl = P0 ^ (d & 1);
+          res.solver_scanned += nc;
+          const bool in0 = l < nc, in1 = l + 64 < nc;
+          const int8_t o0 = in0 ? nodes[f + l].out : kUnsolved;
+          const int8_t o1 = in1 ? nodes[f + l + 64].out : kUnsolved;
+          const bool un0 = in0 && o0 == kUnsolved, un1 = in1 && o1 == kUnsolved;
+          const bool all_solved = (ballot(un0) | ballot(un1)) == 0;
+          // the first solved child with the largest value for the mover
+          const double w0 = in0 && o0 != kUnsolved ? outcome_for(o0, cpl) : -inf;
+          const double w1 = in1 && o1 != kUnsolved ? outcome_for(o1, cpl) : -inf;
+          const double m = wave_max_f64<64>(fmax(w0, w1));
+          if (m == -inf) {
+            solved = false;
+            break;
+          }
+          const uint64_t b0 = ballot(w0 == m);
+          const int bi = b0 ? ctz64(b0) : 64 + ctz64(ballot(w1 == m));
+          const int8_t bo = static_cast<int8_t>(rli(bi < 64 ? o0 : o1, bi & 63));
+          if (all_solved || m == 1.0) {
+            if (l == 0) nodes[x].out = bo;
+            __threadfence_block();
+          } else {
+            solved = false;
+            break;
+          }
+        }
+      }
+      sim += 1;
+      res.sims = sim;
+      const Node<double> rt = nodes[0];
+      const int rout = __builtin_amdgcn_readfirstlane(rt.out);
+      const int rnc = __builtin_amdgcn_readfirstlane(rt.nchild);
+      if (rout != kUnsolved || rnc == 1) break;  // mcts.cc:398-401
+      phase = 0;
+    }
+  }
+  if (request != kAzNone && res.status == kOk) {
+    // ---- save the continuation, write the request ----
+    res.rng_words += bot.words.get();
+    const int mt_pos = bot.export_pos();
+    if (l == 0) {
+      sl.s = s;
+      sl.stage = request == kAzPrior ? kAzWaitPrior : kAzWaitValue;
+      sl.sim = sim;
+      sl.depth = depth;
+      sl.nodes_count = nodes_count;
+      sl.used = used;
+      sl.mt_idx = mt_pos;
+      sl.res = res;
+    }
+    const uint32_t ps[4] = {path.p0, path.p1, path.p2, path.p3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (64 * j + l <= depth) sl.path[64 * j + l] = ps[j];
+    WazCtx<G>::save_tail(ctx, sl);
+    bot.save();
+    const int cells = g.rows * g.cols;
+    const int osz = a.obs_size;
+    const int p = G::to_move(s);
+    float* o = a.obs + r * static_cast<int64_t>(osz);
+    for (int i = l; i < osz; i += 64) o[i] = G::obs(s, g, p, i / cells, i % cells);
+    uint8_t* lm = a.legal + r * static_cast<int64_t>(A);
+    for (int i = l; i < A; i += 64) lm[i] = 0;
+    __threadfence_block();
+    const typename G::Legal lg = G::legal(s, g, ctx);
+    LaneArr acts;
+    legal_lanes(lg, acts);
+    if (l < lg.count) lm[acts.a0] = 1;
+    if (l + 64 < lg.count) lm[acts.a1] = 1;
+    if (l == 0) {
+      a.kind[r] = request;
+      atomicAdd(a.pending, 1);
+    }
+    return;
+  }
+  // ---- finished (or failed): publish the root's children ----
+  res.nodes = nodes_count;
+  res.used = used;
+  res.rng_words += bot.words.get();
+  bot.save();
+  if (l == 0) {
+    sl.stage = kAzDone;
+    sl.res = res;
+    a.kind[r] = kAzNone;
+  }
+  const int mt_end = bot.export_pos();
+  if (a.import_mt && l == 0) a.mt_pos_out[r] = mt_end;
+  __threadfence_block();
+  const Node<double> rn = nodes[0];
+  const int nc = __builtin_amdgcn_readfirstlane(rn.nchild);
+  const uint32_t rf = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(rn.first)));
+  const int64_t ob = r * a.max_children;
+  for (int k = l; k < nc && k < a.max_children; k += 64) {
+    const Node<double> c = nodes[rf + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = c.w;
+    a.child_out[ob + k] =
+        c.out == kUnsolved ? kUnsolved : static_cast<int8_t>(P0 == 0 ? c.out : -c.out);
+  }
+  if (l == 0) {
+    a.results[r] = res;
+    a.nchild[r] = nc;
+    a.root_n[r] = rn.n;
+    a.root_w[r] = rn.w;
+    a.root_out[r] = rn.out == kUnsolved ? kUnsolved
+                                        : static_cast<int8_t>(P0 == 0 ? rn.out : -rn.out);
+    const int b = best_child(nodes, P0);
+    a.best_action[r] = b < 0 ? -1 : nodes[rn.first + b].action;
+  }
+}
+
+
 template <class G>
 struct RollCtx {
   __device__ static NoCtx make(const RollArgs&, int64_t, uint8_t*) { return NoCtx(); }
@@ -1176,6 +1648,16 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.best_action = d.best_action;
   HIP_TRY(hipMemsetAsync(e->az_pending, 0, sizeof(int32_t), stream));
   if (e->num_roots == 0) return OS_OK;
+  if (e->az_wave) {  // one wave per search (k_waz_step)
+    if (e->az_puct)
+      hipLaunchKernelGGL((k_waz_step<G, true>), dim3(static_cast<unsigned>(e->num_roots)),
+                         dim3(64), 0, stream, a);
+    else
+      hipLaunchKernelGGL((k_waz_step<G, false>), dim3(static_cast<unsigned>(e->num_roots)),
+                         dim3(64), 0, stream, a);
+    HIP_TRY(hipGetLastError());
+    return OS_OK;
+  }
   // Searches per workgroup (one wave): os_mcts_params.block_size, 64 by
   // default.  Fewer lanes per wave spread a small batch over more SIMDs.
   const int bs = e->params.block_size > 0 ? std::min(e->params.block_size, 64) : 64;

@@ -514,6 +514,61 @@ struct GoWaveCtx {
   }
 };
 
+// The bot rng of a RESUMABLE wave search (k_waz_step): between launches the
+// stream lives in HBM in numpy's (key[624], pos) form -- a fully twisted
+// block and the words consumed -- so a launch reads only the 64-word windows
+// it draws from.  A twist (block used up) copies the row to LDS and twists it
+// there cooperatively (WaveMt::twist); the launch then reads the LDS copy, and
+// save() writes the new block back.  The row is never written in place while
+// it is being read.
+struct WaveMtRow : WaveMt {
+  uint32_t* row;  // global, 624 words
+  uint32_t* lds;  // LDS scratch, 624 words
+  int dirty;
+  // p: words consumed (kMtN: the next draw twists -- a fresh seed's state).
+  __device__ void init_row(uint32_t* r, uint32_t* scratch, int p, bool row_in_lds) {
+    row = r;
+    lds = scratch;
+    dirty = row_in_lds ? 1 : 0;
+    s = row_in_lds ? scratch : r;
+    use7 = 0;
+    init_import(p);
+  }
+  __device__ void twist() {
+    if (s != lds) {
+      for (int i = lane_id(); i < kMtN; i += 64) lds[i] = row[i];
+      __builtin_amdgcn_wave_barrier();
+      s = lds;
+    }
+    WaveMt::twist();
+    dirty = 1;
+  }
+  __device__ void refill() {
+    int nb = base + valid;
+    if (base >= kMtN || nb >= kMtN) {
+      twist();
+      nb = 0;
+    }
+    base = nb;
+    valid = kMtN - base < 64 ? kMtN - base : 64;
+    load_window(base + lane_id());
+    pos = 0;
+  }
+  __device__ uint32_t next() {
+    if (pos >= valid) refill();
+    const uint32_t w = rl32(cur, pos);
+    ++pos;
+    words.add(1);
+    return w;
+  }
+  __device__ void save() {
+    if (dirty) {
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane_id(); i < kMtN; i += 64) row[i] = lds[i];
+    }
+  }
+};
+
 template <class G>
 struct WaveCtxOf {
   using type = NoCtx;
@@ -582,7 +637,8 @@ __device__ __forceinline__ uint32_t div_pair(uint32_t x, uint32_t d) {
 //  4. one bpermute per slot gathers the shuffled array.
 // Step k: k < e (n even): (1, x), range 2; else i = 1 + e + 2 (k - e), range
 // (i + 1)(i + 2), x -> (i, x / (i + 2)) then (i + 1, x % (i + 2)).
-__device__ __forceinline__ void wave_shuffle_cpp(LaneArr& a, int n, WaveMt& g) {
+template <class Mt>
+__device__ __forceinline__ void wave_shuffle_cpp(LaneArr& a, int n, Mt& g) {
   if (n <= 1) return;
   const int l = lane_id();
   const int e = (n & 1) ? 0 : 1;
@@ -638,7 +694,7 @@ __device__ __forceinline__ void wave_shuffle_cpp(LaneArr& a, int n, WaveMt& g) {
 
 template <int Policy, class Rng>
 __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
-  if constexpr (Policy == kPolicyCpp && std::is_same<Rng, WaveMt>::value) {
+  if constexpr (Policy == kPolicyCpp && std::is_base_of<WaveMt, Rng>::value) {
     wave_shuffle_cpp(a, n, g);
   } else if (Policy == kPolicyCpp) {  // libstdc++ 11 std::shuffle, pair path
     if (n <= 1) return;

@@ -38,6 +38,7 @@ from ._lib import check, lib, ptr
 
 KIND_NONE, KIND_PRIOR, KIND_VALUE, KIND_BOTH = 0, 1, 2, 3
 _REQUESTS = {"separate": _lib.AZ_REQUESTS_SEPARATE, "fused": _lib.AZ_REQUESTS_FUSED}
+_LAYOUTS = {"auto": _lib.LAYOUT_AUTO, "wave": _lib.LAYOUT_WAVE, "lane": _lib.LAYOUT_LANE}
 
 
 class ExternalEvaluatorSearch:
@@ -56,7 +57,8 @@ class ExternalEvaluatorSearch:
   def run(self, root_actions, root_offsets, bot_seeds, evaluator, puct=True,
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
           dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False,
-          bot_rng=None, requests="fused", graph=False, graph_batch=8, block_size=0):
+          bot_rng=None, requests="fused", graph=False, graph_batch=8, block_size=0,
+          layout="auto"):
     """Runs every search to completion; returns the os_mcts_batch outputs.
 
     The evaluator may be called once more after the last step, with every
@@ -68,6 +70,9 @@ class ExternalEvaluatorSearch:
     dirichlet_alpha / dirichlet_epsilon are the MCTSBot constructor's
     (mcts.h:152-159): root priors become (1 - eps) * p + eps * Dir(alpha)
     noise drawn from the bot's rng before the root's shuffle (mcts.cc:265-273).
+    layout: "wave" (k_waz_step, one wavefront per search), "lane" (k_az_step,
+    one lane per search; the only one with GC) or "auto" (wave unless the node
+    budget can be reached).  Same results.
     block_size: searches per k_az_step workgroup (one wave; 64 when 0).
     time_steps: record a HIP event pair around every k_az_step launch on the
     launch stream (`step_ms()` then sums them).
@@ -97,6 +102,9 @@ class ExternalEvaluatorSearch:
     if requests not in _REQUESTS:
       raise ValueError("requests must be 'fused' or 'separate'")
     check(lib.os_az_set_requests(self.eng._h, _REQUESTS[requests]))
+    if layout not in _LAYOUTS:
+      raise ValueError("layout must be 'auto', 'wave' or 'lane'")
+    check(lib.os_az_set_layout(self.eng._h, _LAYOUTS[layout]))
     if bot_rng is None:
       bs = _lib.u32(bot_seeds)
       check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),

@@ -199,7 +199,7 @@ def test_gpu_graph_replayed_rounds_match_oracle(require_gpu, game):
       np.testing.assert_array_equal(got[k], r, err_msg="%s graph=%s" % (k, graph))
 
 
-def _check_gpu(game, puct, alpha=0.0, eps=0.0, requests="fused"):
+def _check_gpu(game, puct, alpha=0.0, eps=0.0, requests="fused", layout="auto"):
   from os_amd.az import ExternalEvaluatorSearch
   acts, offs, seeds, sims = _roots(game)
   og = oracle_lib.Game(game)
@@ -210,7 +210,7 @@ def _check_gpu(game, puct, alpha=0.0, eps=0.0, requests="fused"):
   search = ExternalEvaluatorSearch(game)
   got = search.run(acts, offs, seeds, _gpu_toy_evaluator(A), puct=puct, uct_c=1.5,
                    max_simulations=sims, dirichlet_alpha=alpha, dirichlet_epsilon=eps,
-                   requests=requests)
+                   requests=requests, layout=layout)
   mc = search.eng.max_children
   for k in E.OUTPUT_KEYS:
     r = ref[k][:, :mc] if ref[k].ndim == 2 else ref[k]
@@ -218,17 +218,21 @@ def _check_gpu(game, puct, alpha=0.0, eps=0.0, requests="fused"):
   assert search.requests > 0
 
 
+# Both kernels: k_waz_step (one wave per search, the default) and k_az_step
+# (one lane per search).
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["wave", "lane"])
 @pytest.mark.parametrize("requests", ["fused", "separate"])
 @pytest.mark.parametrize("puct", [True, False])
 @pytest.mark.parametrize("game", sorted(CASES))
-def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct, requests):
-  _check_gpu(game, puct, requests=requests)
+def test_gpu_external_evaluator_matches_oracle(require_gpu, game, puct, requests, layout):
+  _check_gpu(game, puct, requests=requests, layout=layout)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["wave", "lane"])
 @pytest.mark.parametrize("requests", ["separate", "fused"])
-def test_gpu_external_evaluator_many_roots(require_gpu, requests):
+def test_gpu_external_evaluator_many_roots(require_gpu, requests, layout):
   # 160 searches: several waves, every lane of a wave64 (the small cases
   # above run <= 3 roots, all in lanes 0-2).
   from os_amd.az import ExternalEvaluatorSearch
@@ -241,7 +245,7 @@ def test_gpu_external_evaluator_many_roots(require_gpu, requests):
             dirichlet_epsilon=0.25)
   ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=7, **kw)
   got = ExternalEvaluatorSearch(game).run(acts, offs, seeds, _gpu_toy_evaluator(7),
-                                          requests=requests, **kw)
+                                          requests=requests, layout=layout, **kw)
   bad = sorted({int(r) for k in E.OUTPUT_KEYS
                 for r in np.nonzero((got[k] != ref[k]).reshape(R, -1).any(axis=1))[0]})
   assert not bad, "roots differing from the oracle: %s" % bad
@@ -268,6 +272,27 @@ def test_gpu_fused_requests_halve_the_rounds(require_gpu):
 def test_gpu_external_evaluator_dirichlet_matches_oracle(require_gpu, game, noise):
   _check_gpu(game, True, *noise)
   _check_gpu(game, True, *noise, requests="separate")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("game,sims", [("connect_four", 6000)])
+def test_gpu_gc_budget_runs_the_lane_kernel(require_gpu, game, sims):
+  """A node budget GC can reach: `auto` takes k_az_step (GC, mcts.cc:402-424),
+  `wave` is refused."""
+  from os_amd.az import ExternalEvaluatorSearch
+  acts, offs = E.roots_from_histories([[]])
+  seeds = np.array([3], np.uint32)
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  kw = dict(puct=True, uct_c=1.5, max_simulations=sims, max_memory_mb=1)
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=A, **kw)
+  search = ExternalEvaluatorSearch(game)
+  got = search.run(acts, offs, seeds, _torch_toy_evaluator(A), **kw)
+  for k in E.OUTPUT_KEYS:
+    r = ref[k][:, :search.eng.max_children] if ref[k].ndim == 2 else ref[k]
+    np.testing.assert_array_equal(got[k], r, err_msg=k)
+  with pytest.raises(ValueError):
+    search.run(acts, offs, seeds, _torch_toy_evaluator(A), layout="wave", **kw)
 
 
 @pytest.mark.gpu
