@@ -238,8 +238,6 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
   // a deeper tree fails the search with kPathOverflow).
   if (e->game.cfg.max_game_length >= kMaxPath && e->game.cfg.kind != kPig)
     return Fail(OS_ERR_UNSUPPORTED, "game exceeds kMaxPath");
-  if (e->game.cfg.kind == kPig && p->layout == OS_LAYOUT_WAVE)
-    return Fail(OS_ERR_UNSUPPORTED, "games with chance nodes run the lane layout only");
   if (p->child_selection != OS_SELECT_UCT && p->child_selection != OS_SELECT_PUCT)
     return Fail(OS_ERR_INVALID, "unknown child_selection");
   if (search && e->game.cfg.kind == kGo && p->layout == OS_LAYOUT_LANE &&

@@ -453,6 +453,214 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
 }
 
 
+// ---------------------------------------------------------------------------
+// Games with chance nodes on the wave layout (mcts.cc:
+// 285-296): one wave per search running os_chance.h's mcts_search_chance
+// WAVE-UNIFORMLY -- every lane executes the same scalar program on the same
+// values (the MT19937 streams are WaveMt windows in LDS, drawn by readlane;
+// path and expansion buffer in LDS; identical stores from all lanes).  pig
+// offers two actions and six chance outcomes per node and plays its rollouts
+// serially, so there is no data parallelism to spread over lanes; the wave
+// form gives one search per wave (a small batch spreads over every SIMD) and
+// the wave self-play kernel below.  Bit-exact with the oracle's MCTSBot.
+template <class G, class R>
+__host__ __device__ constexpr size_t WaveChanceLdsBytes(int path_cap) {
+  return static_cast<size_t>(2 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+         static_cast<size_t>(kMaxChildren) * 2;
+}
+
+template <class G, class R, int Policy>
+__global__ __launch_bounds__(64) void k_wsearch_chance(DevArgs a) {
+  const int64_t lr = blockIdx.x;
+  if (lr >= a.num_roots) return;
+  const int64_t gr = a.root_base + lr;
+  const int l = lane_id();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 2 * kMtN * 4);
+  uint16_t* actbuf = reinterpret_cast<uint16_t*>(smem + 2 * kMtN * 4 +
+                                                 a.path_cap * sizeof(PathEnt<R>));
+  const bool shared = Policy == kPolicyNumpy && a.shared_stream;
+  WaveMt bot, ev;
+  bot.s = mt;
+  ev.s = mt + kMtN;
+  bot.use7 = ev.use7 = 0;
+  if (a.import_state) {
+    const uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = l; i < 2 * kMtN; i += 64) mt[i] = g0[i];
+    __syncthreads();
+    bot.init_import(a.mt_pos[2 * gr]);
+    ev.init_import(a.mt_pos[2 * gr + 1]);
+  } else {
+    if (l == 0) {
+      mt_seed(bot.s, a.bot_seeds[gr]);
+      if (!shared) mt_seed(ev.s, a.eval_seeds[gr]);
+    }
+    __syncthreads();
+    bot.init_seeded();
+    ev.init_seeded();
+  }
+  const typename G::State root = make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
+  typename G::Ctx ctx;
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  SearchResult res = shared
+      ? mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
+                                         actbuf, a.path_cap)
+      : mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                                         actbuf, a.path_cap);
+  res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
+  __threadfence_block();
+  const Node<R> rn = nodes[0];
+  const int P0 = G::to_move(root);
+  const int nc = rn.nchild;
+  const int64_t ob = gr * a.max_children;
+  for (int k = l; k < nc && k < a.max_children; k += 64) {
+    const Node<R> c = nodes[rn.first + k];
+    a.child_action[ob + k] = c.action;
+    a.child_n[ob + k] = c.n;
+    a.child_w[ob + k] = static_cast<double>(c.w);
+    a.child_out[ob + k] = out_sign<G>(c.out, P0, a.cfg);
+  }
+  if (l == 0) {
+    a.results[gr] = res;
+    a.nchild[gr] = nc;
+    a.root_n[gr] = rn.n;
+    a.root_w[gr] = static_cast<double>(rn.w);
+    a.root_out[gr] = out_sign<G>(rn.out, P0, a.cfg);
+    const int b = best_child_g<G>(nodes, P0, a.cfg);
+    a.best_action[gr] = b < 0 ? -1 : nodes[rn.first + b].action;
+  }
+  if (a.import_state) {
+    if (l == 0) {
+      a.mt_pos[2 * gr] = bot.export_pos();
+      if (!shared) a.mt_pos[2 * gr + 1] = ev.export_pos();
+    }
+    __syncthreads();
+    uint32_t* g0 = a.mt + lr * 2 * kMtN;
+    for (int i = l; i < 2 * kMtN; i += 64) g0[i] = mt[i];
+  }
+}
+
+// Self-play of a two-player game with chance nodes, one game per wave, as
+// examples/mcts_example.cc:77-136 PlayGame drives it: decision nodes ask
+// bots[CurrentPlayer]->Step (mcts_search_chance + BestChild, mcts.cc:219-226),
+// chance nodes take SampleAction(ChanceOutcomes(), rng) (:103-109) with the
+// game's own rng -- actor_seeds[g] (as alpha_zero.cc PlayGame's one rng).
+// Every action (chance outcomes included) is recorded; visit rows are zero
+// for chance moves.  Wave-uniform, like k_wsearch_chance.
+template <class G, class R>
+__host__ __device__ constexpr size_t SelfPlayChanceLdsBytes(int path_cap) {
+  return static_cast<size_t>(4 * kMtN * 4) + static_cast<size_t>(path_cap) * sizeof(PathEnt<R>) +
+         static_cast<size_t>(kMaxChildren) * 2;
+}
+
+template <class G, class R>
+__global__ __launch_bounds__(64) void k_wselfplay_chance(SpArgs a) {
+  const int64_t lg = blockIdx.x;
+  if (lg >= a.num_games) return;
+  const int64_t gg = a.game_base + lg;
+  const int l = lane_id();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);
+  PathEnt<R>* path = reinterpret_cast<PathEnt<R>*>(smem + 4 * kMtN * 4);
+  uint16_t* actbuf = reinterpret_cast<uint16_t*>(smem + 4 * kMtN * 4 +
+                                                 a.path_cap * sizeof(PathEnt<R>));
+  WaveMt b0, b1, ev, act;
+  b0.s = mt;
+  b1.s = mt + kMtN;
+  ev.s = mt + 2 * kMtN;
+  act.s = mt + 3 * kMtN;
+  b0.use7 = b1.use7 = ev.use7 = act.use7 = 0;
+  if (l == 0) {
+    mt_seed(b0.s, a.bot_seeds[2 * gg]);
+    mt_seed(b1.s, a.bot_seeds[2 * gg + 1]);
+    mt_seed(ev.s, a.eval_seeds[gg]);
+    mt_seed(act.s, a.actor_seeds[gg]);
+  }
+  __syncthreads();
+  b0.init_seeded();
+  b1.init_seeded();
+  ev.init_seeded();
+  act.init_seeded();
+  typename G::State s = make_uniform(static_cast<const typename G::State*>(a.starts)[gg]);
+  typename G::Ctx ctx;
+  Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lg * static_cast<int64_t>(a.cap);
+  SearchResult tot;
+  tot.status = kOk;
+  tot.sims = tot.nodes = tot.gc_runs = tot.max_depth = 0;
+  tot.used = tot.scanned = tot.backed = tot.expanded = tot.solver_scanned = 0;
+  tot.rng_words = tot.pad = 0;
+  int m = 0;
+  while (!G::terminal(s, a.cfg)) {
+    if (m >= a.max_len) {
+      tot.status = kGameOverflow;
+      break;
+    }
+    const typename G::Legal lgl = G::legal(s, a.cfg, ctx);
+    int act_i;
+    if (G::chance(s)) {
+      act_i = lgl.kth(sample_chance<G, kPolicyCpp>(a.cfg, act));
+      if (a.visits) {
+        int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+        for (int i = l; i < a.num_actions; i += 64) v[i] = 0;
+      }
+    } else {
+      const int p = G::to_move(s);
+      WaveMt bot = p == 0 ? b0 : b1;
+      const SearchResult r = mcts_search_chance<G, R, kPolicyCpp>(
+          a.cfg, a.sp, s, ctx, nodes, a.cap, bot, ev, path, actbuf, a.path_cap);
+      if (p == 0) b0 = bot;
+      else b1 = bot;
+      tot.sims += r.sims;
+      tot.nodes += r.nodes;
+      tot.used = r.used > tot.used ? r.used : tot.used;
+      tot.gc_runs += r.gc_runs;
+      tot.max_depth = r.max_depth > tot.max_depth ? r.max_depth : tot.max_depth;
+      tot.scanned += r.scanned;
+      tot.backed += r.backed;
+      tot.expanded += r.expanded;
+      tot.solver_scanned += r.solver_scanned;
+      if (r.status != kOk) {
+        tot.status = r.status;
+        break;
+      }
+      __threadfence_block();
+      const int b = best_child_g<G>(nodes, p, a.cfg);  // MCTSBot::Step (mcts.cc:222-225)
+      const uint32_t rfirst = nodes[0].first;
+      const int rnc = nodes[0].nchild;
+      act_i = nodes[rfirst + b].action;
+      if (a.visits) {
+        int32_t* v = a.visits + (gg * a.max_len + m) * static_cast<int64_t>(a.num_actions);
+        for (int i = l; i < a.num_actions; i += 64) v[i] = 0;
+        __threadfence_block();
+        for (int k = l; k < rnc; k += 64) {
+          const Node<R> c = nodes[rfirst + k];
+          v[c.action] = c.n;
+        }
+      }
+      if (a.obs) {  // ObservationTensor(player to move) of the position searched
+        float* o = a.obs + (gg * a.max_len + m) * static_cast<int64_t>(a.obs_size);
+        const int cells = a.cfg.rows * a.cfg.cols;
+        for (int i = l; i < a.obs_size; i += 64) o[i] = G::obs(s, a.cfg, p, i / cells, i % cells);
+      }
+    }
+    if (l == 0) a.actions[gg * a.max_len + m] = act_i;
+    G::apply(s, a.cfg, ctx, act_i);
+    s = make_uniform(s);
+    ++m;
+  }
+  for (int i = m + l; i < a.max_len; i += 64) a.actions[gg * a.max_len + i] = -1;
+  if (l == 0) {
+    a.length[gg] = m;
+    const int code = G::ret0(s, a.cfg, ctx);
+    a.returns[2 * gg] = OutValue<G>::value(code, 0, a.cfg);
+    a.returns[2 * gg + 1] = OutValue<G>::value(code, 1, a.cfg);
+    tot.rng_words = b0.words.get() + b1.words.get() + ev.words.get() + act.words.get();
+    a.results[gg] = tot;
+  }
+}
+
+
 template <class G>
 struct SpCtx {  // games without a history context
   __device__ static NoCtx make(const SpArgs&, int64_t) { return NoCtx(); }
@@ -1483,9 +1691,24 @@ int LaunchSearchOnly(os_engine* e, const DevArgs& a, hipStream_t stream) {
 template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   if constexpr (HasChance<G>::value) {
-    if (e->params.layout == OS_LAYOUT_WAVE)
-      return Fail(OS_ERR_UNSUPPORTED, "games with chance nodes run the lane layout only");
     if (a.path_cap > kChancePathCap) a.path_cap = kChancePathCap;
+    if (e->params.layout == OS_LAYOUT_WAVE) {
+      if (a.pages) return Fail(OS_ERR_UNSUPPORTED, "paged arena on the chance-node wave layout");
+      const size_t lds = WaveChanceLdsBytes<G, R>(a.path_cap);
+      if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
+      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds)));
+      for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+        const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+        a.root_base = base;
+        a.num_roots = n;
+        hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy>), dim3(static_cast<unsigned>(n)),
+                           dim3(64), lds, stream, a);
+        HIP_TRY(hipGetLastError());
+      }
+      return OS_OK;
+    }
   } else {
     if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);
   }
@@ -1572,6 +1795,22 @@ int SpLaunch(os_engine* e, hipStream_t stream) {
   a.max_utility = 1.0;  // every self-play game: Game::MaxUtility() == 1
   a.policy = e->sp_policy ? static_cast<double*>(e->d_sp_pol.p) : nullptr;
   a.root_value = e->sp_values ? static_cast<double*>(e->d_sp_val.p) : nullptr;
+  if constexpr (HasChance<G>::value) {
+    if (a.path_cap > kChancePathCap) a.path_cap = kChancePathCap;
+    const size_t lds = SelfPlayChanceLdsBytes<G, R>(a.path_cap);
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay_chance<G, R>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(lds)));
+    for (int64_t base = 0; base < e->sp_games; base += e->chunk_roots) {
+      const int64_t n = std::min<int64_t>(e->chunk_roots, e->sp_games - base);
+      a.game_base = base;
+      a.num_games = n;
+      hipLaunchKernelGGL((k_wselfplay_chance<G, R>), dim3(static_cast<unsigned>(n)), dim3(64),
+                         lds, stream, a);
+      HIP_TRY(hipGetLastError());
+    }
+    return OS_OK;
+  } else {
   const size_t lds = SelfPlayLdsBytes<G, R>(a.path_cap);
   if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "self-play LDS slice exceeds the CU's LDS");
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wselfplay<G, R, kPuct>),
@@ -1586,6 +1825,7 @@ int SpLaunch(os_engine* e, hipStream_t stream) {
     HIP_TRY(hipGetLastError());
   }
   return OS_OK;
+  }
 }
 
 // ---- external-evaluator search (os_az_*) ----
@@ -1724,9 +1964,22 @@ static int PhaseCycles(uint64_t*, bool) {
 
 template <class G>
 int SelfPlayEntry(os_engine* e, hipStream_t stream) {
-  if constexpr (HasChance<G>::value)
-    return Fail(OS_ERR_UNSUPPORTED, "self-play of games with chance nodes");
-  else
+  if constexpr (HasChance<G>::value) {
+    // mcts_example.cc PlayGame over two MCTSBots; chance outcomes from the
+    // game's rng (actor seeds).  AlphaZero's move choice is not offered here.
+    if (e->game.cfg.pig_players != 2)
+      return Fail(OS_ERR_UNSUPPORTED, "self-play of chance games runs two players "
+                                      "(mcts_example.cc:148-150)");
+    if (e->sp_actor_seeds.empty())
+      return Fail(OS_ERR_INVALID, "games with chance nodes need os_selfplay_set_options actor "
+                                  "seeds: the PlayGame rng that samples chance outcomes");
+    if (e->sp_opts.temperature > 0.0 || e->sp_opts.resign || e->sp_policy || e->sp_values)
+      return Fail(OS_ERR_UNSUPPORTED, "AlphaZero move choice / targets on chance games");
+    const bool puct = e->params.child_selection == OS_SELECT_PUCT;
+    if (e->node_double)
+      return puct ? SpLaunch<G, double, true>(e, stream) : SpLaunch<G, double, false>(e, stream);
+    return puct ? SpLaunch<G, int32_t, true>(e, stream) : SpLaunch<G, int32_t, false>(e, stream);
+  } else
   {
     const bool puct = e->params.child_selection == OS_SELECT_PUCT;
     if (e->params.n_rollouts != 1)

@@ -7,8 +7,9 @@ and the unmodified reference mcts.py pins on the numpy path
     random games; the search engine compiled for the host (csrc/os_chance.h)
     equals the oracle's MCTSBot / numpy bot; product rollouts equal the
     oracle's RandomRolloutEvaluator.
-  * GPU: the same through the lane-layout kernel, the rollout kernel and the
-    Python MCTSBot drop-ins.
+  * GPU: the same through the lane-layout and wave-layout search kernels, the
+    rollout kernel, self-play with chance outcomes and the Python MCTSBot
+    drop-ins.
 """
 import numpy as np
 import pytest
@@ -185,13 +186,68 @@ def test_gpu_rollouts_match_oracle(require_gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_wave_layout_is_refused(require_gpu):
+@pytest.mark.parametrize("gs", PIGS)
+@pytest.mark.parametrize("policy", ["cpp", "numpy"])
+def test_gpu_wave_layout_matches_oracle(require_gpu, gs, policy):
+  """One wave per search (k_wsearch_chance, wave-uniform mcts_search_chance)."""
   from os_amd import _lib
+  R = 40
+  acts, offs = _roots(gs, R)
+  bs = np.arange(R, dtype=np.uint32) * 7 + 2
+  es = bs + np.uint32(1 << 20)
+  eng = E.Engine(gs)
+  kw = dict(max_simulations=250, layout=_lib.LAYOUT_WAVE)
+  if policy == "cpp":
+    ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_simulations=250, max_children=6)
+    got = eng.mcts_batch(acts, offs, bs, es, **kw)
+  else:
+    ref = H.mcts_batch(gs, acts, offs, bs, es, 6, max_simulations=250,
+                       policy=_lib.POLICY_NUMPY)
+    got = eng.mcts_batch(acts, offs, bs, es, policy=_lib.POLICY_NUMPY, **kw)
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(got[k], ref[k][:, :got[k].shape[1]] if ref[k].ndim == 2
+                                  else ref[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gs,sims,nr", [("pig(winscore=20)", 120, 1),
+                                        ("pig(horizon=30,winscore=8)", 200, 2)])
+def test_gpu_selfplay_with_chance_nodes_matches_oracle(require_gpu, gs, sims, nr):
+  """k_wselfplay_chance: mcts_example.cc PlayGame with chance outcomes drawn
+  by the game's rng (actor seed) -- every game equals the oracle's EvaluateBots
+  (evaluate_bots.cc:24-61) with bots (b0, b1), evaluator seed e and chance rng
+  seed = the actor seed."""
+  G = 6
+  acts, offs = E.roots_from_histories([[]] * G)
+  bot = np.array([[3 * g + 1, 3 * g + 2] for g in range(G)], np.uint32)
+  ev = np.arange(G, dtype=np.uint32) + 100
+  actor = np.arange(G, dtype=np.uint32) * 11 + 5
+  eng = E.Engine(gs)
+  L = 600
+  eng.selfplay_set_options(actor_seeds=actor)
+  out = eng.selfplay(acts, offs, bot, ev, max_len=L, max_simulations=sims, n_rollouts=nr,
+                     record_visits=True)
+  for g in range(G):
+    hist, ret = O.evaluate_mcts_bots(gs, [int(bot[g, 0]), int(bot[g, 1])], nr, int(ev[g]),
+                                     int(actor[g]), uct_c=2.0, max_simulations=sims,
+                                     max_memory_mb=1000)
+    n = int(out["length"][g])
+    assert list(out["actions"][g, :n]) == hist, g
+    assert list(out["returns"][g]) == ret, g
+    # visit targets on decision moves only
+    st = pyspiel.load_game(gs).new_initial_state()
+    for m, a in enumerate(hist):
+      row = out["visits"][g, m]
+      assert (row.sum() == 0) == st.is_chance_node()
+      st.apply_action(a)
+
+
+@pytest.mark.gpu
+def test_gpu_selfplay_with_chance_nodes_needs_actor_seeds(require_gpu):
   eng = E.Engine("pig")
-  acts, offs = _roots("pig", 4)
-  with pytest.raises(ValueError):
-    eng.mcts_batch(acts, offs, np.arange(4, dtype=np.uint32), np.arange(4, dtype=np.uint32),
-                   max_simulations=10, layout=_lib.LAYOUT_WAVE)
+  acts, offs = E.roots_from_histories([[]])
+  with pytest.raises(Exception):
+    eng.selfplay(acts, offs, [[1, 2]], [3], max_len=400, max_simulations=10)
 
 
 @pytest.mark.gpu
