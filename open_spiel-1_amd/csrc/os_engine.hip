@@ -401,6 +401,71 @@ void UpdateArenaHint(os_engine* e) {
   h.page_nodes = pn;
 }
 
+// Parent-count LUT from the host libm, N in [0, sims + 1]: UCTValue's
+// std::log(parent_explore_count) (mcts.cc:99), or PUCTValue's
+// std::sqrt(parent_explore_count) (mcts.cc:109).  Uploaded only when the
+// simulation count or the selection changed.
+int UploadLut(os_engine* e, int32_t sims, bool puct) {
+  const size_t n = static_cast<size_t>(sims) + 2;
+  int rc;
+  if ((rc = e->d_lut.ensure(n * 8))) return rc;
+  if (e->lut_at == e->d_lut.p && e->lut_n == static_cast<int64_t>(n) &&
+      e->lut_puct == (puct ? 1 : 0))
+    return OS_OK;
+  std::vector<double> lut(n);
+  for (size_t i = 0; i < n; ++i)
+    lut[i] = puct ? std::sqrt(static_cast<double>(i)) : std::log(static_cast<double>(i));
+  HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), n * 8, hipMemcpyHostToDevice));
+  e->lut_at = e->d_lut.p;
+  e->lut_n = static_cast<int64_t>(n);
+  e->lut_puct = puct ? 1 : 0;
+  return OS_OK;
+}
+
+// go's Zobrist table, uploaded once per engine.
+int UploadZob(os_engine* e) {
+  int rc;
+  if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
+  if (e->zob_at == e->d_zob.p) return OS_OK;
+  HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
+                    hipMemcpyHostToDevice));
+  e->zob_at = e->d_zob.p;
+  return OS_OK;
+}
+
+// Batched small copies through the engine's pinned staging buffer: queued on
+// the null stream, then one wait.
+struct Stager {
+  os_engine* e;
+  size_t off = 0;
+  explicit Stager(os_engine* eng) : e(eng) {}
+  int reserve(size_t bytes) {
+    // The staging buffer is only reused after the previous batch was waited for.
+    return e->h_stage.ensure(std::max<size_t>(bytes, 64 << 10));
+  }
+  unsigned char* slot(size_t bytes) {
+    unsigned char* q = e->h_stage.p + off;
+    off += (bytes + 255) & ~size_t(255);
+    return q;
+  }
+  int up(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return OS_OK;
+    unsigned char* q = slot(bytes);
+    std::memcpy(q, src, bytes);
+    HIP_TRY(hipMemcpyAsync(dst, q, bytes, hipMemcpyHostToDevice, nullptr));
+    return OS_OK;
+  }
+  int down(unsigned char** q, const void* src, size_t bytes) {
+    *q = slot(bytes);
+    if (bytes) HIP_TRY(hipMemcpyAsync(*q, src, bytes, hipMemcpyDeviceToHost, nullptr));
+    return OS_OK;
+  }
+  int wait() {
+    HIP_TRY(hipStreamSynchronize(nullptr));
+    return OS_OK;
+  }
+};
+
 // Uploads roots / seeds, sizes and allocates the arena and outputs.
 int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
             const int64_t* root_actions, const int64_t* root_offsets,
@@ -454,31 +519,24 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   }
   const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
   if ((rc = e->d_roots.ensure(Rz * sb))) return rc;
-  HIP_TRY(hipMemcpy(e->d_roots.p, roots.data(), Rz * sb, hipMemcpyHostToDevice));
   if ((rc = e->d_bseed.ensure(Rz * 4)) || (rc = e->d_eseed.ensure(Rz * 4))) return rc;
-  if (R > 0) {
-    HIP_TRY(hipMemcpy(e->d_bseed.p, bot_seeds, R * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(e->d_eseed.p, eval_seeds ? eval_seeds : bot_seeds, R * 4,
-                      hipMemcpyHostToDevice));
-  }
-  if (go) {
-    if ((rc = e->d_rhash.ensure(rh.size() * 8)) || (rc = e->d_rnh.ensure(rnh.size() * 4)))
+  if (go && ((rc = e->d_rhash.ensure(rh.size() * 8)) || (rc = e->d_rnh.ensure(rnh.size() * 4))))
+    return rc;
+  {
+    Stager st(e);
+    const size_t need = Rz * sb + 2 * Rz * 4 + (go ? rh.size() * 8 + rnh.size() * 4 : 0) +
+                        6 * 256;
+    if ((rc = st.reserve(need)) || (rc = st.up(e->d_roots.p, roots.data(), Rz * sb))) return rc;
+    if (R > 0 && ((rc = st.up(e->d_bseed.p, bot_seeds, R * 4)) ||
+                  (rc = st.up(e->d_eseed.p, eval_seeds ? eval_seeds : bot_seeds, R * 4))))
       return rc;
-    HIP_TRY(hipMemcpy(e->d_rhash.p, rh.data(), rh.size() * 8, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(e->d_rnh.p, rnh.data(), rnh.size() * 4, hipMemcpyHostToDevice));
-    if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
-    HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
-                      hipMemcpyHostToDevice));
+    if (go && ((rc = st.up(e->d_rhash.p, rh.data(), rh.size() * 8)) ||
+               (rc = st.up(e->d_rnh.p, rnh.data(), rnh.size() * 4))))
+      return rc;
+    if ((rc = st.wait())) return rc;
   }
-  // Parent-count LUT from the host libm, N in [0, max_simulations]: UCTValue's
-  // std::log(parent_explore_count) (mcts.cc:99), or PUCTValue's
-  // std::sqrt(parent_explore_count) (mcts.cc:109).
-  std::vector<double> lut(static_cast<size_t>(p->max_simulations) + 2);
-  const bool puct = p->child_selection == OS_SELECT_PUCT;
-  for (size_t i = 0; i < lut.size(); ++i)
-    lut[i] = puct ? std::sqrt(static_cast<double>(i)) : std::log(static_cast<double>(i));
-  if ((rc = e->d_lut.ensure(lut.size() * 8))) return rc;
-  HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice));
+  if (go && (rc = UploadZob(e))) return rc;
+  if ((rc = UploadLut(e, p->max_simulations, p->child_selection == OS_SELECT_PUCT))) return rc;
   // Work buffers.
   const size_t C = static_cast<size_t>(e->chunk_roots);
   if ((rc = e->d_mt.ensure(C * 2 * kMtN * 4))) return rc;
@@ -571,18 +629,28 @@ int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
   }
   UpdateArenaHint(e);
   const int mcd = e->max_children;
-  std::vector<int32_t> ca(R * mcd), cn(R * mcd);
-  std::vector<double> cw(R * mcd);
-  std::vector<int8_t> co(R * mcd);
-  HIP_TRY(hipMemcpy(ca.data(), e->d_cact.p, ca.size() * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(cn.data(), e->d_cn.p, cn.size() * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(cw.data(), e->d_cw.p, cw.size() * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(co.data(), e->d_cout.p, co.size(), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(nchild, e->d_nch.p, R * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(root_n, e->d_rn.p, R * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(root_w, e->d_rw.p, R * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(root_out, e->d_rout.p, R, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(best_action, e->d_best.p, R * 8, hipMemcpyDeviceToHost));
+  const size_t M = static_cast<size_t>(R) * mcd;
+  // One queue of device-to-pinned copies and one wait (a single bot's step
+  // fetches a few hundred bytes: the copies' fixed costs dominate).
+  Stager st(e);
+  unsigned char *ca8, *cn8, *cw8, *co8, *nch8, *rn8, *rw8, *ro8, *ba8;
+  int rc;
+  if ((rc = st.reserve(M * 17 + static_cast<size_t>(R) * 25 + 9 * 256)) ||
+      (rc = st.down(&ca8, e->d_cact.p, M * 4)) || (rc = st.down(&cn8, e->d_cn.p, M * 4)) ||
+      (rc = st.down(&cw8, e->d_cw.p, M * 8)) || (rc = st.down(&co8, e->d_cout.p, M)) ||
+      (rc = st.down(&nch8, e->d_nch.p, R * 4)) || (rc = st.down(&rn8, e->d_rn.p, R * 4)) ||
+      (rc = st.down(&rw8, e->d_rw.p, R * 8)) || (rc = st.down(&ro8, e->d_rout.p, R)) ||
+      (rc = st.down(&ba8, e->d_best.p, R * 8)) || (rc = st.wait()))
+    return rc;
+  const int32_t* ca = reinterpret_cast<const int32_t*>(ca8);
+  const int32_t* cn = reinterpret_cast<const int32_t*>(cn8);
+  const double* cw = reinterpret_cast<const double*>(cw8);
+  const int8_t* co = reinterpret_cast<const int8_t*>(co8);
+  std::memcpy(nchild, nch8, R * 4);
+  std::memcpy(root_n, rn8, R * 4);
+  std::memcpy(root_w, rw8, R * 8);
+  std::memcpy(root_out, ro8, R);
+  std::memcpy(best_action, ba8, R * 8);
   for (int64_t r = 0; r < R; ++r) {
     for (int k = 0; k < max_children; ++k) {
       const int64_t o = r * max_children + k;
@@ -685,21 +753,13 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
     HIP_TRY(hipMemcpy(e->d_bseed.p, bot_seeds, G * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_eseed.p, eval_seeds, G * 4, hipMemcpyHostToDevice));
   }
-  if (go) {
-    if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
-    HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
-                      hipMemcpyHostToDevice));
-  }
-  std::vector<double> lut(static_cast<size_t>(p->max_simulations) + 2);
-  const bool puct = p->child_selection == OS_SELECT_PUCT;
-  for (size_t i = 0; i < lut.size(); ++i)
-    lut[i] = puct ? std::sqrt(static_cast<double>(i)) : std::log(static_cast<double>(i));
-  if ((rc = e->d_lut.ensure(lut.size() * 8))) return rc;
-  HIP_TRY(hipMemcpy(e->d_lut.p, lut.data(), lut.size() * 8, hipMemcpyHostToDevice));
+  if (go && (rc = UploadZob(e))) return rc;
+  if ((rc = UploadLut(e, p->max_simulations, p->child_selection == OS_SELECT_PUCT))) return rc;
+  const size_t lut_n = static_cast<size_t>(p->max_simulations) + 2;
   // AlphaZero move choice: pow(explore_count, 1 / T) from the host libm
   // (alpha_zero.cc:82-83), and the actor rng seeds.
   if (e->sp_opts.temperature > 0.0) {
-    std::vector<double> pw(lut.size());
+    std::vector<double> pw(lut_n);
     const double ex = 1.0 / e->sp_opts.temperature;
     for (size_t i = 0; i < pw.size(); ++i) pw[i] = std::pow(static_cast<double>(i), ex);
     if ((rc = e->d_sp_pow.ensure(pw.size() * 8))) return rc;
@@ -712,6 +772,7 @@ int SpPrepare(os_engine* e, const os_mcts_params* p, int64_t G, const int64_t* s
   }
   const size_t L = static_cast<size_t>(std::max(max_len, 1));
   const size_t A = static_cast<size_t>(cfg.num_actions);
+  (void)lut_n;
   if ((rc = e->d_arena.ensure(static_cast<size_t>(e->chunk_roots) * per_game)) ||
       (rc = e->d_res.ensure(Gz * sizeof(SearchResult))) ||
       (rc = e->d_sp_act.ensure(Gz * L * 4)) || (rc = e->d_sp_len.ensure(Gz * 4)) ||
@@ -926,9 +987,7 @@ int RollPrepare(os_engine* e, const HostState& root, int64_t n, int32_t nr,
     if ((rc = e->d_glog.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 8)) ||
         (rc = e->d_glink.ensure(std::max<int64_t>(n, 1) * kGoLogCap * 4)))
       return rc;
-    if ((rc = e->d_zob.ensure(e->game.zob.size() * 8))) return rc;
-    HIP_TRY(hipMemcpy(e->d_zob.p, e->game.zob.data(), e->game.zob.size() * 8,
-                      hipMemcpyHostToDevice));
+    if ((rc = UploadZob(e))) return rc;
     if ((rc = e->d_rhash.ensure(std::max<size_t>(root.hashes.size(), 1) * 8))) return rc;
     HIP_TRY(hipMemcpy(e->d_rhash.p, root.hashes.data(), root.hashes.size() * 8,
                       hipMemcpyHostToDevice));
@@ -1230,24 +1289,36 @@ int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
   if (rc) return rc;
   e->import_state = true;
   e->shared_stream = shared != 0;
-  HIP_TRY(hipMemcpy(e->d_mt.p, bot_key, kMtN * 4, hipMemcpyHostToDevice));
   int32_t pos[2] = {*bot_pos, shared ? 0 : *eval_pos};
-  if (!shared)
-    HIP_TRY(hipMemcpy(static_cast<uint32_t*>(e->d_mt.p) + kMtN, eval_key, kMtN * 4,
-                      hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_pos.p, pos, 8, hipMemcpyHostToDevice));
+  {
+    Stager st(e);
+    if ((rc = st.reserve(2 * kMtN * 4 + 3 * 256)) ||
+        (rc = st.up(e->d_mt.p, bot_key, kMtN * 4)) ||
+        (!shared && (rc = st.up(static_cast<uint32_t*>(e->d_mt.p) + kMtN, eval_key, kMtN * 4))) ||
+        (rc = st.up(e->d_pos.p, pos, 8)))
+      return rc;
+    // No wait: the null stream runs these copies before the search kernel.
+  }
   if ((rc = Run(e, nullptr))) return rc;
   rc = Fetch(e, max_children, child_action, child_n, child_w, child_out, nchild, root_n,
              root_w, root_out, best_action, nodes);
   e->import_state = false;
   if (rc) return rc;
-  HIP_TRY(hipMemcpy(bot_key, e->d_mt.p, kMtN * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(pos, e->d_pos.p, 8, hipMemcpyDeviceToHost));
-  *bot_pos = pos[0];
-  if (!shared) {
-    HIP_TRY(hipMemcpy(eval_key, static_cast<uint32_t*>(e->d_mt.p) + kMtN, kMtN * 4,
-                      hipMemcpyDeviceToHost));
-    *eval_pos = pos[1];
+  {
+    Stager st(e);
+    unsigned char *bk, *ek = nullptr, *ps;
+    if ((rc = st.reserve(2 * kMtN * 4 + 3 * 256)) || (rc = st.down(&bk, e->d_mt.p, kMtN * 4)) ||
+        (!shared &&
+         (rc = st.down(&ek, static_cast<uint32_t*>(e->d_mt.p) + kMtN, kMtN * 4))) ||
+        (rc = st.down(&ps, e->d_pos.p, 8)) || (rc = st.wait()))
+      return rc;
+    std::memcpy(bot_key, bk, kMtN * 4);
+    std::memcpy(pos, ps, 8);
+    *bot_pos = pos[0];
+    if (!shared) {
+      std::memcpy(eval_key, ek, kMtN * 4);
+      *eval_pos = pos[1];
+    }
   }
   return OS_OK;
 }

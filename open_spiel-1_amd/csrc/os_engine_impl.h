@@ -232,6 +232,33 @@ struct DevBuf {
   }
 };
 
+// Pinned host staging for the per-call copies of small batches (a single
+// bot's step): copies into it are queued with hipMemcpyAsync and waited for
+// once, instead of one synchronous pageable hipMemcpy each.
+struct PinBuf {
+  unsigned char* p = nullptr;
+  size_t bytes = 0;
+  size_t used = 0;
+  int ensure(size_t b) {
+    if (b <= bytes && p) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return Fail(OS_ERR_DEVICE, std::string("hipHostMalloc failed: ") + hipGetErrorString(e));
+    }
+    bytes = b;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
 }  // namespace osx
 
 struct os_engine {
@@ -304,6 +331,13 @@ struct os_engine {
     uint32_t page_nodes = 0;
     double extra_per_root = 0.0;
   } arena_hint;
+  // Uploaded constants (LUT of the last prepared sims / selection, go's
+  // Zobrist table) and the pinned staging of per-call copies.
+  int64_t lut_n = -1;
+  int32_t lut_puct = -1;
+  const void* lut_at = nullptr;
+  const void* zob_at = nullptr;
+  osx::PinBuf h_stage;
   int64_t arena_reruns = 0;     // batches rerun on the reserved arena
   int64_t arena_overflows = 0;  // searches that ran out of pool pages
   ~os_engine() {
@@ -317,6 +351,7 @@ struct os_engine {
                      &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath, &d_lheads, &d_lact};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
+    h_stage.release();
   }
 };
 
