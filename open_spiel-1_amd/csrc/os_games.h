@@ -573,6 +573,12 @@ struct GoCtxT {
 using GoCtx = GoCtxT<uint8_t>;
 using GoCtxW = GoCtxT<uint16_t>;
 
+// 1: GoT::apply floods a chain only where its liberty count is unknown
+// (see apply); 0: every touched chain is flooded (the round-3 form).
+#ifndef OS_GO_LAZY_ATARI
+#define OS_GO_LAZY_ATARI 1
+#endif
+
 template <class B>
 struct GoT {
   using M = CfgMasks<B>;
@@ -660,7 +666,8 @@ struct GoT {
     } else {
       const B pb = BB<B>::bit(a);
       const B nb = nbr4(pb, g);
-      B own = pick(s.bw, c) | pb;
+      const B own0 = pick(s.bw, c);
+      B own = own0 | pb;
       B opp = pick(s.bw, 1 - c);
       const bool enemy_eye = !any(nb & ~opp);
       s.hash ^= ctx.zob[2 * a + c];
@@ -674,6 +681,60 @@ struct GoT {
       B atari = s.atari;
       B capd = BB<B>::zero();
       B on = nb & opp;
+#if OS_GO_LAZY_ATARI
+      // Full chain floods only where a liberty count is unknown.  A chain is in
+      // `atari` as a whole, and two same-coloured atari chains never touch, so
+      // flood(q, colour & atari) is q's chain whenever q is in atari -- a flood
+      // over the few atari stones, not the chain's whole extent.
+      //  * An opponent chain next to a that was in atari had a as its only
+      //    liberty: it is captured.  Otherwise it keeps >= 1 liberty (points
+      //    freed by this move's captures never touch it: they were stones of
+      //    its own colour), and it enters atari only if it had exactly two; a
+      //    stone of it with >= 2 empty neighbours after the move rules that out.
+      //  * The mover's new chain is out of atari if its new stone has >= 2 empty
+      //    neighbours; the chains it joined leave the atari set with it.
+      //  * Own chains next to captured stones gain liberties: any in atari had
+      //    exactly one and now have >= 2.
+      // Every other chain keeps its liberties.  Same set as the full update.
+      const B opp_at = opp & atari;
+      while (any(on)) {
+        const int q = lowest(on);
+        const B qb = BB<B>::bit(q);
+        if (any(qb & opp_at)) {
+          const B ch = flood(qb, opp_at, g);
+          on = on & ~ch;
+          opp = opp & ~ch;
+          E = E | ch;
+          capd = capd | ch;
+          captured += popc(ch);
+          cap_pt = q;
+          atari = atari & ~ch;
+          B rem = ch;
+          while (any(rem)) {
+            const int x = lowest(rem);
+            rem = rem & ~BB<B>::bit(x);
+            s.hash ^= ctx.zob[2 * x + (1 - c)];
+          }
+        } else if (popc(nbr4(qb, g) & E) >= 2) {
+          on = on & ~qb;
+        } else {
+          const B ch = flood(qb, opp, g);
+          on = on & ~ch;
+          atari = atari | BB<B>::sel(popc(nbr4(ch, g) & E) == 1, ch, BB<B>::zero());
+        }
+      }
+      const B own_at = own0 & atari;
+      B touched = (nb | nbr4(capd, g)) & own_at;
+      while (any(touched)) {
+        const B ch = flood(BB<B>::bit(lowest(touched)), own_at, g);
+        touched = touched & ~ch;
+        atari = atari & ~ch;
+      }
+      if (popc(nbr4(pb, g) & E) < 2) {
+        const B ch = flood(pb, own, g);
+        atari = atari | BB<B>::sel(popc(nbr4(ch, g) & E) == 1, ch, BB<B>::zero());
+      }
+#else
       while (any(on)) {
         const int q = lowest(on);
         const B ch = flood(BB<B>::bit(q), opp, g);
@@ -700,6 +761,7 @@ struct GoT {
         todo = todo & ~ch;
         atari = (atari & ~ch) | BB<B>::sel(popc(nbr4(ch, g) & E) == 1, ch, BB<B>::zero());
       }
+#endif
       s.atari = atari;
       s.bw[0] = c ? opp : own;
       s.bw[1] = c ? own : opp;

@@ -120,6 +120,18 @@ def test_rollouts_match_oracle(gs, plies):
   assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("gs", ["go(board_size=5,komi=0.5)", "go(board_size=7,komi=4.5)",
+                                "go(board_size=9)", "go(board_size=11)"])
+def test_go_playouts_match_oracle_many_seeds(gs):
+  """GoT::apply's atari set (os_games.h, lazy chain floods) decides legality in
+  every playout move: 1500 full random games per board from the empty board
+  and from a mid-game position equal the oracle's go_board.cc restatement."""
+  for plies in (0, 30):
+    acts, offs = _roots(gs, 1, plies, seed_base=11)
+    seeds = np.arange(1500, dtype=np.uint32) * 7 + 3
+    assert np.array_equal(H.rollouts(gs, acts, seeds), O.Game(gs).rollouts(acts, seeds))
+
+
 @pytest.mark.parametrize("gs", ["go(board_size=9)", "go(board_size=7,komi=4.5)",
                                 "go(board_size=11)"])
 def test_go_tromp_taylor_score_matches_oracle(gs):
