@@ -568,6 +568,69 @@ struct GoCtxT {
     return true;
   }
 };
+// The same set for one random playout (k_rollouts) screened by a per-lane
+// Bloom filter instead of stone-count buckets: a new position is compared with
+// the log only when both of its filter bits are set, and then only with the
+// entries logged before the most recent capture (without a capture the stone
+// count only grows, so no later position can repeat one -- go.cc:199-208 asks
+// the same question of a hash set).  A filter miss proves absence, so the
+// answers are exact; the log is written (8 B per move) but read almost never,
+// and no link words are kept.  Filter: kWords u32 per playout (1024 bits),
+// word w at filt[w * filt_stride] (LDS, lane-interleaved).  No rewind: each
+// playout starts from reset().
+struct GoCtxBloom {
+  static constexpr int kWords = 32;
+  const uint64_t* zob;
+  const uint64_t* base;   // hashes before the root
+  int32_t n_base;
+  uint64_t* log;          // [cap], element i at log[i * stride]
+  uint32_t* filt;         // [kWords], element w at filt[w * filt_stride]
+  int32_t stride;
+  int32_t filt_stride;
+  int32_t n_log;
+  int32_t cand_end;       // entries [0, cand_end) can repeat a new position
+  int32_t cap;
+  Filter256 base_filt;
+
+  OS_HD void reset() {
+    n_log = 0;
+    cand_end = 0;
+    for (int w = 0; w < kWords; ++w) filt[w * filt_stride] = 0u;
+  }
+  OS_HD void init_filters() {
+    base_filt.clear();
+    for (int i = 0; i < n_base; ++i) base_filt.add(GoCtxT<uint8_t>::fbit(base[i]));
+    reset();
+  }
+  OS_HD static int b0(uint64_t h) { return static_cast<int>(h & 1023u); }
+  OS_HD static int b1(uint64_t h) { return static_cast<int>((h >> 10) & 1023u); }
+  OS_HD bool contains(uint64_t h) const {
+    if (base_filt.has(GoCtxT<uint8_t>::fbit(h)))
+      for (int i = 0; i < n_base; ++i)
+        if (base[i] == h) return true;
+    if (cand_end == 0) return false;
+    const int x = b0(h), y = b1(h);
+    if (!((filt[(x >> 5) * filt_stride] >> (x & 31)) & 1u)) return false;
+    if (!((filt[(y >> 5) * filt_stride] >> (y & 31)) & 1u)) return false;
+    for (int e = 0; e < cand_end; ++e)
+      if (log[static_cast<int64_t>(e) * stride] == h) return true;
+    return false;
+  }
+  OS_HD bool insert(uint64_t h, bool captured, int stones) {
+    (void)stones;
+    if (captured) cand_end = n_log;
+    if (contains(h)) return false;
+    if (n_log < cap) {
+      log[static_cast<int64_t>(n_log) * stride] = h;
+      const int x = b0(h), y = b1(h);
+      filt[(x >> 5) * filt_stride] |= 1u << (x & 31);
+      filt[(y >> 5) * filt_stride] |= 1u << (y & 31);
+      ++n_log;
+    }
+    return true;
+  }
+};
+
 // u8 bucket heads (log cap <= 255: boards up to 11 x 11, and the host's
 // one-move logs); u16 heads for the longer logs of larger boards (k_lsearch).
 using GoCtx = GoCtxT<uint8_t>;

@@ -234,6 +234,27 @@ struct LCtx<Go> {
   }
 };
 
+// Timing-only attribution switches for k_lsearch's HBM traffic (results are
+// NOT the reference's; A/B builds only): bit 0 draws the MT19937 words from a
+// register xorshift (no stream memory), bit 1 logs no superko positions.
+#ifndef OS_LS_AB
+#define OS_LS_AB 0
+#endif
+struct MtStreamNoMem {
+  uint32_t x;
+  uint32_t words;
+  __device__ void seed(uint32_t v) { x = v * 2654435761u + 1u; words = 0; }
+  __device__ void init_import(int p) { x = 0x9e3779b9u + static_cast<uint32_t>(p); words = 0; }
+  __device__ uint32_t next() {
+    ++words;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    return x;
+  }
+  __device__ int finalize() const { return 0; }
+};
+
 template <class G, class R>
 __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   // LDS: go's bucket heads and the expansion buffers, lane-interleaved
@@ -252,8 +273,12 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   // Per-search contiguous buffers: the lanes of a wave drift apart (each at
   // its own draw count, log length and depth), so a batch-SoA layout would
   // touch a new cache line per word; contiguous, a search reuses its lines.
+#if OS_LS_AB & 1
+  MtStreamNoMem bot, ev;
+#else
   MtStreamPf bot{a.mt + lr * 2 * kMtN, 1, 0, 0};
   MtStreamPf ev{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0};
+#endif
   if (a.import_state) {  // the rows hold numpy-form keys (os_mcts_stateful)
     bot.init_import(a.mt_pos[2 * gr]);
     ev.init_import(a.mt_pos[2 * gr + 1]);
@@ -264,6 +289,9 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
   auto ctx = LCtx<G>::make(a, gr, lr, heads);
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
+#if OS_LS_AB & 2
+  if constexpr (G::State::kNeedsLog) ctx.cap = 0;
+#endif
   const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
   using N = Node<R, LsWide<G>::value>;
   N* nodes = static_cast<N*>(a.arena) + lr * static_cast<int64_t>(a.cap);
@@ -1470,16 +1498,51 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
 }
 
 
+// OS_ROLL_BLOOM: go playouts screen the superko log with a per-lane Bloom
+// filter in LDS (GoCtxBloom); 0: stone-count buckets (GoCtx).
+#ifndef OS_ROLL_BLOOM
+#define OS_ROLL_BLOOM 1
+#endif
 template <class G>
 struct RollCtx {
-  __device__ static NoCtx make(const RollArgs&, int64_t, uint8_t*) { return NoCtx(); }
+  using type = NoCtx;
+  static constexpr int kLdsWords = 1;
+  __device__ static NoCtx make(const RollArgs&, int64_t, uint32_t*) { return NoCtx(); }
 };
+#if OS_ROLL_BLOOM
 template <>
 struct RollCtx<Go> {
+  using type = GoCtxBloom;
+  static constexpr int kLdsWords = GoCtxBloom::kWords * 64;
+  __device__ static GoCtxBloom make(const RollArgs& a, int64_t i, uint32_t* lds) {
+    GoCtxBloom c;
+    c.zob = a.zob;
+    c.base = a.root_hashes;
+    c.n_base = a.n_root_hashes;
+#if OS_ROLL_AOS & 2
+    c.log = a.glog + i * kGoLogCap;
+    c.stride = 1;
+#else
+    c.log = a.glog + i;
+    c.stride = static_cast<int32_t>(a.n);
+#endif
+    c.filt = lds + (threadIdx.x & 63);
+    c.filt_stride = 64;
+    c.cap = kGoLogCap;
+    c.init_filters();
+    return c;
+  }
+};
+#else
+template <>
+struct RollCtx<Go> {
+  using type = GoCtx;
+  static constexpr int kLdsWords = (kGoHeads * 64 + 3) / 4;
   // The bucket heads are the only per-move accesses that differ across the
   // lanes (each lane is at its own stone count): they live in LDS, lane-
   // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
-  __device__ static GoCtx make(const RollArgs& a, int64_t i, uint8_t* lds_heads) {
+  __device__ static GoCtx make(const RollArgs& a, int64_t i, uint32_t* lds) {
+    uint8_t* lds_heads = reinterpret_cast<uint8_t*>(lds);
     GoCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes;
@@ -1502,6 +1565,7 @@ struct RollCtx<Go> {
     return c;
   }
 };
+#endif
 
 template <class G>
 struct WaveRollCtx {
@@ -1576,8 +1640,8 @@ __global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   RollMt ev{a.mt + i, a.n, 0, 0};
 #endif
   ev.seed(a.seeds[i]);
-  __shared__ uint8_t heads[G::State::kNeedsLog ? kGoHeads * 64 : 1];
-  typename G::Ctx ctx = RollCtx<G>::make(a, i, heads);
+  __shared__ uint32_t roll_lds[RollCtx<G>::kLdsWords];
+  typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
   uint32_t moves = 0;

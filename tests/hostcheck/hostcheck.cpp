@@ -446,4 +446,43 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
   return 0;
 }
 
+// The same go playouts with the k_rollouts superko screen (GoCtxBloom).
+int hc_rollouts_go_bloom(const char* game_string, const int64_t* actions, int64_t n_actions,
+                         int64_t n, const uint32_t* seeds, double* out) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty() || game.cfg.kind != kGo) {
+    g_err = err.empty() ? "go only" : err;
+    return -1;
+  }
+  HostState hs;
+  hs.game = &game;
+  StateInit(&hs);
+  for (int64_t i = 0; i < n_actions; ++i) StateApply(&hs, actions[i]);
+  std::vector<uint32_t> mt(kMtN);
+  std::vector<uint64_t> log(248);
+  std::vector<uint32_t> filt(GoCtxBloom::kWords);
+  for (int64_t i = 0; i < n; ++i) {
+    MtStream ev{mt.data(), kMtN, 0};
+    mt_seed(ev.s, seeds[i]);
+    GoCtxBloom c;
+    std::memset(&c, 0, sizeof c);
+    c.zob = game.zob.data();
+    c.base = hs.hashes.data();
+    c.n_base = static_cast<int32_t>(hs.hashes.size());
+    c.log = log.data();
+    c.stride = 1;
+    c.filt = filt.data();
+    c.filt_stride = 1;
+    c.cap = 248;
+    c.init_filters();
+    const int r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg,
+                                                c, ev);
+    out[2 * i] = r0;
+    out[2 * i + 1] = -r0;
+  }
+  return 0;
+}
+
 }  // extern "C"

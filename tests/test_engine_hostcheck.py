@@ -129,7 +129,10 @@ def test_go_playouts_match_oracle_many_seeds(gs):
   for plies in (0, 30):
     acts, offs = _roots(gs, 1, plies, seed_base=11)
     seeds = np.arange(1500, dtype=np.uint32) * 7 + 3
-    assert np.array_equal(H.rollouts(gs, acts, seeds), O.Game(gs).rollouts(acts, seeds))
+    ref = O.Game(gs).rollouts(acts, seeds)
+    assert np.array_equal(H.rollouts(gs, acts, seeds), ref)
+    # k_rollouts' Bloom-screened superko set gives the same playouts
+    assert np.array_equal(H.rollouts_go_bloom(gs, acts, seeds), ref)
 
 
 @pytest.mark.parametrize("gs", ["go(board_size=9)", "go(board_size=7,komi=4.5)",

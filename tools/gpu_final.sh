@@ -32,7 +32,7 @@ case "$part" in
       [ "$c" = az ] && EXTRA="--az-graph 0"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_$c" -o run \
         --output-format csv -- python3 "$R/bench.py" --config "$c" --steps 3 --warmup 1 \
-        --no-cpu-baseline --parity-roots 0 $EXTRA > "$OUT/rocprof_$c.log" 2>&1 || exit 1
+        --no-cpu-baseline --parity-roots 0 --no-parity-sweep $EXTRA > "$OUT/rocprof_$c.log" 2>&1 || exit 1
       echo "rocprof $c done"
     done
     ;;
