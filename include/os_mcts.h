@@ -448,6 +448,11 @@ const char* os_build_info(void);
  * Returns the number of phases written; OS_ERR_UNSUPPORTED unless the library
  * was built with -DOS_PHASE_TIMING=1. */
 int os_debug_phase_cycles(uint64_t* out, int32_t n);
+/* Diagnostic (no reference counterpart): the first `count` arena nodes
+ * (Node<double>, 24 B: first u32, n i32, w f64, action u16, nchild u8, out i8)
+ * and priors of search r of the prepared external-evaluator batch. */
+int os_debug_az_arena(os_engine* e, int64_t r, int32_t count, void* out_nodes,
+                      double* out_prior);
 
 #ifdef __cplusplus
 }

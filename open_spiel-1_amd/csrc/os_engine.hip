@@ -618,10 +618,11 @@ int Fetch(os_engine* e, int32_t max_children, int32_t* child_action,
   for (int64_t r = 0; r < R; ++r) {
     const SearchResult& s = e->last_results[r];
     if (s.status != kOk) {
-      const char* why = s.status == kArenaOverflow
+      const std::string why = s.status == kArenaOverflow
                             ? "node arena overflow (raise arena_nodes)"
                             : (s.status == kPathOverflow ? "tree path overflow"
-                                                         : "GC stack overflow");
+                               : s.status == kGcStackOverflow ? "GC stack overflow"
+                                 : "search status " + std::to_string(s.status));
       return Fail(OS_ERR_CAPACITY, "root " + std::to_string(r) + ": " + why);
     }
     e->last_sims += s.sims;
@@ -1020,6 +1021,23 @@ int RollRun(os_engine* e, hipStream_t stream) {
 extern "C" {
 
 const char* os_last_error(void) { return g_err.c_str(); }
+
+// Diagnostic (no reference counterpart): the first `count` arena nodes (24-B
+// Node<double>) and priors of external-evaluator search r, copied to the host.
+int os_debug_az_arena(os_engine* e, int64_t r, int32_t count, void* out_nodes,
+                      double* out_prior) {
+  if (!e || !e->az_ready || r < 0 || r >= e->num_roots || count < 0 ||
+      static_cast<uint32_t>(count) > e->cap)
+    return Fail(OS_ERR_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t nb = sizeof(Node<double>);
+  HIP_TRY(hipMemcpy(out_nodes, static_cast<unsigned char*>(e->d_arena.p) + r * e->cap * nb,
+                    count * nb, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out_prior, static_cast<double*>(e->d_az_prior.p) + r * e->cap, count * 8,
+                    hipMemcpyDeviceToHost));
+  return OS_OK;
+}
 
 int os_debug_phase_cycles(uint64_t* out, int32_t n) {
 #if OS_PHASE_TIMING || OS_WAVE_TIMES

@@ -1102,6 +1102,25 @@ struct WazPath {
   }
 };
 
+// OS_WAZ_CHECK (debug builds): every computed index of k_waz_step is checked
+// before use; a violation ends the search with status 100 + site instead of
+// touching memory out of range.
+#ifndef OS_WAZ_CHECK
+#define OS_WAZ_CHECK 0
+#endif
+#if OS_WAZ_CHECK
+#define WAZ_CHECK(cond, site)                                   \
+  do {                                                          \
+    if (ballot(!(cond))) {                                      \
+      res.status = 100 + (site);                                \
+      request = kAzNone;                                        \
+      goto finish;                                              \
+    }                                                           \
+  } while (0)
+#else
+#define WAZ_CHECK(cond, site) do {} while (0)
+#endif
+
 template <class G, bool kPuct>
 __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
   const int64_t r = blockIdx.x;
@@ -1207,6 +1226,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
     phase = 0;
   } else if (stage == kAzWaitPrior) {
     phase = 2;
+    WAZ_CHECK(path.at(depth) < cap, 1);
     reload_cur(path.at(depth));
   } else {
     v0 = a.value_in[r];
@@ -1221,9 +1241,16 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       } else {
         LaneArr acts;
         legal_lanes(lg, acts);
+        WAZ_CHECK(l >= nc || acts.a0 < static_cast<uint32_t>(A), 2);
+        WAZ_CHECK(l + 64 >= nc || acts.a1 < static_cast<uint32_t>(A), 3);
+        // The leaf's index is read across lanes BEFORE the lane-0 store: a
+        // readlane inside an exec-masked region reads a value the masked
+        // lanes never computed.
+        const uint32_t leaf = path.at(depth);
+        WAZ_CHECK(leaf < cap, 4);
         if (l < nc) raw[used + l] = pin[acts.a0];
         if (l + 64 < nc) raw[used + l + 64] = pin[acts.a1];
-        if (l == 0) nodes[path.at(depth)].first = used;
+        if (l == 0) nodes[leaf].first = used;
         used += nc;
         __threadfence_block();
       }
@@ -1260,6 +1287,12 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       perm.a1 = static_cast<uint32_t>(l + 64);
       wave_shuffle<kPolicyCpp>(perm, nc, bot);
       const uint32_t first = from_raw ? parked_first : used;
+      WAZ_CHECK(nc >= 1 && nc <= 128, 5);
+      WAZ_CHECK(first + static_cast<uint32_t>(nc) <= cap, 6);
+      WAZ_CHECK(cur_x < cap, 7);
+      WAZ_CHECK(l >= nc || perm.a0 < static_cast<uint32_t>(nc), 8);
+      WAZ_CHECK(l + 64 >= nc || perm.a1 < static_cast<uint32_t>(nc), 9);
+      WAZ_CHECK(l >= nc || acts.a0 < static_cast<uint32_t>(A), 10);
       const double* noise = a.noise ? a.noise + r * a.noise_stride : nullptr;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -1304,6 +1337,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
           break;
         }
         // ---- selection: lane k scores child k (and k + 64) ----
+        WAZ_CHECK(cur_first + static_cast<uint32_t>(cur_nc) <= cap, 11);
         const int cp = P0 ^ (depth & 1);
         const bool in0 = l < cur_nc, in1 = l + 64 < cur_nc;
         const Node<double> c0 = nodes[cur_first + (in0 ? l : 0)];
@@ -1327,6 +1361,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
           v1s = uct_value_sel(c1, in1, cp, logN, sp.uct_c);
         }
         const int chosen = wave_argmax2<64, true>(v0s, v1s);
+        WAZ_CHECK(chosen >= 0 && chosen < cur_nc, 12);
         res.scanned += cur_nc;
         const int src = chosen & 63;
         const Node<double> bc = chosen >= 64 ? c1 : c0;
@@ -1351,6 +1386,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       if (request != kAzNone) break;
       if (depth > res.max_depth) res.max_depth = depth;
       if (G::terminal(s, g)) {
+        WAZ_CHECK(cur_x < cap, 13);
         const int r0 = G::ret0(s, g, ctx);
         if (l == 0) nodes[cur_x].out = static_cast<int8_t>(r0);
         __threadfence_block();
@@ -1364,6 +1400,8 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
     }
     if (phase == 3) {
       // ---- backup (mcts.cc:351-357): lane d updates path node d ----
+      WAZ_CHECK(path.p0 < cap || l > depth, 14);
+      WAZ_CHECK(path.p1 < cap || 64 + l > depth, 15);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int d = 64 * j + l;
@@ -1385,6 +1423,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
           const int nc = __builtin_amdgcn_readfirstlane(nd.nchild);
           if (nc <= 0) continue;
           const uint32_t f = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nd.first)));
+          WAZ_CHECK(f + static_cast<uint32_t>(nc) <= cap, 16);
           const int cpl = P0 ^ (d & 1);
           res.solver_scanned += nc;
           const bool in0 = l < nc, in1 = l + 64 < nc;
@@ -1452,6 +1491,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
     const typename G::Legal lg = G::legal(s, g, ctx);
     LaneArr acts;
     legal_lanes(lg, acts);
+    WAZ_CHECK(l >= lg.count || acts.a0 < static_cast<uint32_t>(A), 17);
     if (l < lg.count) lm[acts.a0] = 1;
     if (l + 64 < lg.count) lm[acts.a1] = 1;
     if (l == 0) {
@@ -1461,6 +1501,9 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
     return;
   }
   // ---- finished (or failed): publish the root's children ----
+#if OS_WAZ_CHECK
+finish:
+#endif
   res.nodes = nodes_count;
   res.used = used;
   res.rng_words += bot.words.get();
