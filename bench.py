@@ -95,6 +95,9 @@ def parse():
   ap.add_argument("--az-graph", type=int, default=1,
                   help="az: replay each evaluator round as one captured HIP graph (1) "
                        "or launch it op by op (0)")
+  ap.add_argument("--az-layout", default="auto", choices=("auto", "wave", "lane"),
+                  help="az: one wavefront per search (k_waz_step), one lane per search "
+                       "(k_az_step) or auto (wave unless GC can fire)")
   ap.add_argument("--az-requests", default="fused", choices=("fused", "separate"),
                   help="az: one evaluator round per simulation (pure evaluator) or "
                        "the reference's separate Prior / Evaluate rounds")
@@ -664,7 +667,7 @@ def bench_az(args, ctx, layout):
   net = _az_network(obs_size, A, torch, ctx.dev)
   kw = dict(puct=True, max_simulations=sims, uct_c=c, dirichlet_alpha=alpha,
             dirichlet_epsilon=eps, stream=ctx.stream, requests=args.az_requests,
-            block_size=args.block)
+            block_size=args.block, layout=args.az_layout)
   parity = None
   if ctx.rank == 0 and args.parity_roots > 0:  # exact toy evaluator on a prefix vs the oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -720,8 +723,10 @@ def bench_az(args, ctx, layout):
                                     "hidden) on the same GPU" % (game, R, sims, c, alpha, eps, 256),
                         "game": game, "searches_per_gpu": R, "sims_per_search": sims,
                         "parallelism": "dp%d (independent searches)" % ctx.world,
-                        "layout": "lane (continuation in HBM)",
-                        "searches_per_wave": args.block or 64,
+                        "layout": ("wave (k_waz_step: one wavefront per search)"
+                                   if search.eng_az_wave() else
+                                   "lane (k_az_step: one lane per search)"),
+                        "searches_per_wave": 1 if search.eng_az_wave() else (args.block or 64),
                         "evaluator_requests": args.az_requests,
                         "rounds": "hip graph replay" if args.az_graph else "eager",
                         "sims_per_step_per_gpu": sims_step,
@@ -732,7 +737,8 @@ def bench_az(args, ctx, layout):
                 # the search alone (k_az_step time, no network): the figure
                 # comparable with cpu_baseline, whose evaluator is free
                 "search_only_sims_per_s": sims_step / max(step_ms * 1e-3, 1e-12)}
-  line["roofline"] = _roofline("k_az_step", game, alg / max(launches, 1), kernel_ms,
+  line["roofline"] = _roofline("k_waz_step" if search.eng_az_wave() else "k_az_step", game,
+                               alg / max(launches, 1), kernel_ms,
                                requests / max(launches, 1), "request")
   cpu = None
   if ctx.world == 1 and not args.no_cpu_baseline:

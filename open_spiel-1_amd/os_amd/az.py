@@ -53,6 +53,7 @@ class ExternalEvaluatorSearch:
     self.obs_shape = self.eng.observation_shape
     self.steps = 0
     self.requests = 0
+    self._layout_wave = False
 
   def run(self, root_actions, root_offsets, bot_seeds, evaluator, puct=True,
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
@@ -105,6 +106,10 @@ class ExternalEvaluatorSearch:
     if layout not in _LAYOUTS:
       raise ValueError("layout must be 'auto', 'wave' or 'lane'")
     check(lib.os_az_set_layout(self.eng._h, _LAYOUTS[layout]))
+    # the engine's choice for AUTO: wave unless GC can fire (os_az_set_layout)
+    max_nodes = (int(max_memory_mb) << 20) // 80 + 1
+    gc_possible = max_nodes > 1 and 1 + max_simulations * self.eng.max_children >= max_nodes
+    self._layout_wave = layout == "wave" or (layout == "auto" and not gc_possible)
     if bot_rng is None:
       bs = _lib.u32(bot_seeds)
       check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
@@ -194,6 +199,10 @@ class ExternalEvaluatorSearch:
           break
     st.synchronize()
     self.requests += int(total.item())
+
+  def eng_az_wave(self):
+    """True when the last prepared batch runs k_waz_step (os_az_set_layout)."""
+    return self._layout_wave
 
   def step_ms(self):
     """Summed k_az_step time of the last run(time_steps=True), ms."""
