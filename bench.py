@@ -320,7 +320,7 @@ def bench_search(args, ctx, layout):
   eng.set_arena_mode("reserved" if args.arena == "reserved" else "paged")
   eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
   handle = ctx.handle
-  for _ in range(args.warmup):
+  for _ in range(max(args.warmup, 1)):  # at least one: it sizes the arena / page pool
     eng.run_async(handle)
   out = eng.fetch()  # synchronises; validates per-root status
   arena_mode = args.arena

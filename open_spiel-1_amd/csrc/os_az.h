@@ -47,6 +47,11 @@ namespace osm {
 enum AzStage : int32_t { kAzStart = 0, kAzWaitPrior = 1, kAzWaitValue = 2, kAzDone = 3 };
 enum AzRequest : int32_t { kAzNone = 0, kAzPrior = 1, kAzValue = 2, kAzBoth = 3 };
 
+// Request counters of one step: search r adds to shard r % kAzShards; each
+// shard on its own 128-B line (kAzShardStride int32s).
+constexpr int kAzShards = 256;
+constexpr int kAzShardStride = 32;
+
 constexpr int kAzLogCap = 248;  // go: positions after the root on one tree path (<= 2 * 11 * 11)
 constexpr int kAzHeads = 122;   // go: stone-count buckets, 0 .. 11 * 11
 

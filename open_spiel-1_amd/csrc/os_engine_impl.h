@@ -160,6 +160,7 @@ struct AzArgs {
   const double* prior_in;   // [R][A]
   const double* value_in;   // [R]
   int32_t* pending;         // requests written by this step
+  int32_t* shards;          // kAzShards counters, kAzShardStride apart (zero between steps)
   // Bot rng continuing a caller-held stream (os_az_prepare_stateful): rows of
   // `mt` hold numpy-form keys, mt_pos_in the positions; a finished search
   // writes its stream back in the same form (key row + mt_pos_out).
@@ -308,7 +309,7 @@ struct os_engine {
   bool az_fused = false;    // mode of the prepared batch
   int32_t az_layout = OS_LAYOUT_AUTO;  // os_az_set_layout
   bool az_wave = false;     // the prepared batch runs k_waz_step (one wave per search)
-  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw;
+  osx::DevBuf d_az_slots, d_az_prior, d_az_noise, d_az_skip, d_az_pos, d_az_raw, d_az_shards;
   osx::DevBuf d_lpath, d_lheads, d_lact;  // k_lsearch paths, big-board heads / actions
   osx::DevBuf d_roots, d_bseed, d_eseed, d_mt, d_arena, d_lut, d_zob, d_rhash, d_rnh,
       d_pos, d_res, d_cact, d_cn, d_cw, d_cout, d_nch, d_rn, d_rw, d_rout, d_best,
@@ -348,7 +349,7 @@ struct os_engine {
                      &d_sp_act, &d_sp_len, &d_sp_ret, &d_sp_vis, &d_sp_obs,
                      &d_az_slots, &d_az_prior, &d_az_noise, &d_az_skip, &d_glog, &d_glink,
                      &d_roll_cnt, &d_rp_sum, &d_rp_all, &d_page_next, &d_sp_pol, &d_sp_val,
-                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_lpath, &d_lheads, &d_lact};
+                     &d_sp_actor, &d_sp_pow, &d_az_pos, &d_az_raw, &d_az_shards, &d_lpath, &d_lheads, &d_lact};
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
     h_stage.release();

@@ -637,9 +637,11 @@ using GoCtx = GoCtxT<uint8_t>;
 using GoCtxW = GoCtxT<uint16_t>;
 
 // 1: GoT::apply floods a chain only where its liberty count is unknown
-// (see apply); 0: every touched chain is flooded (the round-3 form).
+// (see apply); 0: every touched chain is flooded (the round-3 form).  Both
+// bit-exact; 0 measured faster (g9 496 vs 505 ms, C5 14.7 vs 15.1 ms:
+// profiles/r04/ab_go.md), so it is the default.
 #ifndef OS_GO_LAZY_ATARI
-#define OS_GO_LAZY_ATARI 1
+#define OS_GO_LAZY_ATARI 0
 #endif
 
 template <class B>

@@ -995,7 +995,7 @@ __global__ __launch_bounds__(64) void k_az_step(AzArgs a) {
   sl.mt_pre = bot.pre;
   sl.res.rng_words += bot.words;
   if (*io.kind != kAzNone) {
-    atomicAdd(a.pending, 1);
+    atomicAdd(a.shards + (blockIdx.x % kAzShards) * kAzShardStride, 1);
     return;
   }
   if (a.import_mt) {  // the bot's rng_ back in numpy (key, pos) form
@@ -1126,11 +1126,52 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
   const int64_t r = blockIdx.x;
   if (r >= a.num_roots) return;
   const int l = lane_id();
+#if OS_PHASE_TIMING
+  // Diagnostic build: cycles per phase of one launch (prologue = kPhRollout,
+  // descent = kPhSelect, expansion = kPhExpand, backup + solver = kPhBackup,
+  // request / result writes = kPhTail), summed over the launch's waves.
+  PhaseCycles ph = {};
+  const uint64_t ph_t0 = OS_PH_NOW();
+  uint64_t ph_t = ph_t0;
+  auto ph_flush = [&]() {  // sampled: one search in 64 (atomics would serialise the launch)
+    ph.c[kPhTotal] = OS_PH_NOW() - ph_t0;
+    if (l == 0 && (r & 63) == 0)
+      for (int i = 0; i < kNumPhases; ++i)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&g_phase_cycles[i]),
+                  static_cast<unsigned long long>(ph.c[i]));
+  };
+#define WAZ_PH(id)                 \
+  do {                             \
+    const uint64_t t_ = OS_PH_NOW(); \
+    ph.c[id] += t_ - ph_t;         \
+    ph_t = t_;                     \
+  } while (0)
+#else
+#define WAZ_PH(id) do {} while (0)
+#endif
+#if OS_WAVE_TIMES
+  // Diagnostic build: (start, end, HW_ID | XCC_ID << 32) of every search's
+  // wave in the launch that runs its 21st simulation (sim == 20 at entry).
+  const uint64_t wt_start = __builtin_amdgcn_s_memrealtime();
+  bool wt_on = false;
+  auto wt_flush = [&]() {
+    if (wt_on && l == 0 && r < kWaveTimesMax) {
+      uint64_t* wt = g_phase_cycles + kNumPhases + 3 * r;
+      wt[0] = wt_start;
+      wt[1] = __builtin_amdgcn_s_memrealtime();
+      wt[2] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF804)) |
+              (static_cast<uint64_t>(__builtin_amdgcn_s_getreg(0xF814)) << 32);
+    }
+  };
+#endif
   __shared__ uint32_t mt_lds[kMtN];
   AzSlot<G>& sl = static_cast<AzSlot<G>*>(a.slots)[r];
   int stage = __builtin_amdgcn_readfirstlane(sl.stage);
   if (stage == kAzDone) {
     if (l == 0) a.kind[r] = kAzNone;
+#if OS_PHASE_TIMING
+    ph_flush();
+#endif
     return;
   }
   const GameCfg& g = a.cfg;
@@ -1146,8 +1187,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
   const double inf = __builtin_huge_val();
   typename WaveCtxOf<G>::type ctx = WazCtx<G>::make(a, r);
 #if OS_PHASE_TIMING
-  PhaseCycles ph_unused = {};
-  if constexpr (std::is_same<G, Go>::value) ctx.sub = ph_unused.c;
+  if constexpr (std::is_same<G, Go>::value) ctx.sub = ph.c;
 #endif
   WaveMtRow bot;
   typename G::State s;
@@ -1191,6 +1231,9 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
     nodes_count = __builtin_amdgcn_readfirstlane(sl.nodes_count);
     used = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(sl.used)));
     res = make_uniform(sl.res);
+#if OS_WAVE_TIMES
+    wt_on = sim == 20;
+#endif
     path.p0 = sl.path[l];
     if (depth >= 64) path.p1 = sl.path[64 + l];
     if (depth >= 128) path.p2 = sl.path[128 + l];
@@ -1256,6 +1299,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       }
     }
   }
+  WAZ_PH(kPhRollout);
   for (;;) {
     if (phase < 0) break;
     if (phase == 0) {
@@ -1323,6 +1367,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       cur_first = first;
       cur_nc = nc;
       phase = 1;
+      WAZ_PH(kPhExpand);
     }
     if (phase == 1) {
       for (;;) {
@@ -1378,6 +1423,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
         }
         path.set(depth, ci);
       }
+      WAZ_PH(kPhSelect);
       if (res.status != kOk) break;
       if (from_raw) {
         phase = 2;
@@ -1456,6 +1502,7 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       const Node<double> rt = nodes[0];
       const int rout = __builtin_amdgcn_readfirstlane(rt.out);
       const int rnc = __builtin_amdgcn_readfirstlane(rt.nchild);
+      WAZ_PH(kPhBackup);
       if (rout != kUnsolved || rnc == 1) break;  // mcts.cc:398-401
       phase = 0;
     }
@@ -1496,8 +1543,15 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
     if (l + 64 < lg.count) lm[acts.a1] = 1;
     if (l == 0) {
       a.kind[r] = request;
-      atomicAdd(a.pending, 1);
+      atomicAdd(a.shards + (r % kAzShards) * kAzShardStride, 1);
     }
+#if OS_PHASE_TIMING
+    WAZ_PH(kPhTail);
+    ph_flush();
+#endif
+#if OS_WAVE_TIMES
+    wt_flush();
+#endif
     return;
   }
   // ---- finished (or failed): publish the root's children ----
@@ -1538,13 +1592,23 @@ finish:
     const int b = best_child(nodes, P0);
     a.best_action[r] = b < 0 ? -1 : nodes[rn.first + b].action;
   }
+#if OS_PHASE_TIMING
+  WAZ_PH(kPhTail);
+  ph_flush();
+#endif
+#if OS_WAVE_TIMES
+  wt_flush();
+#endif
 }
+#undef WAZ_PH
 
 
 // OS_ROLL_BLOOM: go playouts screen the superko log with a per-lane Bloom
-// filter in LDS (GoCtxBloom); 0: stone-count buckets (GoCtx).
+// filter in LDS (GoCtxBloom); 0: stone-count buckets (GoCtx).  Measured on C5
+// (profiles/r04/ab_go.md): 1 = 21.4 ms, 0 = 14.7 ms, both bit-exact -- the
+// buckets stay the default.
 #ifndef OS_ROLL_BLOOM
-#define OS_ROLL_BLOOM 1
+#define OS_ROLL_BLOOM 0
 #endif
 template <class G>
 struct RollCtx {
@@ -1939,6 +2003,23 @@ int SpLaunch(os_engine* e, hipStream_t stream) {
 template <class G>
 size_t AzSlotBytes() { return sizeof(AzSlot<G>); }
 
+// Sums the step's request shards into *pending and zeroes them (one
+// workgroup, one shard per thread).
+static __global__ __launch_bounds__(kAzShards) void k_az_pending(int32_t* shards, int32_t* pending) {
+  __shared__ int32_t part[kAzShards / 64];
+  const int t = threadIdx.x;
+  int32_t v = shards[t * kAzShardStride];
+  shards[t * kAzShardStride] = 0;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((t & 63) == 0) part[t >> 6] = v;
+  __syncthreads();
+  if (t == 0) {
+    int32_t s = 0;
+    for (int i = 0; i < kAzShards / 64; ++i) s += part[i];
+    *pending = s;
+  }
+}
+
 template <class G>
 int AzLaunch(os_engine* e, hipStream_t stream) {
   if constexpr (HasChance<G>::value) {
@@ -1969,6 +2050,7 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.prior_in = e->az_prior;
   a.value_in = e->az_value;
   a.pending = e->az_pending;
+  a.shards = static_cast<int32_t*>(e->d_az_shards.p);
   a.import_mt = e->az_import ? 1 : 0;
   a.mt_pos_in = static_cast<const int32_t*>(e->d_az_pos.p);
   a.mt_pos_out = static_cast<int32_t*>(e->d_az_pos.p) + (e->az_import ? e->num_roots : 0);
@@ -1993,23 +2075,25 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.root_w = d.root_w;
   a.root_out = d.root_out;
   a.best_action = d.best_action;
-  HIP_TRY(hipMemsetAsync(e->az_pending, 0, sizeof(int32_t), stream));
-  if (e->num_roots == 0) return OS_OK;
-  if (e->az_wave) {  // one wave per search (k_waz_step)
-    if (e->az_puct)
-      hipLaunchKernelGGL((k_waz_step<G, true>), dim3(static_cast<unsigned>(e->num_roots)),
-                         dim3(64), 0, stream, a);
-    else
-      hipLaunchKernelGGL((k_waz_step<G, false>), dim3(static_cast<unsigned>(e->num_roots)),
-                         dim3(64), 0, stream, a);
+  if (e->num_roots > 0) {
+    if (e->az_wave) {  // one wave per search (k_waz_step)
+      if (e->az_puct)
+        hipLaunchKernelGGL((k_waz_step<G, true>), dim3(static_cast<unsigned>(e->num_roots)),
+                           dim3(64), 0, stream, a);
+      else
+        hipLaunchKernelGGL((k_waz_step<G, false>), dim3(static_cast<unsigned>(e->num_roots)),
+                           dim3(64), 0, stream, a);
+    } else {
+      // Searches per workgroup (one wave): os_mcts_params.block_size, 64 by
+      // default.  Fewer lanes per wave spread a small batch over more SIMDs.
+      const int bs = e->params.block_size > 0 ? std::min(e->params.block_size, 64) : 64;
+      hipLaunchKernelGGL(k_az_step<G>, dim3(static_cast<unsigned>((e->num_roots + bs - 1) / bs)),
+                         dim3(bs), 0, stream, a);
+    }
     HIP_TRY(hipGetLastError());
-    return OS_OK;
   }
-  // Searches per workgroup (one wave): os_mcts_params.block_size, 64 by
-  // default.  Fewer lanes per wave spread a small batch over more SIMDs.
-  const int bs = e->params.block_size > 0 ? std::min(e->params.block_size, 64) : 64;
-  hipLaunchKernelGGL(k_az_step<G>, dim3(static_cast<unsigned>((e->num_roots + bs - 1) / bs)),
-                     dim3(bs), 0, stream, a);
+  // *pending = the step's request count; the shards are zeroed for the next step.
+  hipLaunchKernelGGL(k_az_pending, dim3(1), dim3(kAzShards), 0, stream, a.shards, a.pending);
   HIP_TRY(hipGetLastError());
   return OS_OK;
   }
