@@ -623,14 +623,25 @@ def _az_network(obs_size, A, torch, dev, hidden=256):
   wp = (torch.randn(hidden, A, generator=g) / hidden ** 0.5).to(dev, torch.bfloat16)
   wv = (torch.randn(hidden, 1, generator=g) / hidden ** 0.5).to(dev, torch.bfloat16)
 
-  def evaluator(obs, legal, kind):
-    x = obs.reshape(obs.shape[0], -1).to(torch.bfloat16)
-    h = torch.relu(x @ w1)
-    logits = (h @ wp).double().masked_fill(~legal, float("-inf"))
-    prior = torch.softmax(logits, dim=-1).nan_to_num(0.0)
-    value = torch.tanh((h @ wv).double()).squeeze(-1)
-    return prior, value
-  return evaluator
+  wpv = torch.cat([wp, wv], dim=1).contiguous()  # policy logits, then the value logit
+
+  class Evaluator:
+    def __call__(self, obs, legal, kind):  # the plain protocol (tensors out)
+      x = obs.reshape(obs.shape[0], -1).to(torch.bfloat16)
+      h = torch.relu(x @ w1)
+      logits = (h @ wp).double().masked_fill(~legal, -1e32)
+      prior = torch.softmax(logits, dim=-1)
+      value = torch.tanh((h @ wv).double()).squeeze(-1)
+      return prior, value
+
+    def evaluate_into(self, obs, legal, kind, prior, value):
+      # one GEMM for both heads, then the fused heads kernel writes the
+      # engine's response buffers (os_amd.az.heads_into)
+      from os_amd.az import heads_into
+      x = obs.reshape(obs.shape[0], -1).to(torch.bfloat16)
+      h = torch.relu_(x @ w1)
+      heads_into(h @ wpv, legal, prior, value)
+  return Evaluator()
 
 
 def _az_toy_evaluator(A, torch):

@@ -277,6 +277,17 @@ int os_az_step_async(os_engine* e, void* hip_stream);
 int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32_t* child_n,
                 double* child_w, int8_t* child_out, int32_t* nchild, int32_t* root_n,
                 double* root_w, int8_t* root_out, int64_t* best_action, int32_t* nodes);
+/* Policy / value heads of an evaluator network, fused into one kernel on
+ * hip_stream (optional: an evaluator may compute the responses any way it
+ * likes).  Row r of `logits` (element stride ld; dtype 0 = f32, 1 = bf16)
+ * holds num_actions policy logits, then the value logit.  As the reference
+ * network's heads (alpha_zero/model.py:278-282, 304): illegal logits
+ * (legal[r * num_actions + a] == 0) become -1e32, prior[r][a] = their softmax,
+ * value[r] = tanh(value logit); f64 arithmetic, written straight into the
+ * engine's response buffers (dev_prior / dev_value of os_az_prepare). */
+int os_az_heads_async(const void* logits, int32_t dtype, int64_t num_rows, int32_t num_actions,
+                      int64_t ld, const uint8_t* legal, double* prior, double* value,
+                      void* hip_stream);
 
 /* ---- Self-play -----------------------------------
  * num_games independent games, each played on the device the way

@@ -499,24 +499,28 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     rh.assign(static_cast<size_t>(std::max<int64_t>(R, 1)) * e->hash_stride, 0);
     rnh.assign(std::max<int64_t>(R, 1), 0);
   }
-  for (int64_t r = 0; r < R; ++r) {
-    HostState hs;
-    std::string err;
-    if (!ReplayRoot(e->game, root_actions + root_offsets[r],
-                    root_offsets[r + 1] - root_offsets[r], &hs, &err))
-      return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
-    if (StateTerminal(hs))
-      return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
-    if (StateIsChance(hs))  // a bot is only asked to move at decision nodes
-      return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is a chance node");
-    std::memcpy(roots.data() + r * sb, hs.raw, sb);
-    if (go) {
-      const int64_t nh = static_cast<int64_t>(hs.hashes.size());
-      if (nh > e->hash_stride) return Fail(OS_ERR_CAPACITY, "go hash history too long");
-      std::memcpy(rh.data() + r * e->hash_stride, hs.hashes.data(), nh * 8);
-      rnh[r] = static_cast<int32_t>(nh);
+  rc = ParallelChunks(R, 1024, [&](int64_t lo, int64_t hi) {
+    for (int64_t r = lo; r < hi; ++r) {
+      HostState hs;
+      std::string err;
+      if (!ReplayRoot(e->game, root_actions + root_offsets[r],
+                      root_offsets[r + 1] - root_offsets[r], &hs, &err))
+        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
+      if (StateTerminal(hs))
+        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
+      if (StateIsChance(hs))  // a bot is only asked to move at decision nodes
+        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is a chance node");
+      std::memcpy(roots.data() + r * sb, hs.raw, sb);
+      if (go) {
+        const int64_t nh = static_cast<int64_t>(hs.hashes.size());
+        if (nh > e->hash_stride) return Fail(OS_ERR_CAPACITY, "go hash history too long");
+        std::memcpy(rh.data() + r * e->hash_stride, hs.hashes.data(), nh * 8);
+        rnh[r] = static_cast<int32_t>(nh);
+      }
     }
-  }
+    return 0;
+  });
+  if (rc) return rc;
   const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
   if ((rc = e->d_roots.ensure(Rz * sb))) return rc;
   if ((rc = e->d_bseed.ensure(Rz * 4)) || (rc = e->d_eseed.ensure(Rz * 4))) return rc;
@@ -909,21 +913,26 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     const int mc = e->game.cfg.max_children;
     std::vector<double> noise(Rz * mc, 0.0);
     std::vector<int32_t> skip(Rz, 0);
-    std::vector<int64_t> acts;
-    for (int64_t r = 0; r < R; ++r) {
-      HostState hs;
-      std::string err;
-      ReplayRoot(e->game, root_actions + root_offsets[r], root_offsets[r + 1] - root_offsets[r],
-                 &hs, &err);
-      StateLegal(hs, &acts);
-      const int64_t w =
-          import ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r],
-                                       static_cast<int>(acts.size()), alpha, noise.data() + r * mc)
-                 : DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
-                                  noise.data() + r * mc);
-      if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
-      skip[r] = static_cast<int32_t>(w);
-    }
+    rc = ParallelChunks(R, 512, [&](int64_t lo, int64_t hi) {
+      std::vector<int64_t> acts;
+      for (int64_t r = lo; r < hi; ++r) {
+        HostState hs;
+        std::string err;
+        ReplayRoot(e->game, root_actions + root_offsets[r],
+                   root_offsets[r + 1] - root_offsets[r], &hs, &err);
+        StateLegal(hs, &acts);
+        const int64_t w =
+            import ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r],
+                                         static_cast<int>(acts.size()), alpha,
+                                         noise.data() + r * mc)
+                   : DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
+                                    noise.data() + r * mc);
+        if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
+        skip[r] = static_cast<int32_t>(w);
+      }
+      return 0;
+    });
+    if (rc) return rc;
     if ((rc = e->d_az_noise.ensure(noise.size() * 8)) || (rc = e->d_az_skip.ensure(Rz * 4)))
       return rc;
     HIP_TRY(hipMemcpy(e->d_az_noise.p, noise.data(), noise.size() * 8, hipMemcpyHostToDevice));
@@ -1532,6 +1541,42 @@ int64_t os_dirichlet_noise(uint32_t seed, int32_t count, double alpha, double* o
   if (count < 0 || (count > 0 && !out)) return Fail(OS_ERR_INVALID, "null argument");
   if (!(alpha > 0.0)) return Fail(OS_ERR_INVALID, "alpha must be > 0");
   return DirichletNoise(seed, count, alpha, out);
+}
+
+// One thread per row (rows are requests; num_actions is small next to them).
+__global__ void k_az_heads(const void* logits, int32_t dtype, int64_t R, int32_t A, int64_t ld,
+                           const uint8_t* legal, double* prior, double* value) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  auto get = [&](int a) -> double {
+    const int64_t i = r * ld + a;
+    if (dtype == 0) return static_cast<double>(static_cast<const float*>(logits)[i]);
+    const uint32_t b = static_cast<uint32_t>(static_cast<const uint16_t*>(logits)[i]) << 16;
+    return static_cast<double>(__uint_as_float(b));
+  };
+  const uint8_t* lg = legal + r * A;
+  double m = -__builtin_huge_val();
+  for (int a = 0; a < A; ++a) m = fmax(m, lg[a] ? get(a) : -1e32);
+  double s = 0.0;
+  for (int a = 0; a < A; ++a) s += exp((lg[a] ? get(a) : -1e32) - m);
+  double* pr = prior + r * A;
+  for (int a = 0; a < A; ++a) pr[a] = exp((lg[a] ? get(a) : -1e32) - m) / s;
+  value[r] = tanh(get(A));
+}
+
+int os_az_heads_async(const void* logits, int32_t dtype, int64_t num_rows, int32_t num_actions,
+                      int64_t ld, const uint8_t* legal, double* prior, double* value,
+                      void* hip_stream) {
+  if (num_rows < 0 || num_actions < 1 || ld < num_actions + 1 || (dtype != 0 && dtype != 1))
+    return Fail(OS_ERR_INVALID, "bad heads shape / dtype");
+  if (num_rows == 0) return OS_OK;
+  if (!logits || !legal || !prior || !value) return Fail(OS_ERR_INVALID, "null heads buffer");
+  const unsigned blocks = static_cast<unsigned>((num_rows + 255) / 256);
+  hipLaunchKernelGGL(k_az_heads, dim3(blocks), dim3(256), 0,
+                     static_cast<hipStream_t>(hip_stream), logits, dtype, num_rows, num_actions,
+                     ld, legal, prior, value);
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
 }
 
 int os_az_step_async(os_engine* e, void* hip_stream) {

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/os_mcts.h"
@@ -28,6 +29,31 @@ extern thread_local std::string g_err;
 inline int Fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+// Host-side per-root work (root replay, Dirichlet draws) over [0, n) in
+// contiguous chunks on up to 16 threads, the calling thread taking the first.
+// body(lo, hi) returns 0 or a Fail() code; the lowest failing chunk's code
+// and message are returned (the same error a serial loop reports first).
+template <class F>
+int ParallelChunks(int64_t n, int64_t min_chunk, F body) {
+  const int64_t hw = std::max<int64_t>(1, std::thread::hardware_concurrency());
+  const int T = static_cast<int>(
+      std::min<int64_t>(std::min<int64_t>(hw, 16), (n + min_chunk - 1) / min_chunk));
+  if (T <= 1) return body(int64_t{0}, n);
+  std::vector<int> rc(T, 0);
+  std::vector<std::string> msg(T);
+  auto run = [&](int t) {
+    rc[t] = body(n * t / T, n * (t + 1) / T);
+    if (rc[t]) msg[t] = g_err;  // g_err is thread-local
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(run, t);
+  run(0);
+  for (std::thread& x : th) x.join();
+  for (int t = 0; t < T; ++t)
+    if (rc[t]) return Fail(rc[t], msg[t]);
+  return 0;
 }
 #define HIP_TRY(expr)                                                        \
   do {                                                                       \

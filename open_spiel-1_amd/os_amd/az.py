@@ -17,7 +17,11 @@ in place and writes priors / values back -- no host round trip of the data.
 obs float32 [N, C, H, W] (ObservationTensor of the player to move), legal bool
 [N, A], kind int32 [N] (1 = Prior wanted, 2 = Evaluate wanted, 3 = both,
 0 = idle), and returns (prior float64 [N, A] action-indexed, value float64 [N]
-for player 0).  Entries whose kind is 0 are ignored.  Results are bit-exact with
+for player 0).  Entries whose kind is 0 are ignored.  An evaluator object may
+instead provide `evaluate_into(obs, legal_u8, kind, prior, value)` and write
+the responses itself (e.g. its last layer's logits through `heads_into`, the
+fused policy / value heads kernel), saving the mask conversion and the two
+response copies per round.  Results are bit-exact with
 the reference `MCTSBot(game, evaluator, uct_c, max_simulations, max_memory_mb,
 solve, seed, false, child_selection_policy)` driving the same evaluator.
 
@@ -39,6 +43,37 @@ from ._lib import check, lib, ptr
 KIND_NONE, KIND_PRIOR, KIND_VALUE, KIND_BOTH = 0, 1, 2, 3
 _REQUESTS = {"separate": _lib.AZ_REQUESTS_SEPARATE, "fused": _lib.AZ_REQUESTS_FUSED}
 _LAYOUTS = {"auto": _lib.LAYOUT_AUTO, "wave": _lib.LAYOUT_WAVE, "lane": _lib.LAYOUT_LANE}
+
+
+def heads_into(logits, legal, prior, value):
+  """prior / value from a network's last layer on the current stream: row r of
+  `logits` (f32 or bf16 [N, A + 1]) holds A policy logits then the value
+  logit; prior = softmax over the legal actions (others -1e32,
+  alpha_zero/model.py:278-282), value = tanh (model.py:304), f64
+  (include/os_mcts.h os_az_heads_async)."""
+  import torch
+  n, a = prior.shape
+  if logits.dtype not in (torch.float32, torch.bfloat16):
+    raise ValueError("logits must be float32 or bfloat16")
+  if logits.shape[0] != n or logits.shape[1] != a + 1 or logits.stride(1) != 1:
+    raise ValueError("logits must be [N, A + 1] with unit column stride")
+  if legal.dtype != torch.uint8 or prior.dtype != torch.float64 or value.dtype != torch.float64:
+    raise ValueError("legal uint8, prior / value float64 expected")
+  st = torch.cuda.current_stream(prior.device)
+  check(lib.os_az_heads_async(logits.data_ptr(), 0 if logits.dtype == torch.float32 else 1, n, a,
+                              logits.stride(0), legal.data_ptr(), prior.data_ptr(),
+                              value.data_ptr(), st.cuda_stream))
+
+
+def _evaluate(evaluator, obs, legal, kind, prior, value):
+  """One evaluator round: in place when the evaluator supports it."""
+  into = getattr(evaluator, "evaluate_into", None)
+  if into is not None:
+    into(obs, legal, kind, prior, value)
+  else:
+    pr, v = evaluator(obs, legal.bool(), kind)
+    prior.copy_(pr)
+    value.copy_(v)
 
 
 class ExternalEvaluatorSearch:
@@ -151,9 +186,7 @@ class ExternalEvaluatorSearch:
       with torch.cuda.stream(st):
         pend_host.copy_(pending, non_blocking=True)
         done.record(st)
-        pr, v = evaluator(obs, legal.bool(), kind)
-        prior.copy_(pr)
-        value.copy_(v)
+        _evaluate(evaluator, obs, legal, kind, prior, value)
       done.synchronize()  # step k and its count, not the evaluation behind it
       n = int(pend_host[0])
       if n == 0:
@@ -183,9 +216,7 @@ class ExternalEvaluatorSearch:
     with torch.cuda.graph(g):
       cs = torch.cuda.current_stream(self.device)
       check(lib.os_az_step_async(self.eng._h, cs.cuda_stream))
-      pr, v = evaluator(obs, legal.bool(), kind)
-      prior.copy_(pr)
-      value.copy_(v)
+      _evaluate(evaluator, obs, legal, kind, prior, value)
       total.add_(pending)
     with torch.cuda.stream(st):
       while True:

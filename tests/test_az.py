@@ -334,3 +334,75 @@ def test_gpu_alphazero_actor_matches_oracle(require_gpu, game, sims, t, drop, re
                                   requests="separate" if resign else "fused", **kw)
   for k in ("actions", "length", "returns", "policy", "root_value"):
     np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+class _IntoToyEvaluator:
+  """The torch toy evaluator through the in-place protocol (evaluate_into)."""
+
+  def __init__(self, A):
+    self.f = _torch_toy_evaluator(A)
+
+  def evaluate_into(self, obs, legal, kind, prior, value):
+    pr, v = self.f(obs, legal.bool(), kind)
+    prior.copy_(pr)
+    value.copy_(v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["wave", "lane"])
+def test_gpu_evaluate_into_protocol_matches_oracle(require_gpu, layout):
+  from os_amd.az import ExternalEvaluatorSearch
+  game = "connect_four"
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  R, sims = 96, 24
+  acts, offs = E.make_roots(game, R, seed_base=11, max_plies=4)
+  seeds = np.arange(R, dtype=np.uint32) + 3
+  kw = dict(puct=True, uct_c=1.25, max_simulations=sims, dirichlet_alpha=1.0,
+            dirichlet_epsilon=0.25)
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=A, **kw)
+  search = ExternalEvaluatorSearch(game)
+  for graph in (False, True):
+    got = search.run(acts, offs, seeds, _IntoToyEvaluator(A), graph=graph, graph_batch=4,
+                     layout=layout, **kw)
+    mc = search.eng.max_children
+    for k in E.OUTPUT_KEYS:
+      r = ref[k][:, :mc] if ref[k].ndim == 2 else ref[k]
+      np.testing.assert_array_equal(got[k], r, err_msg="%s graph=%s" % (k, graph))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_gpu_heads_kernel_matches_torch(require_gpu, dtype):
+  """os_az_heads_async against the reference heads (alpha_zero/model.py:278-282,
+  304) in torch f64: illegal logits -1e32, softmax, tanh.  Tolerance 1e-13
+  relative (device exp / tanh vs torch's, f64)."""
+  import torch
+  from os_amd.az import heads_into
+  g = torch.Generator().manual_seed(1)
+  N, A = 1000, 82
+  logits = (torch.randn(N, A + 1, generator=g) * 4).to("cuda", getattr(torch, dtype))
+  legal = (torch.rand(N, A, generator=g) < 0.4).to(torch.uint8)
+  legal[3] = 0  # a row without a legal action: uniform, as the reference's softmax
+  legal[4] = 1
+  legal = legal.cuda()
+  prior = torch.full((N, A), -7.0, dtype=torch.float64, device="cuda")
+  value = torch.full((N,), -7.0, dtype=torch.float64, device="cuda")
+  heads_into(logits, legal, prior, value)
+  lg = logits.double()
+  ref_p = torch.softmax(lg[:, :A].masked_fill(legal == 0, -1e32), dim=-1)
+  ref_v = torch.tanh(lg[:, A])
+  torch.testing.assert_close(prior, ref_p, rtol=1e-13, atol=1e-300)
+  torch.testing.assert_close(value, ref_v, rtol=1e-13, atol=1e-300)
+  some = legal.any(1, keepdim=True)
+  assert torch.all(prior[(legal == 0) & some] == 0)  # exp(-1e32 - max) underflows to 0
+  np.testing.assert_allclose(prior[3].cpu().numpy(), np.full(A, 1.0 / A), rtol=1e-15)
+
+
+def test_heads_abi_rejects_bad_shapes():
+  from os_amd import _lib
+  L = _lib.lib
+  assert L.os_az_heads_async(None, 0, 0, 7, 8, None, None, None, None) == 0  # empty: no launch
+  assert L.os_az_heads_async(None, 0, 4, 7, 7, None, None, None, None) != 0  # ld < A + 1
+  assert L.os_az_heads_async(None, 2, 4, 7, 8, None, None, None, None) != 0  # dtype
+  assert L.os_az_heads_async(None, 0, 4, 7, 8, None, None, None, None) != 0  # null buffers

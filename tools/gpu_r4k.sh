@@ -1,0 +1,13 @@
+#!/bin/bash
+# az: in-place evaluator protocol + fused heads; threaded host prepare.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+OUT=$R/gpurun_out/r4k
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_az.py > "$OUT/pytest_az.log" 2>&1 || { tail -30 "$OUT/pytest_az.log"; exit 1; }
+tail -2 "$OUT/pytest_az.log"
+timeout -k 10 300 python -u bench.py --config az --steps 3 --warmup 1 --no-cpu-baseline --no-parity-sweep --parity-roots 8 > "$OUT/az.json" 2> "$OUT/az.err" || exit 1
+python -c "import json;d=json.load(open('$OUT/az.json'));print('az', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_per_launch'], d['az'], d['parity']['bit_exact'])"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_az" -o run --output-format csv -- python3 "$R/bench.py" --config az --steps 2 --warmup 1 --no-cpu-baseline --no-parity-sweep --parity-roots 0 > "$OUT/rocprof_az.log" 2>&1 || exit 1
+echo r4k-done
