@@ -1453,6 +1453,71 @@ struct GoLabels {
   }
 };
 
+// Neighbourhoods on the vector unit.  nbr(x) = the board points with a
+// 4-neighbour in x, which is Go::nbr4(x) (adjacency is symmetric); the scalar
+// form is four 128-bit shifts, two column masks and the ORs (~30 SALU).  Here
+// lane l tests points l and l + 64: x shifted up one row (e = x << n, five
+// dwords) puts the neighbours p - n, p - 1, p + 1, p + n of p at bits 0, n - 1,
+// n + 1, 2n of the 32-bit window of e at bit p, one v_alignbit away; the
+// lane's constant mask (m0 / m1, the edge columns and off-board points
+// cleared) picks them and a v_cmp writes the result straight into the mask.
+// ~10 VALU + ~6 SALU: the wave search is bound by the scalar unit (one per
+// CU, shared by its waves) while the VALU idles.  n <= 15 (2n < 32).
+struct GoNbrLanes {
+  uint32_t m0, m1;  // per lane
+  int n;
+  __device__ void init(const GameCfg& g) {
+    n = g.rows;
+    const int N = g.rows * g.cols;
+    const int l = lane_id();
+    auto mk = [&](int p) -> uint32_t {
+      if (p >= N) return 0u;
+      const int c = p % n;
+      uint32_t m = 1u | (1u << (2 * n));
+      if (c > 0) m |= 1u << (n - 1);
+      if (c < n - 1) m |= 1u << (n + 1);
+      return m;
+    };
+    m0 = mk(l);
+    m1 = mk(l + 64);
+  }
+  __device__ B128 any(B128 x) const {
+    const uint64_t elo = x.lo << n;
+    const uint64_t ehi = (x.hi << n) | (x.lo >> (64 - n));
+    const uint32_t e0 = static_cast<uint32_t>(elo), e1 = static_cast<uint32_t>(elo >> 32);
+    const uint32_t e2 = static_cast<uint32_t>(ehi), e3 = static_cast<uint32_t>(ehi >> 32);
+    const uint32_t e4 = static_cast<uint32_t>(x.hi >> (64 - n));
+    const int l = lane_id();
+    const bool up = l >= 32;
+    const uint32_t w0 = __builtin_amdgcn_alignbit(up ? e2 : e1, up ? e1 : e0, l & 31);
+    const uint32_t w1 = __builtin_amdgcn_alignbit(up ? e4 : e3, up ? e3 : e2, l & 31);
+    return b128(ballot((w0 & m0) != 0), ballot((w1 & m1) != 0));
+  }
+};
+
+// Go::legal with the neighbourhoods on the lanes (same mask, go_board.cc:425-440).
+__device__ __forceinline__ Go::Legal go_legal_lanes(const Go::State& s, const GameCfg& g,
+                                                    const GoNbrLanes& nb) {
+  using M = CfgMasks<B128>;
+  const int c = s.to_play;
+  const B128 E = M::board(g) & ~(s.bw[0] | s.bw[1]);
+  B128 cand = E;
+  if (s.ko >= 0) cand = cand & ~bit128(s.ko);
+  const B128 has_lib = nb.any(E);
+  B128 mask = cand & has_lib;
+  const B128 hard = cand & ~has_lib;
+  if (any(hard)) {
+    const B128 own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+    const B128 good = (own & ~s.atari) | (opp & s.atari);
+    mask = mask | (hard & nb.any(good));
+  }
+  Go::Legal l;
+  l.mask = mask;
+  l.count = popc(mask) + 1;
+  l.pass_action = g.rows * g.cols;
+  return l;
+}
+
 // LegalActions()[k] from the legal mask on the lanes: the lane holding the
 // k-th set bit sees exactly k set bits below it (mbcnt); pass is last.
 __device__ __forceinline__ int go_kth_lanes(B128 mask, int k, int pass) {
@@ -1470,7 +1535,7 @@ __device__ __forceinline__ int go_kth_lanes(B128 mask, int k, int pass) {
 
 // GoT::apply (go_board.cc:217-299 via go.cc:124-216) with chains from labels.
 __device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, GoWaveCtx& ctx,
-                                               GoLabels& lab, int a) {
+                                               GoLabels& lab, const GoNbrLanes& nbl, int a) {
   using M = CfgMasks<B128>;
   const int c = s.to_play;
   const int pass = g.rows * g.cols;
@@ -1481,7 +1546,7 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, G
     s.flags |= Go::kLastPass;
   } else {
     const B128 pb = bit128(a);
-    const B128 nb = Go::nbr4(pb, g);
+    const B128 nb = nbl.any(pb);
     const B128 own0 = pick(s.bw, c);
     const B128 own = own0 | pb;
     B128 opp = pick(s.bw, 1 - c);
@@ -1505,7 +1570,7 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, G
       const int q = lowest(on);
       const B128 ch = lab.chain(lab.at(q)) & opp;
       on = on & ~ch;
-      const B128 libs = Go::nbr4(ch, g) & E;
+      const B128 libs = nbl.any(ch) & E;
       if (!any(libs)) {
         opp = opp & ~ch;
         E = E | ch;
@@ -1521,11 +1586,11 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, G
       }
       atari = (atari & ~ch) | sel128(popc(libs) == 1, ch, b128(0, 0));
     }
-    B128 todo = pb | (Go::nbr4(capd, g) & own);
+    B128 todo = pb | (any(capd) ? nbl.any(capd) & own : b128(0, 0));
     while (any(todo)) {
       const B128 ch = lab.chain(lab.at(lowest(todo))) & own;
       todo = todo & ~ch;
-      atari = (atari & ~ch) | sel128(popc(Go::nbr4(ch, g) & E) == 1, ch, b128(0, 0));
+      atari = (atari & ~ch) | sel128(popc(nbl.any(ch) & E) == 1, ch, b128(0, 0));
     }
     s.atari = atari;
     s.bw[0] = c ? opp : own;
@@ -1543,13 +1608,15 @@ __device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rn
   ev.uniformize();
   GoLabels lab;
   lab.init(s, g);
+  GoNbrLanes nbl;
+  nbl.init(g);
   const int pass = g.rows * g.cols;
   for (;;) {
     if (Go::terminal(s, g)) break;
 #if OS_PHASE_TIMING
     const uint64_t t0 = OS_PH_NOW();
 #endif
-    const Go::Legal l = Go::legal(s, g, ctx);
+    const Go::Legal l = go_legal_lanes(s, g, nbl);
     uint32_t k;
     if (Policy == kPolicyCpp)
       k = ev.uniform_lanes(static_cast<uint32_t>(l.count));
@@ -1560,7 +1627,7 @@ __device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rn
     const uint64_t t1 = OS_PH_NOW();
     OS_PH_ADD(ctx.sub[kPhGoLegal], t0);
 #endif
-    go_apply_lanes(s, g, ctx, lab, act);
+    go_apply_lanes(s, g, ctx, lab, nbl, act);
 #if OS_PHASE_TIMING
     OS_PH_ADD(ctx.sub[kPhGoApply], t1);
 #endif

@@ -27,6 +27,8 @@ CASES = [
     ("hex", 72, 200, 4),
     ("go(board_size=7,komi=4.5)", 8, 200, 6),
     ("go(board_size=9)", 8, 160, 8),
+    ("go(board_size=11,komi=6.5)", 6, 60, 6),  # 121 points: the lane neighbourhoods' top dword
+    ("go(board_size=6)", 8, 120, 4),
 ]
 
 
