@@ -1493,22 +1493,35 @@ struct GoNbrLanes {
     const uint32_t w1 = __builtin_amdgcn_alignbit(up ? e4 : e3, up ? e3 : e2, l & 31);
     return b128(ballot((w0 & m0) != 0), ballot((w1 & m1) != 0));
   }
+  // any(bit128(a)): a is p's neighbour iff t = a - p + n is one of p's window
+  // bits, so no one-hot set is built and shifted.
+  __device__ B128 at(int a) const {
+    const int l = lane_id();
+    const uint32_t t0 = static_cast<uint32_t>(a - l + n), t1 = static_cast<uint32_t>(a - l - 64 + n);
+    const bool h0 = t0 < 32u && ((m0 >> (t0 & 31u)) & 1u);
+    const bool h1 = t1 < 32u && ((m1 >> (t1 & 31u)) & 1u);
+    return b128(ballot(h0), ballot(h1));
+  }
+};
+
+// The playout's board relative to the player to move (the state's bw[] is
+// rebuilt at the end): no per-move selects of bw[to_play] on the scalar unit.
+struct GoSides {
+  B128 me, them;
 };
 
 // Go::legal with the neighbourhoods on the lanes (same mask, go_board.cc:425-440).
-__device__ __forceinline__ Go::Legal go_legal_lanes(const Go::State& s, const GameCfg& g,
-                                                    const GoNbrLanes& nb) {
+__device__ __forceinline__ Go::Legal go_legal_lanes(const Go::State& s, const GoSides& sd,
+                                                    const GameCfg& g, const GoNbrLanes& nb) {
   using M = CfgMasks<B128>;
-  const int c = s.to_play;
-  const B128 E = M::board(g) & ~(s.bw[0] | s.bw[1]);
+  const B128 E = M::board(g) & ~(sd.me | sd.them);
   B128 cand = E;
   if (s.ko >= 0) cand = cand & ~bit128(s.ko);
   const B128 has_lib = nb.any(E);
   B128 mask = cand & has_lib;
   const B128 hard = cand & ~has_lib;
   if (any(hard)) {
-    const B128 own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-    const B128 good = (own & ~s.atari) | (opp & s.atari);
+    const B128 good = (sd.me & ~s.atari) | (sd.them & s.atari);
     mask = mask | (hard & nb.any(good));
   }
   Go::Legal l;
@@ -1534,8 +1547,9 @@ __device__ __forceinline__ int go_kth_lanes(B128 mask, int k, int pass) {
 }
 
 // GoT::apply (go_board.cc:217-299 via go.cc:124-216) with chains from labels.
-__device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, GoWaveCtx& ctx,
-                                               GoLabels& lab, const GoNbrLanes& nbl, int a) {
+__device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const GameCfg& g,
+                                               GoWaveCtx& ctx, GoLabels& lab,
+                                               const GoNbrLanes& nbl, int a) {
   using M = CfgMasks<B128>;
   const int c = s.to_play;
   const int pass = g.rows * g.cols;
@@ -1544,12 +1558,15 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, G
   if (a == pass) {
     s.ko = -1;
     s.flags |= Go::kLastPass;
+    const B128 t = sd.me;
+    sd.me = sd.them;
+    sd.them = t;
   } else {
     const B128 pb = bit128(a);
-    const B128 nb = nbl.any(pb);
-    const B128 own0 = pick(s.bw, c);
+    const B128 nb = nbl.at(a);
+    const B128 own0 = sd.me;
     const B128 own = own0 | pb;
-    B128 opp = pick(s.bw, 1 - c);
+    B128 opp = sd.them;
     const bool enemy_eye = !any(nb & ~opp);
     s.hash ^= ctx.zob[2 * a + c];
     B128 E = M::board(g) & ~(own | opp);
@@ -1593,8 +1610,8 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, const GameCfg& g, G
       atari = (atari & ~ch) | sel128(popc(nbl.any(ch) & E) == 1, ch, b128(0, 0));
     }
     s.atari = atari;
-    s.bw[0] = c ? opp : own;
-    s.bw[1] = c ? own : opp;
+    sd.me = opp;  // the next player's stones
+    sd.them = own;
     s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
     if (!ctx.insert(s.hash, captured > 0, popc(own) + popc(opp))) s.flags |= Go::kSuperko;
   }
@@ -1610,13 +1627,16 @@ __device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rn
   lab.init(s, g);
   GoNbrLanes nbl;
   nbl.init(g);
+  GoSides sd;
+  sd.me = pick(s.bw, s.to_play);
+  sd.them = pick(s.bw, 1 - s.to_play);
   const int pass = g.rows * g.cols;
   for (;;) {
     if (Go::terminal(s, g)) break;
 #if OS_PHASE_TIMING
     const uint64_t t0 = OS_PH_NOW();
 #endif
-    const Go::Legal l = go_legal_lanes(s, g, nbl);
+    const Go::Legal l = go_legal_lanes(s, sd, g, nbl);
     uint32_t k;
     if (Policy == kPolicyCpp)
       k = ev.uniform_lanes(static_cast<uint32_t>(l.count));
@@ -1627,11 +1647,13 @@ __device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rn
     const uint64_t t1 = OS_PH_NOW();
     OS_PH_ADD(ctx.sub[kPhGoLegal], t0);
 #endif
-    go_apply_lanes(s, g, ctx, lab, nbl, act);
+    go_apply_lanes(s, sd, g, ctx, lab, nbl, act);
 #if OS_PHASE_TIMING
     OS_PH_ADD(ctx.sub[kPhGoApply], t1);
 #endif
   }
+  s.bw[0] = sel128(s.to_play == 0, sd.me, sd.them);
+  s.bw[1] = sel128(s.to_play == 0, sd.them, sd.me);
 #if OS_PHASE_TIMING
   const uint64_t t2 = OS_PH_NOW();
   const int r0 = Go::ret0(s, g, ctx);

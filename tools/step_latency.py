@@ -74,6 +74,21 @@ def measure(gs, sims, reps, torch):
     ks.append(e0.elapsed_time(e1))
   eng.fetch()
   kernel_ms = float(np.median(ks[1:]))
+  # the numpy-policy search (mcts.MCTSBot's kernel: np.random draws, one stream)
+  from os_amd import _lib
+  eng.prepare(acts, offs, [3], [3], uct_c=2.0, max_simulations=sims, max_memory_mb=0,
+              policy=_lib.POLICY_NUMPY)
+  ks = []
+  for _ in range(reps + 1):
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    eng.run_async(stream.cuda_stream)
+    e1.record(stream)
+    e1.synchronize()
+    ks.append(e0.elapsed_time(e1))
+  eng.fetch()
+  np_kernel_ms = float(np.median(ks[1:]))
   # oracle, one core
   og = O.Game(gs)
   osecs = []
@@ -84,7 +99,8 @@ def measure(gs, sims, reps, torch):
   return {"game": gs, "sims": sims, "cpp_step_ms": cpp_ms, "py_step_ms": py_ms,
           "kernel_ms": kernel_ms, "host_overhead_ms": cpp_ms - kernel_ms,
           "host_overhead_frac": (cpp_ms - kernel_ms) / kernel_ms,
-          "py_overhead_frac": (py_ms - kernel_ms) / kernel_ms,
+          "np_kernel_ms": np_kernel_ms, "py_overhead_ms": py_ms - np_kernel_ms,
+          "py_overhead_frac": (py_ms - np_kernel_ms) / np_kernel_ms,
           "oracle_1core_ms": float(np.median(osecs)),
           "gpu_over_oracle": float(np.median(osecs)) / cpp_ms}
 
@@ -107,13 +123,16 @@ def main():
   with open(os.path.join(args.out, "step_latency.json"), "w") as f:
     json.dump(rows, f, indent=1)
   with open(os.path.join(args.out, "step_latency.md"), "w") as f:
-    f.write("| game | sims | pyspiel.MCTSBot.step ms | mcts.MCTSBot.step ms | kernel ms | "
-            "host overhead | oracle 1 core ms | oracle / GPU step |\n|---|---|---|---|---|---|---|---|\n")
+    f.write("| game | sims | pyspiel.MCTSBot.step ms | its kernel ms | host overhead | "
+            "mcts.MCTSBot.step ms | its kernel ms (numpy policy) | host overhead | "
+            "oracle 1 core ms | oracle / GPU step |\n|---|---|---|---|---|---|---|---|---|---|\n")
     for r in rows:
-      f.write("| %s | %d | %.3f | %.3f | %.3f | %.3f ms (%.1f%%) | %.2f | %.2f |\n" % (
-          r["game"], r["sims"], r["cpp_step_ms"], r["py_step_ms"], r["kernel_ms"],
-          r["host_overhead_ms"], 100 * r["host_overhead_frac"], r["oracle_1core_ms"],
-          r["gpu_over_oracle"]))
+      f.write("| %s | %d | %.3f | %.3f | %.3f ms (%.1f%%) | %.3f | %.3f | %.3f ms (%.1f%%) | "
+              "%.2f | %.2f |\n" % (
+                  r["game"], r["sims"], r["cpp_step_ms"], r["kernel_ms"], r["host_overhead_ms"],
+                  100 * r["host_overhead_frac"], r["py_step_ms"], r["np_kernel_ms"],
+                  r["py_overhead_ms"], 100 * r["py_overhead_frac"], r["oracle_1core_ms"],
+                  r["gpu_over_oracle"]))
 
 
 if __name__ == "__main__":
