@@ -1481,7 +1481,9 @@ struct GoNbrLanes {
     m0 = mk(l);
     m1 = mk(l + 64);
   }
-  __device__ B128 any(B128 x) const {
+  __device__ B128 any(B128 x) const { return any_but(x, -1); }
+  // any(x) without point `skip` (-1: none): the ko point drops out in the same v_cmp.
+  __device__ B128 any_but(B128 x, int skip) const {
     const uint64_t elo = x.lo << n;
     const uint64_t ehi = (x.hi << n) | (x.lo >> (64 - n));
     const uint32_t e0 = static_cast<uint32_t>(elo), e1 = static_cast<uint32_t>(elo >> 32);
@@ -1491,7 +1493,7 @@ struct GoNbrLanes {
     const bool up = l >= 32;
     const uint32_t w0 = __builtin_amdgcn_alignbit(up ? e2 : e1, up ? e1 : e0, l & 31);
     const uint32_t w1 = __builtin_amdgcn_alignbit(up ? e4 : e3, up ? e3 : e2, l & 31);
-    return b128(ballot((w0 & m0) != 0), ballot((w1 & m1) != 0));
+    return b128(ballot((w0 & m0) != 0 && l != skip), ballot((w1 & m1) != 0 && l + 64 != skip));
   }
   // any(bit128(a)): a is p's neighbour iff t = a - p + n is one of p's window
   // bits, so no one-hot set is built and shifted.
@@ -1510,20 +1512,15 @@ struct GoSides {
   B128 me, them;
 };
 
-// Go::legal with the neighbourhoods on the lanes (same mask, go_board.cc:425-440).
+// Go::legal with the neighbourhoods on the lanes (same mask, go_board.cc:425-440):
+// Go::legal's cand & (nbr4(E) | (hard & nbr4(good))) is E & ~ko & nbr4(E | good),
+// one neighbourhood with the ko point dropped in its compare.
 __device__ __forceinline__ Go::Legal go_legal_lanes(const Go::State& s, const GoSides& sd,
                                                     const GameCfg& g, const GoNbrLanes& nb) {
   using M = CfgMasks<B128>;
   const B128 E = M::board(g) & ~(sd.me | sd.them);
-  B128 cand = E;
-  if (s.ko >= 0) cand = cand & ~bit128(s.ko);
-  const B128 has_lib = nb.any(E);
-  B128 mask = cand & has_lib;
-  const B128 hard = cand & ~has_lib;
-  if (any(hard)) {
-    const B128 good = (sd.me & ~s.atari) | (sd.them & s.atari);
-    mask = mask | (hard & nb.any(good));
-  }
+  const B128 good = (sd.me & ~s.atari) | (sd.them & s.atari);
+  const B128 mask = E & nb.any_but(E | good, s.ko);
   Go::Legal l;
   l.mask = mask;
   l.count = popc(mask) + 1;
@@ -1603,11 +1600,17 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const 
       }
       atari = (atari & ~ch) | sel128(popc(libs) == 1, ch, b128(0, 0));
     }
-    B128 todo = pb | (any(capd) ? nbl.any(capd) & own : b128(0, 0));
-    while (any(todo)) {
-      const B128 ch = lab.chain(lab.at(lowest(todo))) & own;
-      todo = todo & ~ch;
+    // The mover's chain (label a) and, after captures, the own chains next to
+    // the captured stones.
+    {
+      const B128 ch = lab.chain(a) & own;
       atari = (atari & ~ch) | sel128(popc(nbl.any(ch) & E) == 1, ch, b128(0, 0));
+      B128 todo = any(capd) ? nbl.any(capd) & own & ~ch : b128(0, 0);
+      while (any(todo)) {
+        const B128 cx = lab.chain(lab.at(lowest(todo))) & own;
+        todo = todo & ~cx;
+        atari = (atari & ~cx) | sel128(popc(nbl.any(cx) & E) == 1, cx, b128(0, 0));
+      }
     }
     s.atari = atari;
     sd.me = opp;  // the next player's stones
