@@ -21,7 +21,7 @@ for c in $CFGS; do
     # many-launch configs would exceed what gpurun copies back).
     case $c in
       c2|c3|c4) K=k_wsearch ;; c5) K=k_rollouts ;; sp) K=k_wselfplay ;;
-      az) K=k_az_step ;; g9) K=k_lsearch ;;
+      az) K=k_waz_step ;; g9) K=k_lsearch ;;
     esac
     case $c in
       c2|sp|az) G=connect_four ;; c3) G=breakthrough ;; c4) G=hex ;; c5|g9) G=go ;;
