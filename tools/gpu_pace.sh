@@ -13,3 +13,6 @@ for tag in main pe64 pe128 main; do
 done
 timeout -k 10 300 python -u bench.py --config c5 --roots 131072 --steps 10 --warmup 3 --no-cpu-baseline --no-parity-sweep > "$OUT/c5_131072.json" 2> "$OUT/c5_131072.err" || exit 1
 python -c "import json;d=json.load(open('$OUT/c5_131072.json'));print('c5 per-rank 131072', d['value'], d['ms_per_step'], d['parity'])"
+mkdir -p gpurun_out/r4n
+timeout -k 10 500 python -u tools/step_latency.py --reps 7 --out gpurun_out/r4n/step_latency > gpurun_out/r4n/step_latency.log 2>&1 || { tail -20 gpurun_out/r4n/step_latency.log; exit 1; }
+cat gpurun_out/r4n/step_latency/step_latency.md
