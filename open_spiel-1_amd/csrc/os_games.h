@@ -636,12 +636,17 @@ struct GoCtxBloom {
 using GoCtx = GoCtxT<uint8_t>;
 using GoCtxW = GoCtxT<uint16_t>;
 
-// 1: GoT::apply floods a chain only where its liberty count is unknown
-// (see apply); 0: every touched chain is flooded (the round-3 form).  Both
-// bit-exact; 0 measured faster (g9 496 vs 505 ms, C5 14.7 vs 15.1 ms:
-// profiles/r04/ab_go.md), so it is the default.
+// How GoT::apply keeps the atari set (all three exact):
+// 0: every touched chain is flooded to its full extent (the round-3 form);
+// 1: chains are flooded only where a liberty count is unknown (see apply) --
+//    measured slower on the lane kernels (g9 505 vs 496 ms, C5 15.1 vs
+//    14.7 ms, profiles/r04/go_ab/): its three branches diverge across lanes;
+// 2: as 1, but one kind of flood for every chain whose count is unknown,
+//    which stops as soon as it has seen two liberties (flood_libs2): a chain
+//    with two liberties is out of atari whatever its extent, so most floods
+//    end after one or two steps instead of the chain's diameter.
 #ifndef OS_GO_LAZY_ATARI
-#define OS_GO_LAZY_ATARI 0
+#define OS_GO_LAZY_ATARI 2
 #endif
 
 template <class B>
@@ -670,6 +675,21 @@ struct GoT {
     B c = seed;
     for (;;) {
       B nx = (c | nbr4(c, g)) & within;
+      if (nx == c) return c;
+      c = nx;
+    }
+  }
+  // The chain of `seed` within `within`, grown until it is complete or shows
+  // two liberties (empty points of E next to it).  Returns the stones reached;
+  // *libs = the liberties seen: when popc(*libs) < 2 the chain is complete and
+  // *libs are all its liberties.
+  OS_HD static B flood_libs2(B seed, B within, B E, const GameCfg& g, B* libs) {
+    B c = seed;
+    for (;;) {
+      const B n4 = nbr4(c, g);
+      *libs = n4 & E;
+      if (popc(*libs) >= 2) return c;
+      const B nx = (c | n4) & within;
       if (nx == c) return c;
       c = nx;
     }
@@ -746,7 +766,56 @@ struct GoT {
       B atari = s.atari;
       B capd = BB<B>::zero();
       B on = nb & opp;
-#if OS_GO_LAZY_ATARI
+#if OS_GO_LAZY_ATARI == 2
+      // Captures: an opponent chain next to a that was in atari had a as its
+      // only liberty; `flood(q, opp & atari)` is its chain (two same-coloured
+      // atari chains never touch).  Any other opponent chain next to a keeps
+      // >= 1 liberty (points freed by this move's captures were stones of its
+      // own colour, so they never touch it) and enters atari iff exactly one
+      // is left: flood_libs2 answers that without walking the whole chain (a
+      // partial answer leaves the set unchanged; another stone of the same
+      // chain in `on` only repeats it).  Own chains in atari next to a (they
+      // merge into a's chain) or next to captured stones leave the set; a's
+      // chain enters it iff it has exactly one liberty.  Same set as mode 0.
+      const B opp_at = opp & atari;
+      while (any(on)) {
+        const int q = lowest(on);
+        const B qb = BB<B>::bit(q);
+        if (any(qb & opp_at)) {
+          const B ch = flood(qb, opp_at, g);
+          on = on & ~ch;
+          opp = opp & ~ch;
+          E = E | ch;
+          capd = capd | ch;
+          captured += popc(ch);
+          cap_pt = q;
+          atari = atari & ~ch;
+          B rem = ch;
+          while (any(rem)) {
+            const int x = lowest(rem);
+            rem = rem & ~BB<B>::bit(x);
+            s.hash ^= ctx.zob[2 * x + (1 - c)];
+          }
+        } else {
+          B libs;
+          const B ch = flood_libs2(qb, opp, E, g, &libs);
+          on = on & ~ch;
+          atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
+        }
+      }
+      const B own_at = own0 & atari;
+      B touched = (nb | nbr4(capd, g)) & own_at;
+      while (any(touched)) {
+        const B ch = flood(BB<B>::bit(lowest(touched)), own_at, g);
+        touched = touched & ~ch;
+        atari = atari & ~ch;
+      }
+      {
+        B libs;
+        const B ch = flood_libs2(pb, own, E, g, &libs);
+        atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
+      }
+#elif OS_GO_LAZY_ATARI
       // Full chain floods only where a liberty count is unknown.  A chain is in
       // `atari` as a whole, and two same-coloured atari chains never touch, so
       // flood(q, colour & atari) is q's chain whenever q is in atari -- a flood
