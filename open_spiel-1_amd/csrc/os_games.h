@@ -490,6 +490,16 @@ struct Filter256 {
 // scan -- and the buckets give the same answers as testing the whole set.
 // Positions before the root (`base`, counts unknown) are scanned behind a
 // 256-bit pre-filter.  Arrays may be batch-SoA: element i at [i * stride].
+#ifndef OS_GO_NOWALK
+#define OS_GO_NOWALK 0
+#endif
+// OS_GO_LOG_BLOOM: the lane kernels' go superko logs (k_rollouts, k_lsearch)
+// keep a 512-bit Bloom filter per lane in LDS in front of the bucket walk
+// (GoCtxT::bloom; exact).  A timing A/B without the walk at all
+// (OS_GO_NOWALK, not exact) put the walk at 10% of C5 and 17% of g9.
+#ifndef OS_GO_LOG_BLOOM
+#define OS_GO_LOG_BLOOM 1
+#endif
 template <class H>
 struct GoCtxT {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
@@ -504,11 +514,36 @@ struct GoCtxT {
   int32_t cap;
   int32_t n_heads;         // cells + 1
   Filter256 base_filt;     // base hashes
+  // Optional Bloom filter over the log (kBloomWords words, word w at
+  // bloom[w * head_stride]; nullptr: none).  A position whose bucket is not
+  // empty is compared with it only when both of its filter bits are set --
+  // a miss proves absence, so the answers stay exact -- which spares most of
+  // the bucket walks' dependent HBM reads (k_rollouts / k_lsearch keep it in
+  // LDS next to the bucket heads).
+  uint32_t* bloom = nullptr;
+  static constexpr int kBloomWords = 16;  // 512 bits, 2 bits per position
+
+  OS_HD static int bbit0(uint64_t h) { return static_cast<int>(h & 511u); }
+  OS_HD static int bbit1(uint64_t h) { return static_cast<int>((h >> 9) & 511u); }
+  OS_HD bool bloom_has(uint64_t h) const {
+    const int x = bbit0(h), y = bbit1(h);
+    return ((bloom[(x >> 5) * head_stride] >> (x & 31)) & 1u) &&
+           ((bloom[(y >> 5) * head_stride] >> (y & 31)) & 1u);
+  }
+  OS_HD void bloom_add(uint64_t h) {
+    const int x = bbit0(h), y = bbit1(h);
+    bloom[(x >> 5) * head_stride] |= 1u << (x & 31);
+    bloom[(y >> 5) * head_stride] |= 1u << (y & 31);
+  }
+  OS_HD void bloom_clear() {
+    for (int w = 0; w < kBloomWords; ++w) bloom[w * head_stride] = 0u;
+  }
 
   // Empties the log (the base stays).
   OS_HD void reset() {
     n_log = 0;
     for (int k = 0; k < n_heads; ++k) head[k * head_stride] = 0;
+    if (bloom) bloom_clear();
   }
   // Builds base_filt from base[0, n_base) and resets.
   OS_HD void init_filters() {
@@ -525,6 +560,10 @@ struct GoCtxT {
     if (base_filt.has(fbit(h)))
       for (int i = 0; i < n_base; ++i)
         if (base[i] == h) return true;
+#if OS_GO_NOWALK  // timing A/B only (not exact): no bucket walk
+    return false;
+#endif
+    if (bloom && head[stones * head_stride] != 0 && !bloom_has(h)) return false;
 #if OS_DEBUG_GOLOG
     int steps = 0;
 #endif
@@ -551,6 +590,10 @@ struct GoCtxT {
       const uint32_t lk = link[static_cast<int64_t>(n_log) * stride];
       head[static_cast<int>(lk >> 16) * head_stride] = static_cast<H>(lk & 0xFFFFu);
     }
+    if (bloom) {  // a Bloom filter cannot forget: rebuilt from the entries kept
+      bloom_clear();
+      for (int e = 0; e < n_log; ++e) bloom_add(log[static_cast<int64_t>(e) * stride]);
+    }
   }
   // Logs the position after a non-pass move; false if it was already present
   // (go.cc:201-205).
@@ -563,6 +606,7 @@ struct GoCtxT {
       log[e] = h;
       link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
       head[hk] = static_cast<H>(n_log + 1);
+      if (bloom) bloom_add(h);
       ++n_log;
     }
     return true;
@@ -719,18 +763,14 @@ struct GoT {
     const B E = M::board(g) & ~(s.bw[0] | s.bw[1]);
     B cand = E;
     if (s.ko >= 0) cand = cand & ~BB<B>::bit(s.ko);
-    const B has_lib = nbr4(E, g);
-    B mask = cand & has_lib;
-    const B hard = cand & ~has_lib;
-    if (any(hard)) {
-      // A surrounded point is legal iff it joins an own chain that keeps a
-      // liberty (>= 2 now) or captures an opponent chain in atari
-      // (go_board.cc:425-440).  Every stone's chain has >= 1 liberty, so with
-      // the atari set both are masks: no chain is flooded here.
-      const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-      const B good = (own & ~s.atari) | (opp & s.atari);
-      mask = mask | (hard & nbr4(good, g));
-    }
+    // A point with an empty neighbour is legal; a surrounded one iff it joins
+    // an own chain that keeps a liberty (>= 2 now) or captures an opponent
+    // chain in atari (go_board.cc:425-440).  Every stone's chain has >= 1
+    // liberty, so with the atari set both are masks ("good" stones), and
+    // cand & (nbr4(E) | nbr4(good)) is one neighbourhood: cand & nbr4(E | good).
+    const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+    const B good = (own & ~s.atari) | (opp & s.atari);
+    const B mask = cand & nbr4(E | good, g);
     Legal l;
     l.mask = mask;
     l.count = popc(mask) + 1;

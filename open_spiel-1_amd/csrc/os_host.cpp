@@ -366,7 +366,7 @@ std::string LoadHostGame(const std::string& gs, HostGame* g, bool* unsupported) 
 
 GoCtx HostGoCtx(const HostState& s, HostGoLog* buf) {
   GoCtx ctx;
-  std::memset(&ctx, 0, sizeof ctx);
+  std::memset(static_cast<void*>(&ctx), 0, sizeof ctx);
   const GameCfg& g = s.game->cfg;
   ctx.zob = s.game->zob.data();
   ctx.base = s.hashes.data();

@@ -170,19 +170,20 @@ __global__ __launch_bounds__(64) void k_mcts(DevArgs a) {
 // boards above 11 x 11 keep u16 heads per search in HBM), position-log cap.
 template <class G>
 struct LsCaps {
-  static constexpr int act = 1, zob = 1, heads = 1, log = 1;
+  static constexpr int act = 1, zob = 1, heads = 1, log = 1, bloom = 1;
 };
 template <>
 struct LsCaps<Go> {
-  static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads * 64, log = kGoLogCap;
+  static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads * 64, log = kGoLogCap,
+                       bloom = GoCtx::kBloomWords * 64;
 };
 template <>
 struct LsCaps<GoBig> {  // actions up to 361: u16 expansion buffers in HBM
-  static constexpr int act = 1, zob = 2 * 361, heads = 1, log = kGoLogCapBig;
+  static constexpr int act = 1, zob = 2 * 361, heads = 1, log = kGoLogCapBig, bloom = 1;
 };
 template <>
 struct LsCaps<HexBig> {  // actions up to 360: u16 expansion buffers in HBM
-  static constexpr int act = 1, zob = 1, heads = 1, log = 1;
+  static constexpr int act = 1, zob = 1, heads = 1, log = 1, bloom = 1;
 };
 template <class G>
 struct LsWide : std::false_type {};  // Node<R, true>: 16-bit child counts
@@ -193,11 +194,13 @@ struct LsWide<HexBig> : std::true_type {};
 
 template <class G>
 struct LCtx {
-  __device__ static NoCtx make(const DevArgs&, int64_t, int64_t, uint8_t*) { return NoCtx(); }
+  __device__ static NoCtx make(const DevArgs&, int64_t, int64_t, uint8_t*, uint32_t*) {
+    return NoCtx();
+  }
 };
 template <>
 struct LCtx<GoBig> {
-  __device__ static GoCtxW make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t*) {
+  __device__ static GoCtxW make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t*, uint32_t*) {
     GoCtxW c;
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
@@ -216,7 +219,8 @@ struct LCtx<GoBig> {
 };
 template <>
 struct LCtx<Go> {
-  __device__ static GoCtx make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t* lds_heads) {
+  __device__ static GoCtx make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t* lds_heads,
+                               uint32_t* lds_bloom) {
     GoCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
@@ -225,6 +229,11 @@ struct LCtx<Go> {
     c.link = a.lglink + lr * kGoLogCap;
     c.head = lds_heads + (threadIdx.x & 63);
     c.head_stride = 64;
+#if OS_GO_LOG_BLOOM
+    c.bloom = lds_bloom + (threadIdx.x & 63);
+#else
+    (void)lds_bloom;
+#endif
     c.stride = 1;
     c.n_log = 0;
     c.cap = kGoLogCap;
@@ -260,6 +269,7 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   // LDS: go's bucket heads and the expansion buffers, lane-interleaved
   // ([i][64]), and the Zobrist table (read by every move of every lane).
   __shared__ uint8_t heads[LsCaps<G>::heads];
+  __shared__ uint32_t lbloom[OS_GO_LOG_BLOOM ? LsCaps<G>::bloom : 1];  // go: superko log filter
   __shared__ uint8_t acts[LsCaps<G>::act * 64];  // go actions up to 15 x 15 are < 256
   __shared__ uint64_t zob[LsCaps<G>::zob];
   if constexpr (G::State::kNeedsLog) {
@@ -287,7 +297,7 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
     ev.seed(a.eval_seeds[gr]);
   }
   StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
-  auto ctx = LCtx<G>::make(a, gr, lr, heads);
+  auto ctx = LCtx<G>::make(a, gr, lr, heads, lbloom);
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
 #if OS_LS_AB & 2
   if constexpr (G::State::kNeedsLog) ctx.cap = 0;
@@ -1644,7 +1654,9 @@ struct RollCtx<Go> {
 template <>
 struct RollCtx<Go> {
   using type = GoCtx;
-  static constexpr int kLdsWords = (kGoHeads * 64 + 3) / 4;
+  // heads (cells + 1 bytes per lane), then the log's Bloom filter
+  // (OS_GO_LOG_BLOOM): launched with RollLdsBytes of dynamic LDS.
+  static constexpr int kLdsWords = (kGoHeads * 64 + 3) / 4 + GoCtx::kBloomWords * 64;
   // The bucket heads are the only per-move accesses that differ across the
   // lanes (each lane is at its own stone count): they live in LDS, lane-
   // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
@@ -1665,6 +1677,9 @@ struct RollCtx<Go> {
 #endif
     c.head = lds_heads + (threadIdx.x & 63);
     c.head_stride = 64;
+#if OS_GO_LOG_BLOOM
+    c.bloom = lds + (((a.cfg.rows * a.cfg.cols + 1) * 64 + 3) / 4) + (threadIdx.x & 63);
+#endif
     c.n_log = 0;
     c.cap = kGoLogCap;
     c.n_heads = a.cfg.rows * a.cfg.cols + 1;
@@ -1747,7 +1762,7 @@ __global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
   RollMt ev{a.mt + i, a.n, 0, 0};
 #endif
   ev.seed(a.seeds[i]);
-  __shared__ uint32_t roll_lds[RollCtx<G>::kLdsWords];
+  extern __shared__ uint32_t roll_lds[];  // RollLdsBytes<G>(cfg) bytes
   typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
@@ -2099,6 +2114,23 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   }
 }
 
+// k_rollouts' dynamic LDS: go's bucket heads for this board size (one byte
+// per stone count per lane) and the log's Bloom filter; the heads' static
+// bound (11 x 11) would cost occupancy on 9 x 9.
+template <class G>
+size_t RollLdsBytes(const GameCfg& c) {
+#if OS_ROLL_BLOOM
+  (void)c;
+  return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
+#else
+  if constexpr (std::is_same<G, Go>::value)
+    return 4 * (((c.rows * c.cols + 1) * 64 + 3) / 4 +
+                (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * 64 : 0));
+  else
+    return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
+#endif
+}
+
 template <class G>
 int RollLaunch(os_engine* e, hipStream_t stream) {
   RollArgs a;
@@ -2130,7 +2162,7 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   {
     const int bs = 64;
     hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                       dim3(bs), 0, stream, a);
+                       dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
   }
   HIP_TRY(hipGetLastError());
   return OS_OK;

@@ -1601,7 +1601,9 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const 
       atari = (atari & ~ch) | sel128(popc(libs) == 1, ch, b128(0, 0));
     }
     // The mover's chain (label a) and, after captures, the own chains next to
-    // the captured stones.
+    // the captured stones.  (Skipping the liberty counts where the atari set
+    // or two empty neighbours settle them was measured slower here: 1.70e7 ->
+    // 1.63e7 sims/s at 4096 roots; the lane kernels do use it, GoT::apply.)
     {
       const B128 ch = lab.chain(a) & own;
       atari = (atari & ~ch) | sel128(popc(nbl.any(ch) & E) == 1, ch, b128(0, 0));

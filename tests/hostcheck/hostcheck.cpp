@@ -35,7 +35,7 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
   typename G::Ctx ctx;
   HostGoLog logbuf;
   if constexpr (G::State::kNeedsLog) {
-    std::memset(&ctx, 0, sizeof ctx);
+    std::memset(static_cast<void*>(&ctx), 0, sizeof ctx);
     ctx.zob = game.zob.data();
     ctx.base = root.hashes.data();
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
@@ -199,7 +199,7 @@ int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp
   sl->s = rs;
   typename G::Ctx ctx;
   if constexpr (G::State::kNeedsLog) {
-    std::memset(&ctx, 0, sizeof ctx);
+    std::memset(static_cast<void*>(&ctx), 0, sizeof ctx);
     ctx.zob = game.zob.data();
     ctx.base = root.hashes.data();
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
@@ -430,7 +430,7 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
       case kPig: { NoCtx c; r0 = rollout_ret0_chance<Pig, kPolicyCpp>(*reinterpret_cast<Pig::State*>(hs.raw), game.cfg, c, ev); break; }
       case kGo: {
         GoCtx c;
-        std::memset(&c, 0, sizeof c);
+        std::memset(static_cast<void*>(&c), 0, sizeof c);
         c.zob = game.zob.data();
         c.base = hs.hashes.data();
         c.n_base = static_cast<int32_t>(hs.hashes.size());
@@ -447,6 +447,43 @@ int hc_rollouts(const char* game_string, const int64_t* actions, int64_t n_actio
 }
 
 // The same go playouts with the k_rollouts superko screen (GoCtxBloom).
+// go playouts with the bucketed superko log behind its Bloom filter
+// (GoCtxT::bloom, as k_rollouts / k_lsearch run it).
+int hc_rollouts_go_logbloom(const char* game_string, const int64_t* actions, int64_t n_actions,
+                            int64_t n, const uint32_t* seeds, double* out) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty() || game.cfg.kind != kGo) {
+    g_err = err.empty() ? "go only" : err;
+    return -1;
+  }
+  HostState hs;
+  hs.game = &game;
+  StateInit(&hs);
+  for (int64_t i = 0; i < n_actions; ++i) StateApply(&hs, actions[i]);
+  std::vector<uint32_t> mt(kMtN);
+  HostGoLog logbuf;
+  std::vector<uint32_t> bloom(GoCtx::kBloomWords * 64);
+  for (int64_t i = 0; i < n; ++i) {
+    MtStream ev{mt.data(), kMtN, 0};
+    mt_seed(ev.s, seeds[i]);
+    GoCtx c;
+    std::memset(static_cast<void*>(&c), 0, sizeof c);
+    c.zob = game.zob.data();
+    c.base = hs.hashes.data();
+    c.n_base = static_cast<int32_t>(hs.hashes.size());
+    logbuf.bind(&c, 248, game.cfg.rows * game.cfg.cols);
+    c.bloom = bloom.data();
+    c.init_filters();
+    const int r0 = rollout_ret0<Go, kPolicyCpp>(*reinterpret_cast<Go::State*>(hs.raw), game.cfg,
+                                                c, ev);
+    out[2 * i] = r0;
+    out[2 * i + 1] = -r0;
+  }
+  return 0;
+}
+
 int hc_rollouts_go_bloom(const char* game_string, const int64_t* actions, int64_t n_actions,
                          int64_t n, const uint32_t* seeds, double* out) {
   HostGame game;
@@ -467,7 +504,7 @@ int hc_rollouts_go_bloom(const char* game_string, const int64_t* actions, int64_
     MtStream ev{mt.data(), kMtN, 0};
     mt_seed(ev.s, seeds[i]);
     GoCtxBloom c;
-    std::memset(&c, 0, sizeof c);
+    std::memset(static_cast<void*>(&c), 0, sizeof c);
     c.zob = game.zob.data();
     c.base = hs.hashes.data();
     c.n_base = static_cast<int32_t>(hs.hashes.size());

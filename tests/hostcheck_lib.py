@@ -26,6 +26,7 @@ def lib():
     L.hc_rollouts.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.c_int64,
                               vp, vp]
     L.hc_rollouts_go_bloom.argtypes = L.hc_rollouts.argtypes
+    L.hc_rollouts_go_logbloom.argtypes = L.hc_rollouts.argtypes
     L.hc_go_score.restype = ctypes.c_float
     L.hc_go_score.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64]
     L.hc_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
@@ -216,6 +217,18 @@ def az_batch(game_string, acts, offs, bot_seeds, max_children, eval_fn, puct=Tru
     raise RuntimeError(L.hc_last_error().decode())
   o["calls"] = calls[0]
   return o
+
+
+def rollouts_go_logbloom(game_string, history, seeds):
+  """go playouts with the bucketed superko log behind GoCtxT's Bloom filter."""
+  a = np.ascontiguousarray(history, np.int64)
+  s = np.ascontiguousarray(seeds, np.uint32)
+  out = np.zeros((len(s), 2), np.float64)
+  rc = lib().hc_rollouts_go_logbloom(game_string.encode(), a.ctypes.data, len(a), len(s),
+                                     s.ctypes.data, out.ctypes.data)
+  if rc:
+    raise RuntimeError(lib().hc_last_error().decode())
+  return out
 
 
 def rollouts_go_bloom(game_string, history, seeds):
