@@ -493,6 +493,11 @@ struct Filter256 {
 #ifndef OS_GO_NOWALK
 #define OS_GO_NOWALK 0
 #endif
+// Contexts of wave-uniform code (GoWaveCtx) declare kWaveUniform.
+template <class C, class = void>
+struct WaveUniformCtx : std::false_type {};
+template <class C>
+struct WaveUniformCtx<C, std::void_t<decltype(C::kWaveUniform)>> : std::true_type {};
 // OS_GO_LOG_BLOOM: the lane kernels' go superko logs (k_rollouts, k_lsearch)
 // keep a 512-bit Bloom filter per lane in LDS in front of the bucket walk
 // (GoCtxT::bloom; exact).  A timing A/B without the walk at all
@@ -768,9 +773,24 @@ struct GoT {
     // chain in atari (go_board.cc:425-440).  Every stone's chain has >= 1
     // liberty, so with the atari set both are masks ("good" stones), and
     // cand & (nbr4(E) | nbr4(good)) is one neighbourhood: cand & nbr4(E | good).
-    const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
-    const B good = (own & ~s.atari) | (opp & s.atari);
-    const B mask = cand & nbr4(E | good, g);
+    B mask;
+    if constexpr (WaveUniformCtx<C>::value) {
+      // Wave-uniform (scalar unit): the second neighbourhood only when some
+      // point is surrounded -- rare near the root, where the wave search's
+      // tree positions are (3% faster there; the lanes prefer one form).
+      const B has_lib = nbr4(E, g);
+      mask = cand & has_lib;
+      const B hard = cand & ~has_lib;
+      if (any(hard)) {
+        const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+        const B good = (own & ~s.atari) | (opp & s.atari);
+        mask = mask | (hard & nbr4(good, g));
+      }
+    } else {
+      const B own = pick(s.bw, c), opp = pick(s.bw, 1 - c);
+      const B good = (own & ~s.atari) | (opp & s.atari);
+      mask = cand & nbr4(E | good, g);
+    }
     Legal l;
     l.mask = mask;
     l.count = popc(mask) + 1;

@@ -454,6 +454,7 @@ struct WaveMt {
 // capture -- without a capture the stone count only grows, so no later
 // position can repeat (the same rule as GoCtx, os_games.h).
 struct GoWaveCtx {
+  static constexpr bool kWaveUniform = true;  // GoT::legal: the scalar-unit form
 #if OS_PHASE_TIMING
   uint64_t* sub;  // PhaseCycles::c of the search (go breakdown)
 #endif
@@ -1423,6 +1424,8 @@ __device__ int bt_rollout_wave(Breakthrough::State s, const GameCfg& g, Rng& ev)
 
 struct GoLabels {
   int32_t l0, l1;  // per lane: labels of points lane, lane + 64
+  // One select on the lanes and one readlane (no branch on the slot).
+  // (A select of the slot and one readlane instead of the branch: 1% slower.)
   __device__ int at(int q) const { return q < 64 ? rli(l0, q) : rli(l1, q - 64); }
   __device__ B128 chain(int lab) const { return b128(ballot(l0 == lab), ballot(l1 == lab)); }
   __device__ void relabel(int from, int to) {
