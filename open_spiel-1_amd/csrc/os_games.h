@@ -827,6 +827,10 @@ struct GoT {
       B capd = BB<B>::zero();
       B on = nb & opp;
 #if OS_GO_LAZY_ATARI == 2
+      // Wave-uniform callers (the wave search's tree moves, on the scalar unit)
+      // keep the full floods: the early-stopping form costs the numpy-policy
+      // wave kernel its registers (248 VGPRs + 1 KB scratch against 115).
+      if constexpr (!WaveUniformCtx<C>::value) {
       // Captures: an opponent chain next to a that was in atari had a as its
       // only liberty; `flood(q, opp & atari)` is its chain (two same-coloured
       // atari chains never touch).  Any other opponent chain next to a keeps
@@ -874,6 +878,34 @@ struct GoT {
         B libs;
         const B ch = flood_libs2(pb, own, E, g, &libs);
         atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
+      }
+      } else {
+      while (any(on)) {
+        const int q = lowest(on);
+        const B ch = flood(BB<B>::bit(q), opp, g);
+        on = on & ~ch;
+        const B libs = nbr4(ch, g) & E;
+        if (!any(libs)) {
+          opp = opp & ~ch;
+          E = E | ch;
+          capd = capd | ch;
+          captured += popc(ch);
+          cap_pt = q;
+          B rem = ch;
+          while (any(rem)) {
+            const int x = lowest(rem);
+            rem = rem & ~BB<B>::bit(x);
+            s.hash ^= ctx.zob[2 * x + (1 - c)];
+          }
+        }
+        atari = (atari & ~ch) | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
+      }
+      B todo = pb | (nbr4(capd, g) & own);
+      while (any(todo)) {
+        const B ch = flood(BB<B>::bit(lowest(todo)), own, g);
+        todo = todo & ~ch;
+        atari = (atari & ~ch) | BB<B>::sel(popc(nbr4(ch, g) & E) == 1, ch, BB<B>::zero());
+      }
       }
 #elif OS_GO_LAZY_ATARI
       // Full chain floods only where a liberty count is unknown.  A chain is in
