@@ -98,7 +98,9 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
   res.max_depth = 0;
   res.scanned = res.backed = res.expanded = res.solver_scanned = 0;
   const int P0 = G::to_move(root);
-  int8_t chooser[kChancePathCap];  // player choosing at path node d (-1: chance)
+  // The player choosing at path node d (-1: chance) lives in path[d].nc, a
+  // field this search does not otherwise use: a per-thread array indexed by
+  // depth would sit in scratch memory.
   if (path_cap > kChancePathCap) path_cap = kChancePathCap;
   nodes[0].first = 0;
   nodes[0].n = 0;
@@ -122,7 +124,7 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
       const Node<R> nx = nodes[x];
       if (G::terminal(s, g) || nx.n <= 0) break;
       const int cp = G::to_move(s);  // -1 at a chance node
-      chooser[depth] = static_cast<int8_t>(cp);
+      path[depth].nc = cp;
       uint32_t first = nx.first;
       int nc = nx.nchild;
       const typename G::Legal l = G::legal(s, g, ctx);
@@ -206,20 +208,20 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
       // ---- backup + MCTS-Solver (mcts.cc:351-396) ----
       for (int d = depth; d >= 0; --d) {
         Node<R>& nd = nodes[path[d].idx];
-        const int pl = d == 0 ? P0 : reward_player(chooser[d - 1], P0);
+        const int pl = d == 0 ? P0 : reward_player(path[d - 1].nc, P0);
         nd.w += static_cast<R>(ret.of(pl));
         nd.n += 1;
         res.backed += 1;
         if (solved && nd.nchild > 0) {
           res.solver_scanned += nd.nchild;
-          if (chooser[d] < 0) {  // chance node: all children share one outcome
+          if (path[d].nc < 0) {  // chance node: all children share one outcome
             const int8_t o = nodes[nd.first].out;
             bool same = o != kUnsolved;
             for (int k = 1; k < nd.nchild; ++k) same = same && nodes[nd.first + k].out == o;
             if (same) nd.out = o;
             else solved = false;
           } else {
-            const int cpl = chooser[d];
+            const int cpl = path[d].nc;
             int best = -1;
             int8_t best_out = kUnsolved;
             double bestv = 0.0;
