@@ -257,7 +257,11 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
 // searches to fill the chip, so go takes it from 16384 roots.
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
   if (layout != OS_LAYOUT_AUTO) return layout;
-  if (cfg.kind == kPig || BigBoard(cfg)) return OS_LAYOUT_LANE;  // os_chance.h / k_lsearch
+  // pig (chance nodes): one wave per search (k_wsearch_chance) beats a lane
+  // per search at every batch size, 1.7x at one root and 4.3x from 64
+  // (tools/pig_layout_probe.py, profiles/r04/pig_layout.txt).
+  if (cfg.kind == kPig) return OS_LAYOUT_WAVE;
+  if (BigBoard(cfg)) return OS_LAYOUT_LANE;  // k_lsearch
   if (cfg.kind == kGo)
     return policy == OS_POLICY_CPP && R >= 16384 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
   if (cfg.kind == kHex)
@@ -327,7 +331,7 @@ int SizeArena(os_engine* e, bool allow_paged) {
   // mcts_search takes pages under every policy and child selection.
   const bool pageable_layout =
       (p->layout == OS_LAYOUT_WAVE && p->policy == OS_POLICY_CPP &&
-       p->child_selection == OS_SELECT_UCT) ||
+       p->child_selection == OS_SELECT_UCT && e->game.cfg.kind != kPig) ||
       p->layout == OS_LAYOUT_LANE;
   if (allow_paged && e->arena_mode == OS_ARENA_PAGED && pageable_layout &&
       !gc_possible && p->arena_nodes == 0 && R >= kPagedMinRoots &&

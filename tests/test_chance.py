@@ -157,6 +157,7 @@ def test_chance_node_api():
 @pytest.mark.parametrize("policy", ["cpp", "numpy"])
 @pytest.mark.parametrize("block", [0, 64])
 def test_gpu_search_matches_oracle(require_gpu, gs, policy, block):
+  # The lane layout (k_mcts; AUTO picks the wave layout for pig).
   # block 64: full wave64 workgroups, searches in lanes 32-63 too
   from os_amd import _lib
   R = 64 if block == 0 else 96
@@ -166,12 +167,13 @@ def test_gpu_search_matches_oracle(require_gpu, gs, policy, block):
   eng = E.Engine(gs)
   if policy == "cpp":
     ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_simulations=300, max_children=6)
-    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300, block_size=block)
+    got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300, block_size=block,
+                         layout=_lib.LAYOUT_LANE)
   else:
     ref = H.mcts_batch(gs, acts, offs, bs, es, 6, max_simulations=300,
                        policy=_lib.POLICY_NUMPY)
     got = eng.mcts_batch(acts, offs, bs, es, max_simulations=300, block_size=block,
-                         policy=_lib.POLICY_NUMPY)
+                         policy=_lib.POLICY_NUMPY, layout=_lib.LAYOUT_LANE)
   for k in E.OUTPUT_KEYS:
     np.testing.assert_array_equal(got[k], ref[k][:, :got[k].shape[1]] if ref[k].ndim == 2
                                   else ref[k], err_msg=k)
