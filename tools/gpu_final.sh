@@ -5,6 +5,8 @@
 #   tools/gpu_final.sh bench    one bench line per config (with cpu_baseline)
 #                               + rocprofv3 --kernel-trace --stats of each
 #   tools/gpu_final.sh pmc CFG...  PMC passes (tools/pmc_configs.sh)
+#   tools/gpu_final.sh extras   C5 per-rank line, 4096-root go9 wave line,
+#                               single-bot step latency (tools/step_latency.py)
 # Results under gpurun_out/final/.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -38,6 +40,17 @@ case "$part" in
     ;;
   pmc)
     bash "$R/tools/pmc_configs.sh" "$@" || exit 1
+    ;;
+  extras)
+    # per-rank C5 line (8-GPU share of the 2^20 playouts), the 4096-root go9
+    # wave line, and the single-bot step latency table
+    timeout -k 10 300 python -u bench.py --config c5 --roots 131072 --steps 10 --warmup 3 \
+      --no-cpu-baseline --no-parity-sweep > "$OUT/c5_131072.json" 2> "$OUT/c5_131072.err" || exit 1
+    timeout -k 10 300 python -u bench.py --config g9 --layout wave --roots 4096 --steps 2 \
+      --warmup 1 --no-cpu-baseline --no-parity-sweep > "$OUT/g9_wave_4096.json" \
+      2> "$OUT/g9_wave_4096.err" || exit 1
+    timeout -k 10 500 python -u tools/step_latency.py --reps 7 --out "$OUT/step_latency" \
+      > "$OUT/step_latency.log" 2>&1 || exit 1
     ;;
 esac
 echo "gpu_final $part done"
