@@ -19,18 +19,64 @@
 namespace osm {
 
 namespace {
-// A std::mt19937 that counts the words drawn from it (same URBG range, so
-// generate_canonical consumes it exactly as it consumes the engine itself).
+// std::mt19937(seed)'s output stream, counting the words drawn (same URBG
+// range, so generate_canonical consumes it exactly as it consumes the engine
+// itself).  A Dirichlet draw takes a few dozen words, so the first block is
+// twisted word by word from running cursors of the init_genrand recurrence
+// (x[i], x[i+1], x[i+397]) instead of seeding all 624 words and twisting
+// them up front -- the device streams' scheme (MtStreamSoA) -- and the full
+// state exists only once the first block is used up.
 struct CountingMt {
   using result_type = uint32_t;
-  std::mt19937 g;
+  uint32_t s[kMtN];   // twisted words of the current block
+  uint32_t lo0, lo1, hi;  // seeded x[i], x[i + 1], x[i + 397] (first block)
+  int idx = 0;
+  bool blk0 = true;
   int64_t words = 0;
-  explicit CountingMt(uint32_t seed) : g(seed) {}
-  static constexpr result_type min() { return std::mt19937::min(); }
-  static constexpr result_type max() { return std::mt19937::max(); }
+  static uint32_t seed_step(uint32_t x, int k) {
+    return 1812433253u * (x ^ (x >> 30)) + static_cast<uint32_t>(k);
+  }
+  explicit CountingMt(uint32_t seed) {
+    lo0 = seed;
+    lo1 = seed_step(seed, 1);
+    uint32_t x = lo1;
+    for (int k = 2; k <= kMtM; ++k) x = seed_step(x, k);
+    hi = x;
+  }
+  static constexpr result_type min() { return 0; }
+  static constexpr result_type max() { return 0xFFFFFFFFu; }
   result_type operator()() {
     ++words;
-    return static_cast<result_type>(g());
+    uint32_t v;
+    if (blk0) {
+      const int i = idx;
+      const uint32_t b = (i + 1 == kMtN) ? s[0] : lo1;
+      const uint32_t m = (i + kMtM < kMtN) ? hi : s[i + kMtM - kMtN];
+      const uint32_t y = (lo0 & 0x80000000u) | (b & 0x7fffffffu);
+      v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      s[i] = v;
+      lo0 = lo1;
+      lo1 = seed_step(lo1, i + 2);
+      hi = seed_step(hi, i + kMtM + 1);
+      if (++idx == kMtN) {
+        blk0 = false;
+        idx = 0;
+        Twist();
+      }
+    } else {
+      v = s[idx];
+      if (++idx == kMtN) {
+        idx = 0;
+        Twist();
+      }
+    }
+    return MtStream::temper(v);
+  }
+  void Twist() {  // the next block, in place (standard MT19937 recurrence)
+    for (int i = 0; i < kMtN; ++i) {
+      const uint32_t y = (s[i] & 0x80000000u) | (s[(i + 1) % kMtN] & 0x7fffffffu);
+      s[i] = s[(i + kMtM) % kMtN] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
   }
 };
 

@@ -94,7 +94,7 @@ def py_dirichlet(seed, count, alpha):
 
 
 @pytest.mark.parametrize("alpha", [0.03, 0.3, 1.0, 2.5])
-@pytest.mark.parametrize("count", [1, 7, 82, 121])
+@pytest.mark.parametrize("count", [1, 7, 82, 121, 362])  # 362: past the first 624 words
 def test_noise_matches_libstdcxx_restatement(alpha, count):
   for seed in (0, 1, 42, 12345):
     want, words = py_dirichlet(seed, count, alpha)
