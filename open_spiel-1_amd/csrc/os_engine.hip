@@ -7,8 +7,6 @@
 // the per-game kernels through the launcher table (os_kernels.h,
 // os_game_*.hip), fetches results and reports errors.
 #include <algorithm>
-#include <chrono>
-#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -473,19 +471,6 @@ struct Stager {
 };
 
 // Uploads roots / seeds, sizes and allocates the arena and outputs.
-// OS_AMD_HOST_TIMING=1: host phases of Prepare / os_az_prepare on stderr (diagnostic).
-struct HostPhases {
-  bool on = std::getenv("OS_AMD_HOST_TIMING") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  void mark(const char* what) {
-    if (!on) return;
-    const auto n = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "HOSTPHASE %-12s %8.3f ms\n", what,
-                 std::chrono::duration<double, std::milli>(n - t).count());
-    t = n;
-  }
-};
-
 int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
             const int64_t* root_actions, const int64_t* root_offsets,
             const uint32_t* bot_seeds, const uint32_t* eval_seeds, bool search = true) {
@@ -505,9 +490,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   e->node_bytes = static_cast<int>(
       e->node_wide ? (e->node_double ? sizeof(Node<double, true>) : sizeof(Node<int32_t, true>))
                    : (e->node_double ? sizeof(Node<double>) : sizeof(Node<int32_t>)));
-  HostPhases hp;
   if ((rc = SizeArena(e, true))) return rc;
-  hp.mark("p:size");
 
   // Root states (+ go hash sets) on the host.
   const int sb = e->game.state_bytes;
@@ -520,19 +503,13 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     rh.assign(static_cast<size_t>(std::max<int64_t>(R, 1)) * e->hash_stride, 0);
     rnh.assign(std::max<int64_t>(R, 1), 0);
   }
-  if (e->want_nlegal) e->root_nlegal.assign(static_cast<size_t>(std::max<int64_t>(R, 1)), 0);
   rc = ParallelChunks(R, 1024, [&](int64_t lo, int64_t hi) {
-    std::vector<int64_t> legal;
     for (int64_t r = lo; r < hi; ++r) {
       HostState hs;
       std::string err;
       if (!ReplayRoot(e->game, root_actions + root_offsets[r],
                       root_offsets[r + 1] - root_offsets[r], &hs, &err))
         return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
-      if (e->want_nlegal) {
-        StateLegal(hs, &legal);
-        e->root_nlegal[r] = static_cast<int32_t>(legal.size());
-      }
       if (StateTerminal(hs))
         return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
       if (StateIsChance(hs))  // a bot is only asked to move at decision nodes
@@ -548,7 +525,6 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
     return 0;
   });
   if (rc) return rc;
-  hp.mark("p:replay");
   const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
   if ((rc = e->d_roots.ensure(Rz * sb))) return rc;
   if ((rc = e->d_bseed.ensure(Rz * 4)) || (rc = e->d_eseed.ensure(Rz * 4))) return rc;
@@ -910,13 +886,9 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   q.n_rollouts = 2;  // f64 node rewards (Node<double>): values are not integral
   q.child_selection = OS_SELECT_UCT;  // `puct` selects; the LUT stays log(N)
   q.layout = OS_LAYOUT_LANE;
-  HostPhases hp;
-  e->want_nlegal = alpha > 0.0;  // the noise loop below needs |LegalActions()| per root
   int rc = Prepare(e, &q, R, root_actions, root_offsets, bot_seeds, bot_seeds,
                    /*search=*/false);  // buffers only: k_az_step runs the search
-  e->want_nlegal = false;
   if (rc) return rc;
-  hp.mark("prepare");
   if (e->chunk_roots < R)
     return Fail(OS_ERR_CAPACITY, "external-evaluator searches must all fit in HBM at once");
   const GameLaunchers* L = LaunchersFor(e->game.cfg);
@@ -932,7 +904,6 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   e->az_fused = e->az_requests == OS_AZ_REQUESTS_FUSED;
   if (e->az_fused && (rc = e->d_az_raw.ensure(Rz * static_cast<size_t>(e->cap) * 8))) return rc;
   HIP_TRY(hipMemset(e->d_az_slots.p, 0, Rz * slot_bytes));  // stage kAzStart
-  hp.mark("slots");
   e->az_noise = alpha > 0.0;
   e->az_eps = eps;
   if (e->az_noise) {
@@ -947,24 +918,29 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     std::vector<double> noise(Rz * mc, 0.0);
     std::vector<int32_t> skip(Rz, 0);
     rc = ParallelChunks(R, 512, [&](int64_t lo, int64_t hi) {
+      std::vector<int64_t> acts;
       for (int64_t r = lo; r < hi; ++r) {
-        const int nl = e->root_nlegal[r];  // recorded by Prepare's replay
+        HostState hs;
+        std::string err;
+        ReplayRoot(e->game, root_actions + root_offsets[r],
+                   root_offsets[r + 1] - root_offsets[r], &hs, &err);
+        StateLegal(hs, &acts);
         const int64_t w =
-            import ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r], nl, alpha,
+            import ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r],
+                                         static_cast<int>(acts.size()), alpha,
                                          noise.data() + r * mc)
-                   : DirichletNoise(bot_seeds[r], nl, alpha, noise.data() + r * mc);
+                   : DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
+                                    noise.data() + r * mc);
         if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
         skip[r] = static_cast<int32_t>(w);
       }
       return 0;
     });
     if (rc) return rc;
-    hp.mark("noise");
     if ((rc = e->d_az_noise.ensure(noise.size() * 8)) || (rc = e->d_az_skip.ensure(Rz * 4)))
       return rc;
     HIP_TRY(hipMemcpy(e->d_az_noise.p, noise.data(), noise.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->d_az_skip.p, skip.data(), Rz * 4, hipMemcpyHostToDevice));
-    hp.mark("noise-up");
   }
   e->az_import = import;
   if (import && R > 0) {  // keys into the bot rng rows, positions in / out
@@ -1001,7 +977,6 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     if ((rc = e->d_az_shards.ensure(sb))) return rc;
     HIP_TRY(hipMemset(e->d_az_shards.p, 0, sb));
   }
-  hp.mark("tail");
   e->az_ready = true;
   return OS_OK;
 }

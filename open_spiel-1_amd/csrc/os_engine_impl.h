@@ -321,10 +321,6 @@ struct os_engine {
   std::vector<uint32_t> sp_actor_seeds;
   // prepared external-evaluator batch (os_az_*): caller-owned device buffers
   bool az_ready = false;
-  // Set by os_az_prepare around Prepare: the replay also records each root's
-  // |LegalActions()| (the Dirichlet draw's size) in root_nlegal.
-  bool want_nlegal = false;
-  std::vector<int32_t> root_nlegal;
   int32_t az_puct = 0;
   int32_t* az_kind = nullptr;
   float* az_obs = nullptr;
