@@ -505,13 +505,16 @@ struct WaveUniformCtx<C, std::void_t<decltype(C::kWaveUniform)>> : std::true_typ
 #ifndef OS_GO_LOG_BLOOM
 #define OS_GO_LOG_BLOOM 1
 #endif
-template <class H>
+// L: link word.  uint32_t keeps the stone count for rewind (the searches);
+// a rollout-only context (k_rollouts, never rewound) stores the uint16_t
+// link alone: 2 B less HBM write per logged move.
+template <class H, class L = uint32_t>
 struct GoCtxT {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
   const uint64_t* base;    // hashes of positions before this search's root
   int32_t n_base;
   uint64_t* log;           // hashes added since the root (capacity cap)
-  uint32_t* link;          // [cap] stone count << 16 | previous same-count entry + 1
+  L* link;                 // [cap] (stone count << 16 |) previous same-count entry + 1
   H* head;                 // [n_heads] last entry + 1 with k stones (cap <= max of H)
   int32_t stride;          // SoA stride of log / link (1: contiguous)
   int32_t head_stride;     // stride of head (k_rollouts: LDS, 64 lanes)
@@ -590,6 +593,7 @@ struct GoCtxT {
   // reverse order of insertion.
   OS_HD int mark() const { return n_log; }
   OS_HD void rewind(int m) {
+    static_assert(sizeof(L) == 4, "rewind needs the stone count in the link");
     while (n_log > m) {
       --n_log;
       const uint32_t lk = link[static_cast<int64_t>(n_log) * stride];
@@ -609,7 +613,10 @@ struct GoCtxT {
       const int64_t e = static_cast<int64_t>(n_log) * stride;
       const int hk = stones * head_stride;
       log[e] = h;
-      link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
+      if constexpr (sizeof(L) == 4)
+        link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
+      else
+        link[e] = static_cast<L>(head[hk]);
       head[hk] = static_cast<H>(n_log + 1);
       if (bloom) bloom_add(h);
       ++n_log;

@@ -1653,26 +1653,27 @@ struct RollCtx<Go> {
 #else
 template <>
 struct RollCtx<Go> {
-  using type = GoCtx;
+  using type = GoCtxT<uint8_t, uint16_t>;  // never rewound: 16-bit links
   // heads (cells + 1 bytes per lane), then the log's Bloom filter
   // (OS_GO_LOG_BLOOM): launched with RollLdsBytes of dynamic LDS.
   static constexpr int kLdsWords = (kGoHeads * 64 + 3) / 4 + GoCtx::kBloomWords * 64;
   // The bucket heads are the only per-move accesses that differ across the
   // lanes (each lane is at its own stone count): they live in LDS, lane-
   // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
-  __device__ static GoCtx make(const RollArgs& a, int64_t i, uint32_t* lds) {
+  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds) {
     uint8_t* lds_heads = reinterpret_cast<uint8_t*>(lds);
-    GoCtx c;
+    uint16_t* glink = reinterpret_cast<uint16_t*>(a.glink);
+    type c;
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
 #if OS_ROLL_AOS & 2
     c.log = a.glog + i * kGoLogCap;
-    c.link = a.glink + i * kGoLogCap;
+    c.link = glink + i * kGoLogCap;
     c.stride = 1;
 #else
     c.log = a.glog + i;
-    c.link = a.glink + i;
+    c.link = glink + i;
     c.stride = static_cast<int32_t>(a.n);
 #endif
     c.head = lds_heads + (threadIdx.x & 63);
