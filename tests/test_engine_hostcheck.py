@@ -134,6 +134,7 @@ def test_go_playouts_match_oracle_many_seeds(gs):
     # k_rollouts' Bloom-screened superko set gives the same playouts
     assert np.array_equal(H.rollouts_go_bloom(gs, acts, seeds), ref)
     assert np.array_equal(H.rollouts_go_logbloom(gs, acts, seeds), ref)
+    assert np.array_equal(H.rollouts_go_link16(gs, acts, seeds), ref)
 
 
 @pytest.mark.parametrize("gs", ["go(board_size=9)", "go(board_size=7,komi=4.5)",
