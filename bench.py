@@ -92,6 +92,9 @@ def parse():
                   help="c2: skip the bit-exact sweep over the other kernels (C3/C4/C5 "
                        "shapes, go lane layout, PUCT, numpy policy, chance nodes), run "
                        "after the timed region")
+  ap.add_argument("--no-configs", dest="configs", action="store_false",
+                  help="c2: skip the timed full-size C3 / C4 / C5 / g9 entries run after "
+                       "the headline line (the `configs` sub-object)")
   ap.add_argument("--az-graph", type=int, default=1,
                   help="az: replay each evaluator round as one captured HIP graph (1) "
                        "or launch it op by op (0)")
@@ -345,7 +348,8 @@ def bench_search(args, ctx, layout):
     og = _oracle(game)
     pr = min(args.parity_roots, R)
     ref = og.mcts_batch(acts[:offs[pr]], offs[:pr + 1], bot_seeds[:pr], eval_seeds[:pr],
-                        uct_c=2.0, max_simulations=sims, max_children=eng.max_children)
+                        uct_c=2.0, max_simulations=sims, max_children=eng.max_children,
+                        threads=host_cores()[0])
     bad = [k for k in E.OUTPUT_KEYS if not np.array_equal(out[k][:pr], ref[k])]
     parity = {"roots_checked": pr, "bit_exact": not bad, "mismatch_fields": bad}
 
@@ -362,6 +366,9 @@ def bench_search(args, ctx, layout):
   sweep = None
   if (ctx.rank == 0 and args.config == "c2" and args.parity_sweep and not ctx.rehearse):
     sweep = parity_sweep(ctx)
+  subs = None
+  if args.config == "c2" and args.configs and not ctx.rehearse and ctx.world == 1:
+    subs = timed_configs(args, ctx, layout)
 
   cpu = None
   if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
@@ -387,6 +394,8 @@ def bench_search(args, ctx, layout):
   line["parity"] = parity
   if sweep is not None:
     line["parity_sweep"] = sweep
+  if subs is not None:
+    line["configs"] = subs
   line["tree_stats"] = stats
   line["arena"] = dict(arena, mode=arena_mode)
   return line
@@ -442,11 +451,12 @@ def bench_root_parallel(args, ctx, layout):
   parity = None
   if ctx.rank == 0 and args.parity_roots > 0:
     og = _oracle(game)
-    pr = min(args.parity_roots, 4, T)
+    pr = min(args.parity_roots, 8, T)
     acts = np.zeros(0, np.int64)
     offs = np.zeros(pr + 1, np.int64)
     ref = og.mcts_batch(acts, offs, ids[:pr], ids[:pr] + np.uint32(EVAL_OFFSET),
-                        uct_c=2.0, max_simulations=sims, max_children=be.eng.max_children)
+                        uct_c=2.0, max_simulations=sims, max_children=be.eng.max_children,
+                        threads=host_cores()[0])
     bad = [k for k in ("child_action", "child_n", "child_w", "root_n", "best_action")
            if not np.array_equal(out[k][:pr], ref[k])]
     parity = {"trees_checked": pr, "bit_exact": not bad, "mismatch_fields": bad,
@@ -758,6 +768,57 @@ def bench_az(args, ctx, layout):
   line["parity"] = parity
   line["tree_stats"] = st
   return line
+
+
+# ---------------------------------------------------------------------------
+# the other BASELINE configs, timed at full size after the headline line
+# name: (timed steps, warmup steps).  C3 is ~1 s per step, g9 ~0.45 s.
+SUB_CONFIGS = {"c3": (2, 1), "c4": (5, 1), "c5": (10, 2), "g9": (3, 1)}
+SUB_CPU_SECONDS = 3.0
+
+
+def timed_configs(args, ctx, layout):
+  """C3, C4 (this GPU's share), C5 and g9 at their full BASELINE sizes, each
+  timed exactly as its own `--config` run would be (barrier + sync around K
+  steps), with its roofline, a >= 3 s CPU baseline and a bit-exact oracle
+  prefix at the config's full depth (C3: 32 roots x 2048 sims; C4: 8 trees x
+  2048 sims plus the device root sums against every tree; C5: 4096 seeds;
+  g9: 32 roots x 256 sims).  Single-GPU only: at N > 1 the driver's per-N
+  lines are the C2 headline."""
+  import gc
+  out = {}
+  t_all = time.perf_counter()
+  for name, (steps, warmup) in SUB_CONFIGS.items():
+    sub = argparse.Namespace(**vars(args))
+    sub.config, sub.steps, sub.warmup = name, steps, warmup
+    sub.cpu_seconds, sub.parity_roots = SUB_CPU_SECONDS, 32
+    sub.roots = sub.sims = sub.arena_nodes = sub.block = 0
+    sub.arena = "auto"
+    mode = CONFIGS[name][0]
+    fn = {"search": bench_search, "root_parallel": bench_root_parallel,
+          "playouts": bench_playouts}[mode]
+    t0 = time.perf_counter()
+    try:
+      line = fn(sub, ctx, layout)
+    except Exception as e:  # reported in the line, never hidden
+      line = {"error": "%s: %s" % (type(e).__name__, e)}
+    gc.collect()  # the config's engine (and its arena) goes before the next one
+    line["seconds_total"] = round(time.perf_counter() - t0, 2)
+    for k in ("tree_stats", "n_gpus", "higher_is_better", "data"):
+      line.pop(k, None)
+    out[name] = line
+  out["all_bit_exact"] = all(_entry_exact(v) for v in out.values() if isinstance(v, dict))
+  out["seconds"] = round(time.perf_counter() - t_all, 2)
+  return out
+
+
+def _entry_exact(line):
+  p = line.get("parity")
+  if not p:
+    return False
+  flags = [p.get("bit_exact"), p.get("timed_run_bit_exact", True),
+           p.get("allreduce_equals_sum_of_trees", True), p.get("counts_equal_returns", True)]
+  return all(bool(f) for f in flags)
 
 
 # ---------------------------------------------------------------------------

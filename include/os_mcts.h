@@ -268,6 +268,9 @@ int os_az_set_requests(os_engine* e, int32_t mode);
  * mcts.cc:402-424) or OS_LAYOUT_AUTO (default: wave unless the node budget can
  * be reached).  Same results either way. */
 int os_az_set_layout(os_engine* e, int32_t layout);
+/* The kernel the last os_az_prepare* chose (OS_LAYOUT_WAVE or OS_LAYOUT_LANE),
+ * AUTO resolved by the engine's own rule. */
+int os_az_get_layout(os_engine* e, int32_t* layout);
 /* The Dirichlet noise os_az_prepare draws for one fresh MCTSBot(seed) at a
  * root with `count` legal actions: out[count] (normalised, legal-action
  * order); returns the MT19937 words consumed (< 0 on error).  Exposed so the
@@ -284,7 +287,11 @@ int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32
  * network's heads (alpha_zero/model.py:278-282, 304): illegal logits
  * (legal[r * num_actions + a] == 0) become -1e32, prior[r][a] = their softmax,
  * value[r] = tanh(value logit); f64 arithmetic, written straight into the
- * engine's response buffers (dev_prior / dev_value of os_az_prepare). */
+ * engine's response buffers (dev_prior / dev_value of os_az_prepare).  The
+ * reference model evaluates its heads in float32 (TensorFlow softmax / tanh),
+ * so these priors agree with a float32 softmax to float32 rounding, not
+ * bitwise; search parity is defined on the responses the engine receives,
+ * whatever produced them. */
 int os_az_heads_async(const void* logits, int32_t dtype, int64_t num_rows, int32_t num_actions,
                       int64_t ld, const uint8_t* legal, double* prior, double* value,
                       void* hip_stream);

@@ -438,12 +438,22 @@ int UploadZob(os_engine* e) {
 }
 
 // Batched small copies through the engine's pinned staging buffer: queued on
-// the null stream, then one wait.
+// the null stream, then one wait.  Only batches of up to kStageMax bytes are
+// staged (a single bot's step moves a few hundred bytes, where the copies'
+// fixed costs dominate); larger ones copy directly with synchronous
+// hipMemcpy, pageable memory on the host side, so the pinned buffer stays
+// small and a big prepare never depends on a large hipHostMalloc.
+constexpr size_t kStageMax = size_t(1) << 20;
+
 struct Stager {
   os_engine* e;
   size_t off = 0;
+  bool direct = false;                        // batch above kStageMax
+  std::vector<std::vector<unsigned char>> dn;  // direct mode: download targets
   explicit Stager(os_engine* eng) : e(eng) {}
   int reserve(size_t bytes) {
+    direct = bytes > kStageMax;
+    if (direct) return OS_OK;
     // The staging buffer is only reused after the previous batch was waited for.
     return e->h_stage.ensure(std::max<size_t>(bytes, 64 << 10));
   }
@@ -454,12 +464,22 @@ struct Stager {
   }
   int up(void* dst, const void* src, size_t bytes) {
     if (!bytes) return OS_OK;
+    if (direct) {
+      HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+      return OS_OK;
+    }
     unsigned char* q = slot(bytes);
     std::memcpy(q, src, bytes);
     HIP_TRY(hipMemcpyAsync(dst, q, bytes, hipMemcpyHostToDevice, nullptr));
     return OS_OK;
   }
   int down(unsigned char** q, const void* src, size_t bytes) {
+    if (direct) {
+      dn.emplace_back(std::max<size_t>(bytes, 1));
+      *q = dn.back().data();
+      if (bytes) HIP_TRY(hipMemcpy(*q, src, bytes, hipMemcpyDeviceToHost));
+      return OS_OK;
+    }
     *q = slot(bytes);
     if (bytes) HIP_TRY(hipMemcpyAsync(*q, src, bytes, hipMemcpyDeviceToHost, nullptr));
     return OS_OK;
@@ -1339,7 +1359,11 @@ int os_mcts_stateful(os_engine* e, const os_mcts_params* p,
       return rc;
     // No wait: the null stream runs these copies before the search kernel.
   }
-  if ((rc = Run(e, nullptr))) return rc;
+  if ((rc = Run(e, nullptr))) {
+    (void)hipStreamSynchronize(nullptr);  // the queued copies still read h_stage
+    e->import_state = false;
+    return rc;
+  }
   rc = Fetch(e, max_children, child_action, child_n, child_w, child_out, nchild, root_n,
              root_w, root_out, best_action, nodes);
   e->import_state = false;
@@ -1512,6 +1536,13 @@ int os_az_set_layout(os_engine* e, int32_t layout) {
   if (layout != OS_LAYOUT_WAVE && layout != OS_LAYOUT_LANE && layout != OS_LAYOUT_AUTO)
     return Fail(OS_ERR_INVALID, "unknown layout");
   e->az_layout = layout;
+  return OS_OK;
+}
+
+int os_az_get_layout(os_engine* e, int32_t* layout) {
+  if (!e || !layout) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->az_ready) return Fail(OS_ERR_INVALID, "no os_az_prepare batch");
+  *layout = e->az_wave ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
   return OS_OK;
 }
 

@@ -268,7 +268,11 @@ struct PinBuf {
   size_t used = 0;
   int ensure(size_t b) {
     if (b <= bytes && p) return 0;
-    if (p) (void)hipHostFree(p);
+    // Copies queued from the old buffer (a failed call's) finish first.
+    if (p) {
+      (void)hipStreamSynchronize(nullptr);
+      (void)hipHostFree(p);
+    }
     p = nullptr;
     bytes = 0;
     hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), b);

@@ -59,6 +59,13 @@ def heads_into(logits, legal, prior, value):
     raise ValueError("logits must be [N, A + 1] with unit column stride")
   if legal.dtype != torch.uint8 or prior.dtype != torch.float64 or value.dtype != torch.float64:
     raise ValueError("legal uint8, prior / value float64 expected")
+  # the kernel indexes legal / prior as contiguous [N, A] rows and value as [N]
+  if tuple(legal.shape) != (n, a) or tuple(value.shape) != (n,):
+    raise ValueError("legal must be [N, A] and value [N] like prior")
+  if not (legal.is_contiguous() and prior.is_contiguous() and value.is_contiguous()):
+    raise ValueError("legal, prior and value must be contiguous")
+  if not (logits.device == legal.device == prior.device == value.device) or not logits.is_cuda:
+    raise ValueError("logits, legal, prior and value must be on the same GPU")
   st = torch.cuda.current_stream(prior.device)
   check(lib.os_az_heads_async(logits.data_ptr(), 0 if logits.dtype == torch.float32 else 1, n, a,
                               logits.stride(0), legal.data_ptr(), prior.data_ptr(),
@@ -141,10 +148,6 @@ class ExternalEvaluatorSearch:
     if layout not in _LAYOUTS:
       raise ValueError("layout must be 'auto', 'wave' or 'lane'")
     check(lib.os_az_set_layout(self.eng._h, _LAYOUTS[layout]))
-    # the engine's choice for AUTO: wave unless GC can fire (os_az_set_layout)
-    max_nodes = (int(max_memory_mb) << 20) // 80 + 1
-    gc_possible = max_nodes > 1 and 1 + max_simulations * self.eng.max_children >= max_nodes
-    self._layout_wave = layout == "wave" or (layout == "auto" and not gc_possible)
     if bot_rng is None:
       bs = _lib.u32(bot_seeds)
       check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
@@ -160,6 +163,10 @@ class ExternalEvaluatorSearch:
           ptr(pos), float(dirichlet_alpha), float(dirichlet_epsilon), kind.data_ptr(),
           obs.data_ptr(), legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
           pending.data_ptr()))
+    # the kernel the engine chose (AUTO: wave unless GC can fire)
+    lay = np.zeros(1, np.int32)
+    check(lib.os_az_get_layout(self.eng._h, ptr(lay)))
+    self._layout_wave = int(lay[0]) == _lib.LAYOUT_WAVE
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     self.steps = 0
     self.requests = 0

@@ -107,19 +107,40 @@ def root_parallel(backend, history, trees_per_rank, group=None, **params):
 
 
 def _all_reduce_root_sums(visits, rewards, group):
-  """ONE all-reduce of the concatenated f64[2A] (visits, rewards) message.
+  """The root sums of every rank, added in RANK ORDER on every rank.
 
-  The exchange is ~2 KB and latency-bound on xGMI, so one collective per step
-  instead of two halves the step's fixed cost.  Visit counts travel as f64 and
-  come back exact (every partial sum is an integer below 2^53: 8 ranks x 8192
-  trees x 2048 sims ~ 1.3e8); rewards are the f64 sums they were before.
+  Each rank sends its concatenated f64[2A] (visits, rewards) message through
+  ONE all_gather (~2 KB per rank: latency-bound on xGMI, so one collective per
+  step), then every rank adds the W parts left to right: rank 0's sums, plus
+  rank 1's, ...  The result is therefore fixed by the data alone, not by the
+  collective library's ring or tree order: with f64 rewards that are not
+  integers (n_rollouts > 1, pig's -1/(n-1)) an all-reduce's association
+  order changes the last bits, and this order does not.  Within a rank,
+  k_root_reduce sums each action over the rank's trees in ascending tree
+  order.  Visit counts travel as f64 and come back exact
+  (every partial sum is an integer below 2^53: 8 ranks x 8192 trees x 2048
+  sims ~ 1.3e8).
   """
   import torch
   import torch.distributed as dist
   A = visits.numel()
   msg = torch.cat((visits.to(torch.float64), rewards))
-  dist.all_reduce(msg, group=group)
-  return msg[:A].to(torch.int64), msg[A:]
+  world = dist.get_world_size(group)
+  parts = [torch.empty_like(msg) for _ in range(world)]
+  dist.all_gather(parts, msg, group=group)
+  acc = parts[0].clone()
+  for p in parts[1:]:
+    acc += p
+  return acc[:A].to(torch.int64), acc[A:]
+
+
+def fixed_order_sum(per_rank):
+  """The reduction _all_reduce_root_sums performs, on host arrays: rank 0's
+  f64 sums, plus rank 1's, ... (the order tests hold the oracle to)."""
+  acc = np.array(per_rank[0], np.float64, copy=True)
+  for p in per_rank[1:]:
+    acc += np.asarray(p, np.float64)
+  return acc
 
 
 def sharded_playouts(backend, history, total, group=None, n_rollouts=1):

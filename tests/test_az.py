@@ -397,6 +397,34 @@ def test_gpu_heads_kernel_matches_torch(require_gpu, dtype):
   some = legal.any(1, keepdim=True)
   assert torch.all(prior[(legal == 0) & some] == 0)  # exp(-1e32 - max) underflows to 0
   np.testing.assert_allclose(prior[3].cpu().numpy(), np.full(A, 1.0 / A), rtol=1e-15)
+  # The reference model's heads run in float32 (alpha_zero/model.py:278-282,
+  # 304): the f64 kernel agrees with a float32 softmax / tanh to float32
+  # rounding (a few ulp of f32), not bitwise.
+  f32_p = torch.softmax(logits.float()[:, :A].masked_fill(legal == 0, -1e32), dim=-1)
+  f32_v = torch.tanh(logits.float()[:, A])
+  torch.testing.assert_close(prior, f32_p.double(), rtol=4e-6, atol=1e-7)
+  torch.testing.assert_close(value, f32_v.double(), rtol=4e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_gpu_heads_into_rejects_bad_tensors(require_gpu):
+  """heads_into checks what the kernel assumes: [N, A] contiguous legal /
+  prior, [N] value, all on the logits' GPU."""
+  import torch
+  from os_amd.az import heads_into
+  N, A = 8, 7
+  logits = torch.zeros(N, A + 1, device="cuda")
+  legal = torch.ones(N, A, dtype=torch.uint8, device="cuda")
+  prior = torch.zeros(N, A, dtype=torch.float64, device="cuda")
+  value = torch.zeros(N, dtype=torch.float64, device="cuda")
+  heads_into(logits, legal, prior, value)
+  bad = [(logits, legal[:, :A - 1], prior, value),
+         (logits, legal, prior, value[:N - 1]),
+         (logits, legal, torch.zeros(A, N, dtype=torch.float64, device="cuda").t(), value),
+         (logits, legal.cpu(), prior, value)]
+  for args in bad:
+    with pytest.raises(ValueError):
+      heads_into(*args)
 
 
 def test_heads_abi_rejects_bad_shapes():

@@ -177,6 +177,80 @@ def _check_world2(hip):
       np.testing.assert_array_equal(g[k], ref[k], err_msg=k)
 
 
+# ---------------------------------------------------------------------------
+# The cross-rank reward sum in a fixed order: with
+# non-integer f64 rewards (n_rollouts = 3 averages; pig with 4 players credits
+# -1/3) the association order of the sum changes its last bits, so the ranks
+# add their parts in rank order (dist._all_reduce_root_sums), not in whatever
+# order the collective library reduces.  World 3: with two ranks every order
+# gives s0 + s1, so it takes three to tell orders apart.
+WORLD3_CASES = (("hex(board_size=5)", [12], dict(max_simulations=SIMS, n_rollouts=3)),
+                ("pig(players=4,horizon=8,winscore=6)", [],
+                 dict(max_simulations=40)))
+
+
+def _worker_fixed_order(rank, world, port, q):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  try:
+    out = []
+    for gs, hist, kw in WORLD3_CASES:
+      v, w = D.root_parallel(HostBackend(gs), hist, trees_per_rank=4, **kw)
+      out.append((v.numpy(), w.numpy()))
+    q.put((rank, out))
+  finally:
+    dist.destroy_process_group()
+
+
+def _oracle_rank_sums(gs, hist, world, T, kw):
+  og = oracle_lib.Game(gs)
+  parts_v, parts_w = [], []
+  for g in range(world):
+    ids = np.arange(g * T, (g + 1) * T, dtype=np.uint32)
+    acts = np.tile(np.asarray(hist, np.int64), T)
+    offs = np.arange(T + 1, dtype=np.int64) * len(hist)
+    o = og.mcts_batch(acts, offs, ids, ids + np.uint32(D.EVAL_SEED_OFFSET), **kw)
+    v, w = _action_sums(o, og.num_distinct_actions)
+    parts_v.append(v.numpy())
+    parts_w.append(w.numpy())
+  return parts_v, parts_w
+
+
+def test_gloo_world3_reward_sum_in_rank_order():
+  world, port = 3, _free_port()
+  ctx = mp.get_context("spawn")
+  q = ctx.Queue()
+  procs = [ctx.Process(target=_worker_fixed_order, args=(r, world, port, q))
+           for r in range(world)]
+  for p in procs:
+    p.start()
+  res = [q.get(timeout=300) for _ in range(world)]
+  for p in procs:
+    p.join(60)
+    assert p.exitcode == 0
+  inexact = 0
+  for i, (gs, hist, kw) in enumerate(WORLD3_CASES):
+    pv, pw = _oracle_rank_sums(gs, hist, world, 4, kw)
+    want_w = D.fixed_order_sum(pw)
+    want_v = np.sum(pv, axis=0)
+    # the other association, s0 + (s1 + s2): differs where the order matters
+    other = pw[0] + (pw[1] + pw[2])
+    inexact += int((other != want_w).sum())
+    for _, out in res:
+      v, w = out[i]
+      np.testing.assert_array_equal(v, want_v)
+      assert w.tobytes() == want_w.tobytes(), gs
+  assert inexact > 0  # the cases do exercise a non-associative sum
+
+
+def test_fixed_order_sum_is_left_to_right():
+  a = np.array([0.1, 1e16]), np.array([0.2, 1.0]), np.array([0.3, -1e16])
+  got = D.fixed_order_sum(a)
+  assert got.tobytes() == ((a[0] + a[1]) + a[2]).tobytes()
+  assert got[1] == 0.0  # (1e16 + 1) - 1e16 in f64
+
+
 @pytest.mark.gpu
 def test_gpu_root_parallel_world1(require_gpu):
   be = D.HipBackend(HEX5)

@@ -86,3 +86,25 @@ def test_full_c5_million_go_playouts(torch_dev):
   assert np.array_equal(ret[pick], ref)
   stats = be.eng.rollouts_stats()
   assert stats["moves"] > 100 * N             # random go9 games run > 100 plies
+
+
+def test_c3_prefix_full_depth(torch_dev):
+  """C3: breakthrough 8x8 roots from the config's own generator
+  (seed 1000 + i, k ~ U[0,6] plies) at the full 2048 simulations; the first
+  and last 32 of the 65536 roots, bit-exact against the oracle
+  (mcts.cc:325-428)."""
+  from os_amd import engine as E
+  gs, R, sims = "breakthrough(rows=8,columns=8)", 65536, 2048
+  acts, offs = E.make_roots(gs, R, seed_base=1000, max_plies=6)
+  rows = np.r_[0:32, R - 32:R]
+  hist = [acts[offs[r]:offs[r + 1]] for r in rows]
+  sa, so = E.roots_from_histories(hist)
+  bs = rows.astype(np.uint32)
+  es = bs + np.uint32(1 << 20)
+  eng = E.Engine(gs, device=0)
+  kw = dict(uct_c=2.0, max_simulations=sims)
+  got = eng.mcts_batch(sa, so, bs, es, **kw)
+  ref = O.Game(gs).mcts_batch(sa, so, bs, es, max_children=eng.max_children, threads=8, **kw)
+  for k in E.OUTPUT_KEYS:
+    assert np.array_equal(got[k], ref[k]), k
+  assert (got["root_n"] > 1).all()
