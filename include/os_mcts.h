@@ -271,6 +271,20 @@ int os_az_set_layout(os_engine* e, int32_t layout);
 /* The kernel the last os_az_prepare* chose (OS_LAYOUT_WAVE or OS_LAYOUT_LANE),
  * AUTO resolved by the engine's own rule. */
 int os_az_get_layout(os_engine* e, int32_t* layout);
+/* Root Dirichlet noise drawn by the CALLER, for the batch of the last
+ * os_az_prepare*: noise[r * stride + j] pairs with root r's j-th legal action
+ * (ascending), mixed at the root's expansion as (1 - eps) * prior + eps *
+ * noise (mcts.py:314-317, mcts.cc:265-273) without consuming bot words.  For
+ * OS_POLICY_NUMPY batches, whose noise is RandomState.dirichlet on the
+ * caller's own RandomState (mcts.py:315): the caller draws it where the
+ * reference does -- first on the stream, since an external evaluator draws
+ * nothing before the root's expansion -- and passes the stream after the draw
+ * to os_az_prepare_stateful.  noise == NULL removes the noise. */
+int os_az_set_noise(os_engine* e, const double* noise, int64_t stride, double eps);
+/* Priors of search r's tree nodes in os_engine_tree's node order (the root's
+ * is 1; children's are the evaluator's, mixed with the root noise); count =
+ * the node count os_engine_tree reports.  After os_az_fetch. */
+int os_az_tree_priors(os_engine* e, int64_t r, int64_t count, double* prior);
 /* The Dirichlet noise os_az_prepare draws for one fresh MCTSBot(seed) at a
  * root with `count` legal actions: out[count] (normalised, legal-action
  * order); returns the MT19937 words consumed (< 0 on error).  Exposed so the

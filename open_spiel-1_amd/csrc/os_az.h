@@ -139,12 +139,16 @@ OS_HD void az_request(const GameCfg& g, const typename G::State& s, int kind, co
 // history context with its root fields set (go: Zobrist table, the positions
 // before the root, n_heads); its log is bound to the continuation here.
 // `raw` ([cap], or nullptr for separate Prior / Evaluate requests): the parked
-// priors of fused requests (see above).
+// priors of fused requests (see above).  `np_policy`: the search of
+// python/algorithms/mcts.py (mcts.py:292-333, 395-443) -- the expansion's
+// shuffle is RandomState.shuffle on the bot's stream, and the search stops
+// early only on a solved root (no single-child stop; the caller disables GC).
 template <class G>
 OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
                    const typename G::State& root, AzSlot<G>& sl, Node<double>* nodes,
                    double* prior, double* raw, uint32_t cap, MtStream& bot, const AzIo& io,
-                   int obs_size, int num_actions, typename G::Ctx& ctx, const AzNoise& nz) {
+                   int obs_size, int num_actions, typename G::Ctx& ctx, const AzNoise& nz,
+                   bool np_policy = false) {
   az_bind_log(ctx, sl.glog, sl.stage != kAzStart);
   const int P0 = G::to_move(root);
   const double inf = __builtin_huge_val();
@@ -220,7 +224,8 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
         for (int i = 0; i < nz.skip; ++i) bot.next();
       uint8_t perm[kMaxChildren];
       for (int k = 0; k < nc; ++k) perm[k] = static_cast<uint8_t>(k);
-      CppShuffle(perm, nc, bot);
+      if (np_policy) NpShuffle(perm, nc, bot);  // mcts.py:320
+      else CppShuffle(perm, nc, bot);
       const uint32_t first = from_raw ? nodes[x].first : sl.used;
       for (int k = 0; k < nc; ++k) {
         const int j = perm[k];
@@ -351,7 +356,8 @@ OS_HD void az_step(const GameCfg& g, const SearchParams& sp, int puct,
       }
       sl.sim += 1;
       sl.res.sims = sl.sim;
-      if (nodes[0].out != kUnsolved || nodes[0].nchild == 1) break;  // mcts.cc:398-401
+      if (nodes[0].out != kUnsolved) break;  // mcts.cc:398-401, mcts.py:440-441
+      if (!np_policy && nodes[0].nchild == 1) break;
       if (sp.max_nodes > 1 && sl.nodes_count >= sp.max_nodes) {      // mcts.cc:402-424
         const int st = garbage_collect(nodes, sl.used, cap, sl.gc_limit, &sl.nodes_count);
         if (st != kOk) {

@@ -898,11 +898,18 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   }
   if (!(alpha >= 0.0) || !(eps >= 0.0) || eps > 1.0)
     return Fail(OS_ERR_INVALID, "dirichlet_alpha must be >= 0 and epsilon in [0, 1]");
-  if (p->policy != OS_POLICY_CPP)
-    return Fail(OS_ERR_UNSUPPORTED, "external-evaluator search implements the C++ MCTSBot");
+  if (p->policy != OS_POLICY_CPP && p->policy != OS_POLICY_NUMPY)
+    return Fail(OS_ERR_INVALID, "unknown policy");
+  const bool np = p->policy == OS_POLICY_NUMPY;
+  if (np && alpha > 0.0)
+    return Fail(OS_ERR_INVALID,
+                "OS_POLICY_NUMPY: draw RandomState.dirichlet on the host and pass it with "
+                "os_az_set_noise (alpha must be 0 here)");
   if (R > 0 && (!kind || !obs || !legal || !prior || !value || !pending || !bot_seeds))
     return Fail(OS_ERR_INVALID, "null request / response buffer");
   os_mcts_params q = *p;
+  q.policy = OS_POLICY_CPP;  // the shuffle is the az kernels' own (e->az_np)
+  if (np) q.max_memory_mb = 0;  // mcts.py never garbage-collects
   q.n_rollouts = 2;  // f64 node rewards (Node<double>): values are not integral
   q.child_selection = OS_SELECT_UCT;  // `puct` selects; the LUT stays log(N)
   q.layout = OS_LAYOUT_LANE;
@@ -929,7 +936,7 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   if (e->az_noise) {
     // The root expands once unless GC clears its children (mcts.cc:430-443);
     // the noise is drawn ahead for that one expansion.
-    const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+    const int64_t max_nodes = (q.max_memory_mb << 20) / 80 + 1;
     const int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * e->game.cfg.max_children;
     if (max_nodes > 1 && worst >= max_nodes)
       return Fail(OS_ERR_UNSUPPORTED,
@@ -970,10 +977,11 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     HIP_TRY(hipMemcpy(e->d_az_pos.p, bot_pos, static_cast<size_t>(R) * 4, hipMemcpyHostToDevice));
   }
   e->az_puct = puct ? 1 : 0;
+  e->az_np = np ? 1 : 0;
   {
     // One wave per search unless GC could fire (k_waz_step has no GC; the
     // lane kernel runs mcts.cc:402-424 exactly) or the caller asks for lanes.
-    const int64_t max_nodes = (p->max_memory_mb << 20) / 80 + 1;
+    const int64_t max_nodes = (q.max_memory_mb << 20) / 80 + 1;
     const int64_t worst = 1 + static_cast<int64_t>(p->max_simulations) * e->game.cfg.max_children;
     const bool gc_possible = max_nodes > 1 && worst >= max_nodes;
     if (e->az_layout == OS_LAYOUT_WAVE && gc_possible)
@@ -1543,6 +1551,50 @@ int os_az_get_layout(os_engine* e, int32_t* layout) {
   if (!e || !layout) return Fail(OS_ERR_INVALID, "null argument");
   if (!e->az_ready) return Fail(OS_ERR_INVALID, "no os_az_prepare batch");
   *layout = e->az_wave ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
+  return OS_OK;
+}
+
+int os_az_set_noise(os_engine* e, const double* noise, int64_t stride, double eps) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  if (!e->az_ready) return Fail(OS_ERR_INVALID, "no os_az_prepare batch");
+  if (!(eps >= 0.0) || eps > 1.0) return Fail(OS_ERR_INVALID, "epsilon must be in [0, 1]");
+  if (e->params.max_memory_mb != 0 &&
+      1 + static_cast<int64_t>(e->params.max_simulations) * e->game.cfg.max_children >=
+          (e->params.max_memory_mb << 20) / 80 + 1)
+    return Fail(OS_ERR_UNSUPPORTED, "root noise with a node budget small enough for GC to fire");
+  const int64_t R = e->num_roots;
+  const int mc = e->game.cfg.max_children;
+  if (!noise) {
+    e->az_noise = false;
+    return OS_OK;
+  }
+  if (stride < mc) return Fail(OS_ERR_INVALID, "noise stride below max_children");
+  const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
+  std::vector<double> packed(Rz * mc, 0.0);
+  for (int64_t r = 0; r < R; ++r)
+    std::memcpy(packed.data() + r * mc, noise + r * stride, mc * 8);
+  std::vector<int32_t> skip(Rz, 0);  // drawn by the caller: no bot words to skip
+  int rc;
+  if ((rc = e->d_az_noise.ensure(packed.size() * 8)) || (rc = e->d_az_skip.ensure(Rz * 4)))
+    return rc;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipMemcpy(e->d_az_noise.p, packed.data(), packed.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_az_skip.p, skip.data(), Rz * 4, hipMemcpyHostToDevice));
+  e->az_noise = true;
+  e->az_eps = eps;
+  return OS_OK;
+}
+
+int os_az_tree_priors(os_engine* e, int64_t r, int64_t count, double* prior) {
+  if (!e || !prior) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->az_ready) return Fail(OS_ERR_INVALID, "no os_az_prepare batch");
+  if (r < 0 || r >= e->num_roots || r >= static_cast<int64_t>(e->last_results.size()))
+    return Fail(OS_ERR_INVALID, "root index out of range (os_az_fetch first)");
+  if (count != static_cast<int64_t>(e->last_results[r].used))
+    return Fail(OS_ERR_INVALID, "count must be the tree's node count (os_engine_tree)");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipMemcpy(prior, static_cast<const double*>(e->d_az_prior.p) + r * e->cap, count * 8,
+                    hipMemcpyDeviceToHost));
   return OS_OK;
 }
 

@@ -169,6 +169,7 @@ struct AzArgs {
   GameCfg cfg;
   SearchParams sp;
   int32_t puct;
+  int32_t np_policy;        // python/algorithms/mcts.py semantics (os_az.h az_step)
   int64_t num_roots;
   const void* roots;        // [R] G::State
   void* slots;              // [R] AzSlot<G>
@@ -326,6 +327,7 @@ struct os_engine {
   // prepared external-evaluator batch (os_az_*): caller-owned device buffers
   bool az_ready = false;
   int32_t az_puct = 0;
+  int32_t az_np = 0;  // OS_POLICY_NUMPY external-evaluator batch
   int32_t* az_kind = nullptr;
   float* az_obs = nullptr;
   uint8_t* az_legal = nullptr;

@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(64) void k_az_step(AzArgs a) {
   typename G::Ctx ctx = AzCtx<G>::make(a, r);
   az_step<G>(a.cfg, a.sp, a.puct, root, sl, nodes, a.priors + r * static_cast<int64_t>(a.cap),
              a.raw ? a.raw + r * static_cast<int64_t>(a.cap) : nullptr, a.cap, bot, io,
-             a.obs_size, a.num_actions, ctx, nz);
+             a.obs_size, a.num_actions, ctx, nz, a.np_policy != 0);
   sl.mt_idx = bot.idx;
   sl.mt_pre = bot.pre;
   sl.res.rng_words += bot.words;
@@ -1339,7 +1339,8 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       legal_lanes(lg, acts);
       perm.a0 = static_cast<uint32_t>(l);
       perm.a1 = static_cast<uint32_t>(l + 64);
-      wave_shuffle<kPolicyCpp>(perm, nc, bot);
+      if (a.np_policy) wave_shuffle<kPolicyNumpy>(perm, nc, bot);  // mcts.py:320
+      else wave_shuffle<kPolicyCpp>(perm, nc, bot);
       const uint32_t first = from_raw ? parked_first : used;
       WAZ_CHECK(nc >= 1 && nc <= 128, 5);
       WAZ_CHECK(first + static_cast<uint32_t>(nc) <= cap, 6);
@@ -1513,7 +1514,8 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       const int rout = __builtin_amdgcn_readfirstlane(rt.out);
       const int rnc = __builtin_amdgcn_readfirstlane(rt.nchild);
       WAZ_PH(kPhBackup);
-      if (rout != kUnsolved || rnc == 1) break;  // mcts.cc:398-401
+      // mcts.cc:398-401; mcts.py:440-441 stops on a solved root only
+      if (rout != kUnsolved || (rnc == 1 && !a.np_policy)) break;
       phase = 0;
     }
   }
@@ -2049,6 +2051,7 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
   a.cfg = d.cfg;
   a.sp = d.sp;
   a.puct = e->az_puct;
+  a.np_policy = e->az_np;
   a.num_roots = e->num_roots;
   a.roots = d.roots;
   a.slots = e->d_az_slots.p;

@@ -101,7 +101,7 @@ class ExternalEvaluatorSearch:
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
           dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False,
           bot_rng=None, requests="fused", graph=False, graph_batch=8, block_size=0,
-          layout="auto"):
+          layout="auto", policy="cpp", root_noise=None):
     """Runs every search to completion; returns the os_mcts_batch outputs.
 
     The evaluator may be called once more after the last step, with every
@@ -119,6 +119,14 @@ class ExternalEvaluatorSearch:
     block_size: searches per k_az_step workgroup (one wave; 64 when 0).
     time_steps: record a HIP event pair around every k_az_step launch on the
     launch stream (`step_ms()` then sums them).
+
+    policy="numpy": the search of python/algorithms/mcts.py (mcts.py:292-443)
+    -- RandomState.shuffle of each expansion on the bot's stream (bot_rng:
+    the RandomState's (key, pos)), no single-child stop, no GC.  Its root
+    noise is RandomState.dirichlet, which only the caller's RandomState can
+    draw: pass it as root_noise ([R][>= max_children] float64, root r's j-th
+    legal action) with dirichlet_epsilon, and the stream after the draw as
+    bot_rng (dirichlet_alpha stays 0; os_az_set_noise).
 
     graph=True: after two eager rounds, one round (k_az_step + the evaluator +
     the response copies) is captured into a HIP graph and replayed
@@ -139,8 +147,14 @@ class ExternalEvaluatorSearch:
     prior = torch.zeros(R, A, dtype=torch.float64, device=dev)
     value = torch.zeros(R, dtype=torch.float64, device=dev)
     pending = torch.zeros(1, dtype=torch.int32, device=dev)
+    if policy not in ("cpp", "numpy"):
+      raise ValueError("policy must be 'cpp' or 'numpy'")
+    if root_noise is not None and policy != "numpy":
+      raise ValueError("root_noise is for policy='numpy' (the C++ bot's noise is drawn "
+                       "by the engine from dirichlet_alpha)")
     p = E.make_params(uct_c=uct_c, max_simulations=max_simulations,
-                      max_memory_mb=max_memory_mb, solve=solve, block_size=block_size)
+                      max_memory_mb=max_memory_mb, solve=solve, block_size=block_size,
+                      policy=_lib.POLICY_NUMPY if policy == "numpy" else _lib.POLICY_CPP)
     acts = _lib.i64(root_actions)
     if requests not in _REQUESTS:
       raise ValueError("requests must be 'fused' or 'separate'")
@@ -163,6 +177,11 @@ class ExternalEvaluatorSearch:
           ptr(pos), float(dirichlet_alpha), float(dirichlet_epsilon), kind.data_ptr(),
           obs.data_ptr(), legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
           pending.data_ptr()))
+    if root_noise is not None:
+      rn = np.ascontiguousarray(root_noise, dtype=np.float64)
+      if rn.ndim != 2 or rn.shape[0] != R or rn.shape[1] < self.eng.max_children:
+        raise ValueError("root_noise must be [R][>= max_children]")
+      check(lib.os_az_set_noise(self.eng._h, ptr(rn), rn.shape[1], float(dirichlet_epsilon)))
     # the kernel the engine chose (AUTO: wave unless GC can fire)
     lay = np.zeros(1, np.int32)
     check(lib.os_az_get_layout(self.eng._h, ptr(lay)))
@@ -237,6 +256,15 @@ class ExternalEvaluatorSearch:
           break
     st.synchronize()
     self.requests += int(total.item())
+
+  def tree(self, r=0):
+    """Search r's tree after run(): os_engine_tree's flat arrays plus the
+    node priors (os_az_tree_priors)."""
+    t = self.eng.tree(r)
+    pr = np.zeros(len(t["n"]), np.float64)
+    check(lib.os_az_tree_priors(self.eng._h, r, len(pr), ptr(pr)))
+    t["prior"] = pr
+    return t
 
   def eng_az_wave(self):
     """True when the last prepared batch runs k_waz_step (os_az_set_layout)."""

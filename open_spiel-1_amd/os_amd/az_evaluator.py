@@ -1,0 +1,116 @@
+"""AlphaZeroEvaluator drop-in (python/algorithms/alpha_zero/evaluator.py) with
+the batched protocol the device search drives.
+
+The reference evaluator answers `evaluate(state)` / `prior(state)` one state at
+a time through its model's `inference(obs, mask)` on a singleton batch,
+memoised in an LRU cache keyed by the observation and mask bytes
+(evaluator.py:28-83).  The model's `inference` takes a batch, so the same
+network answers a whole round of device requests at once: `evaluate_batch`
+hands it every pending request of an external-evaluator step
+(os_amd/az.py) with the arrays `_inference` would have built -- observation
+rows as float64 (ObservationTensor, flat), legal masks as int64 -- and returns
+action-indexed priors and player-0 values.  The evaluator is a pure function
+of (observation, mask) (the cache relies on that too), so the device search
+fuses each leaf's Evaluate and Prior into one request
+(os_az_set_requests OS_AZ_REQUESTS_FUSED).  Results equal the per-state calls
+for a model whose outputs do not depend on the batch they are computed in.
+"""
+import collections
+
+import numpy as np
+
+from . import pyspiel
+from .mcts import Evaluator
+
+
+class LRUCache(object):
+  """Least-recently-used cache (python/utils/lru_cache.py:38-93)."""
+
+  CacheInfo = collections.namedtuple("CacheInfo", ["hits", "misses", "size", "max_size"])
+
+  def __init__(self, max_size):
+    self._max_size = max_size
+    self._data = collections.OrderedDict()
+    self._hits = 0
+    self._misses = 0
+
+  def clear(self):
+    self._data.clear()
+    self._hits = self._misses = 0
+
+  def make(self, key, fn):
+    if key in self._data:
+      val = self._data.pop(key)
+      self._hits += 1
+    else:
+      self._misses += 1
+      val = fn()
+      if len(self._data) >= self._max_size:
+        self._data.popitem(last=False)
+    self._data[key] = val
+    return val
+
+  def info(self):
+    return LRUCache.CacheInfo(self._hits, self._misses, len(self._data), self._max_size)
+
+
+class AlphaZeroEvaluator(Evaluator):
+  """An AlphaZero MCTS evaluator over a model with `inference(obs, mask)`
+  returning (value [N, 1], policy [N, A]) (evaluator.py:28-83)."""
+
+  # evaluate / prior are one cached inference: a fused device request
+  pure_function = True
+
+  def __init__(self, game, model, cache_size=2 ** 16):
+    if game.num_players() != 2:
+      raise ValueError("Game must be for two players.")
+    gt = game.get_type()
+    if gt.reward_model != pyspiel.GameType.RewardModel.TERMINAL:
+      raise ValueError("Game must have terminal rewards.")
+    if gt.dynamics != pyspiel.GameType.Dynamics.SEQUENTIAL:
+      raise ValueError("Game must have sequential turns.")
+    if gt.chance_mode != pyspiel.GameType.ChanceMode.DETERMINISTIC:
+      raise ValueError("Game must be deterministic.")
+    self._model = model
+    self._cache = LRUCache(cache_size)
+
+  def cache_info(self):
+    return self._cache.info()
+
+  def clear_cache(self):
+    self._cache.clear()
+
+  def _inference(self, state):
+    obs = np.expand_dims(state.observation_tensor(), 0)
+    mask = np.expand_dims(state.legal_actions_mask(), 0)
+    key = obs.tobytes() + mask.tobytes()
+    value, policy = self._cache.make(key, lambda: self._model.inference(obs, mask))
+    return value[0, 0], policy[0]
+
+  def evaluate(self, state):
+    value, _ = self._inference(state)
+    return np.array([value, -value])
+
+  def prior(self, state):
+    _, policy = self._inference(state)
+    return [(action, policy[action]) for action in state.legal_actions()]
+
+  def evaluate_batch(self, obs, legal, kind):
+    """One round of device requests (os_amd/az.py protocol): obs float32
+    [N, C, H, W], legal bool [N, A], kind int32 [N] (0 = idle) on the GPU;
+    returns (prior float64 [N, A] action-indexed, value float64 [N], player 0)."""
+    import torch
+    n, a = legal.shape
+    prior = np.zeros((n, a), np.float64)
+    value = np.zeros(n, np.float64)
+    live = np.nonzero(kind.cpu().numpy())[0]
+    if len(live):
+      # the arrays _inference builds: ObservationTensor as float64 rows (the
+      # tensor's values are exact in float32), legal_actions_mask as int64
+      o = obs.reshape(n, -1)[live].to(torch.float64).cpu().numpy()
+      m = legal[live].to(torch.int64).cpu().numpy()
+      v, p = self._model.inference(o, m)
+      prior[live] = np.asarray(p, np.float64)
+      value[live] = np.asarray(v, np.float64).reshape(len(live), -1)[:, 0]
+    dev = obs.device
+    return torch.from_numpy(prior).to(dev), torch.from_numpy(value).to(dev)

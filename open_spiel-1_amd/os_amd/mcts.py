@@ -3,18 +3,25 @@
 Public names and signatures follow the reference module (Evaluator :29-43,
 RandomRolloutEvaluator :46-82, SearchNode :85-196, MCTSBot :199-443).
 
-`MCTSBot.mcts_search` runs on the MI355X whenever the search is the hot path
-the engine implements — a `RandomRolloutEvaluator`, UCT or PUCT child
-selection (`SearchNode.uct_value` / `SearchNode.puct_value`), no Dirichlet
-noise, one of the supported games (the five, and pig with its chance nodes) —
-continuing the bot's and
-the evaluator's `np.random.RandomState` streams in place, bit-exact with the
-reference module (one shared RandomState, as in mcts_test.py:41-54, or two).
-Searches the engine does not implement (user evaluators, custom
-`child_selection_fn`, Dirichlet noise, hex / go boards above 11 x 11) run the
-generic host loop below with a RuntimeWarning under `backend="auto"`; pass
-`backend="hip"` to forbid that and fail loudly instead, or `backend="host"` to
-choose it.
+`MCTSBot.mcts_search` runs on the MI355X whenever the search is one the
+engine implements, continuing the bot's (and the evaluator's)
+`np.random.RandomState` streams in place, bit-exact with the reference module:
+- a `RandomRolloutEvaluator` (one shared RandomState, as in
+  mcts_test.py:41-54, or two), UCT or PUCT child selection
+  (`SearchNode.uct_value` / `SearchNode.puct_value`), no Dirichlet noise, one
+  of the supported games (the five, and pig with its chance nodes);
+- an evaluator with a batched protocol -- `evaluate_into`, or
+  `evaluate_batch(obs, legal, kind) -> (prior, value)` such as this package's
+  `AlphaZeroEvaluator` -- on a deterministic two-player game: the AlphaZero
+  bot of alpha_zero.py:185-192 (PUCT, Dirichlet root noise, solve=False).
+  The search runs in the external-evaluator kernel (os_amd/az.py), one
+  evaluator round per simulation; the root noise is drawn with the bot's own
+  `RandomState.dirichlet` where mcts.py:314-316 draws it (the first use of the
+  stream in a search whose evaluator draws nothing), and mixed on the device.
+Searches the engine does not implement (other evaluators, a custom
+`child_selection_fn`, hex / go boards above 11 x 11) run the generic host
+loop below with a RuntimeWarning under `backend="auto"`; pass `backend="hip"`
+to forbid that and fail loudly instead, or `backend="host"` to choose it.
 """
 import math
 import time
@@ -146,10 +153,12 @@ def _outcome_vector(code, nplayers):
 class _TreeView(object):
   """The engine's flat arena of one search (os_engine_tree) plus what node
   construction needs; shared by every lazy node of that tree."""
-  __slots__ = ("first", "n", "w", "action", "nchild", "out0", "p0", "chance", "nplayers")
+  __slots__ = ("first", "n", "w", "action", "nchild", "out0", "p0", "chance", "nplayers",
+               "prior")
 
   def __init__(self, flat, state, game):
     self.first, self.n, self.w = flat["first"], flat["n"], flat["w"]
+    self.prior = flat.get("prior")  # external-evaluator trees: the node priors
     self.action, self.nchild, self.out0 = flat["action"], flat["nchild"], flat["out0"]
     self.p0 = state.current_player()
     self.chance = (game.get_type().chance_mode !=
@@ -197,7 +206,8 @@ class _LazySearchNode(SearchNode):
                   for k, a in enumerate(acts)]
         else:
           child_player = v.p0 ^ (self._depth & 1)
-          kids = [_LazySearchNode(v, base + k, self._depth + 1, a, child_player, 1.0 / nc)
+          kids = [_LazySearchNode(v, base + k, self._depth + 1, a, child_player,
+                                  1.0 / nc if v.prior is None else float(v.prior[base + k]))
                   for k, a in enumerate(acts)]
       self._kids = kids
     return self._kids
@@ -248,15 +258,37 @@ class MCTSBot(pyspiel.Bot):
     self._child_selection_fn = child_selection_fn
     self.backend = backend
     if backend == "hip" and not self._gpu_eligible():
-      raise ValueError("backend='hip' needs RandomRolloutEvaluator, UCT or PUCT "
-                       "child selection, no Dirichlet noise and a supported game")
+      raise ValueError("backend='hip' needs UCT or PUCT child selection, a supported game "
+                       "and either RandomRolloutEvaluator without Dirichlet noise or an "
+                       "evaluator with a batched protocol (evaluate_into / evaluate_batch)")
     self._warned_host = False
 
   def _gpu_eligible(self):
+    return self._rollout_eligible() or self._external_eligible()
+
+  def _rollout_eligible(self):
     return (type(self.evaluator) is RandomRolloutEvaluator and
             self._child_selection_fn in (SearchNode.uct_value, SearchNode.puct_value) and
             not self._dirichlet_noise and
             isinstance(self._game, pyspiel.Game) and self._game.on_device(numpy_policy=True))
+
+  def _device_evaluator(self):
+    """The batched form of the evaluator the external-evaluator kernel drives
+    (os_amd/az.py protocol), or None."""
+    ev = self.evaluator
+    if type(ev) is RandomRolloutEvaluator:
+      return None
+    if getattr(ev, "evaluate_into", None) is not None:
+      return ev
+    return getattr(ev, "evaluate_batch", None)
+
+  def _external_eligible(self):
+    g = self._game
+    return (self._device_evaluator() is not None and
+            self._child_selection_fn in (SearchNode.uct_value, SearchNode.puct_value) and
+            isinstance(g, pyspiel.Game) and g.on_device(numpy_policy=True) and
+            g.num_players() == 2 and
+            g.get_type().chance_mode == pyspiel.GameType.ChanceMode.DETERMINISTIC)
 
   def restart_at(self, state):
     pass
@@ -315,7 +347,9 @@ class MCTSBot(pyspiel.Bot):
 
   def _run_gpu(self, state):
     """One search on the device continuing the RandomState streams; returns
-    (root outputs, engine holding the tree)."""
+    (root outputs, object whose tree(0) is the search tree)."""
+    if not self._rollout_eligible():
+      return self._run_gpu_external(state)
     eng = pyspiel._engine_for(self._game)
     bot_rs = self._random_state
     ev_rs = self.evaluator._random_state
@@ -333,6 +367,36 @@ class MCTSBot(pyspiel.Bot):
     if not shared:
       ev_rs.set_state(("MT19937", ne[0], ne[1], e[3], e[4]))
     return out, eng
+
+  def _run_gpu_external(self, state):
+    """mcts.py's search (:395-443) with a batched evaluator, in the
+    external-evaluator kernel: RandomState.shuffle expansions on the bot's
+    stream, no single-child stop, no GC; one evaluator round per simulation
+    (fused Evaluate + Prior for a pure evaluator)."""
+    search = pyspiel._az_search_for(self._game)
+    rs = self._random_state
+    noise = None
+    eps = 0.0
+    if (self._dirichlet_noise and self.max_simulations >= 2 and not state.is_terminal()):
+      # mcts.py:314-316 at the root's expansion (simulation 1): the evaluator
+      # drew nothing before it, so it is the search's first use of the stream.
+      eps, alpha = self._dirichlet_noise
+      n = len(state.legal_actions(state.current_player()))
+      noise = np.zeros((1, search.eng.max_children), np.float64)
+      noise[0, :n] = rs.dirichlet([alpha] * n)
+    b = rs.get_state()
+    hist = np.asarray(state.history(), np.int64)
+    pure = bool(getattr(self.evaluator, "pure_function", False))
+    out = search.run(hist, np.array([0, len(hist)], np.int64), None, self._device_evaluator(),
+                     puct=self._child_selection_fn is SearchNode.puct_value,
+                     max_simulations=self.max_simulations, uct_c=self.uct_c,
+                     solve=self.solve, max_memory_mb=0,
+                     bot_rng=(np.asarray(b[1], np.uint32)[None], np.array([b[2]], np.int32)),
+                     requests="fused" if pure else "separate", policy="numpy",
+                     root_noise=noise, dirichlet_epsilon=eps)
+    keys, pos = search.bot_rng_out
+    rs.set_state(("MT19937", keys[0], int(pos[0]), b[3], b[4]))
+    return out, search
 
   # ---- generic host path (user evaluators / selection functions) ------------
   def _descend(self, root, state):

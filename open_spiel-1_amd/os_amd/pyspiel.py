@@ -522,6 +522,21 @@ def _engine_for(game):
   return eng
 
 
+_AZ_SEARCHES = {}
+
+
+def _az_search_for(game):
+  """The external-evaluator search (os_amd/az.py) a Python MCTSBot with a
+  batched evaluator runs on, one per game."""
+  from .az import ExternalEvaluatorSearch
+  key = str(game)
+  s = _AZ_SEARCHES.get(key)
+  if s is None:
+    s = ExternalEvaluatorSearch(game.game_string, device=0)
+    _AZ_SEARCHES[key] = s
+  return s
+
+
 class MCTSBot(Bot):
   """pyspiel.MCTSBot (mcts.h:139-208; pyspiel.cc:512-524) on the GPU.
 

@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Generates tests/golden/python_az_bot.json: the reference Python AlphaZero
+bot -- `mcts.MCTSBot` built exactly as alpha_zero.py:181-192 `_init_bot`
+builds it (PUCT, Dirichlet root noise, solve=False) over the reference
+`AlphaZeroEvaluator` (alpha_zero/evaluator.py) -- playing a few moves of a
+game with a deterministic model (tests/az_toy_model.py).
+
+Run in the build container only (it reads /root/reference, which does not
+exist on the GPU box).  The reference modules are loaded UNMODIFIED from their
+files: mcts.py, alpha_zero/evaluator.py and utils/lru_cache.py (the
+evaluator's own imports are pointed at those two); `import pyspiel` inside
+them resolves to this repo's drop-in, which runs the game rules on the host.
+The JSON holds data only: inputs and the reference's outputs.
+
+    python tools/gen_az_python_goldens.py [--reference /root/reference]
+
+Per game and seed: the bot's RandomState is seeded in place after
+construction (`bot._random_state.seed(seed)`, since _init_bot leaves it
+unseeded); then `moves` times: root = bot.mcts_search(state), record the
+root's children in tree order (action, explore_count, total_reward, prior,
+outcome) and root counts, best_child, and the RandomState after the search
+(position, key sha256, has_gauss, cached gaussian); play best_child.
+"""
+import argparse
+import hashlib
+import importlib.util
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "open_spiel-1_amd")
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def load_module(name, path):
+  spec = importlib.util.spec_from_file_location(name, path)
+  mod = importlib.util.module_from_spec(spec)
+  sys.modules[name] = mod
+  spec.loader.exec_module(mod)
+  return mod
+
+
+def rs_state(rs):
+  st = rs.get_state()
+  return {"pos": int(st[2]),
+          "key_sha256": hashlib.sha256(np.asarray(st[1], np.uint32).tobytes()).hexdigest(),
+          "has_gauss": int(st[3]), "gauss": float(st[4])}
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--reference", default="/root/reference")
+  args = ap.parse_args()
+  sys.path.insert(0, PKG)
+  sys.path.insert(0, os.path.join(ROOT, "tests"))
+  import pyspiel  # the drop-in: the reference modules import it
+  from az_toy_model import ToyModel
+  ref = os.path.join(args.reference, "open_spiel", "python")
+  # The reference evaluator imports `open_spiel.python.algorithms.mcts` and
+  # `open_spiel.python.utils.lru_cache`: point those names at the reference files.
+  pkgs = {}
+  for name in ("open_spiel", "open_spiel.python", "open_spiel.python.algorithms",
+               "open_spiel.python.utils"):
+    pkgs[name] = sys.modules.get(name)
+    m = types.ModuleType(name)
+    m.__path__ = []
+    sys.modules[name] = m
+  mcts = load_module("open_spiel.python.algorithms.mcts", os.path.join(ref, "algorithms/mcts.py"))
+  sys.modules["open_spiel.python.algorithms"].mcts = mcts
+  lru = load_module("open_spiel.python.utils.lru_cache", os.path.join(ref, "utils/lru_cache.py"))
+  sys.modules["open_spiel.python.utils"].lru_cache = lru
+  evl = load_module("ref_az_evaluator", os.path.join(ref, "algorithms/alpha_zero/evaluator.py"))
+  assert evl.mcts is mcts and mcts.pyspiel is sys.modules["pyspiel"]
+
+  def init_bot(config, game, evaluator_, evaluation):
+    # alpha_zero.py:181-192, verbatim in effect
+    noise = None if evaluation else (config["policy_epsilon"], config["policy_alpha"])
+    return mcts.MCTSBot(game, config["uct_c"], config["max_simulations"], evaluator_,
+                        solve=False, dirichlet_noise=noise,
+                        child_selection_fn=mcts.SearchNode.puct_value, verbose=False)
+
+  plan = [
+      # game, max_simulations, moves, seeds, evaluation (no noise), alpha, eps
+      ("tic_tac_toe", 100, 4, [0, 42], False, 1.0, 0.25),
+      # alpha > 1: the gamma draws use the polar normal, whose spare value
+      # stays cached in the RandomState (has_gauss) across searches
+      ("tic_tac_toe", 80, 3, [9], False, 2.0, 0.25),
+      ("connect_four", 200, 4, [0, 7], False, 1.0, 0.25),
+      ("connect_four", 150, 3, [3], False, 0.3, 0.25),
+      ("connect_four", 150, 2, [5], True, 1.0, 0.25),
+      ("hex(board_size=5)", 150, 3, [1], False, 0.5, 0.25),
+      ("breakthrough(rows=6,columns=6)", 120, 2, [2], False, 1.0, 0.25),
+      ("go(board_size=7,komi=4.5)", 100, 2, [4], False, 0.03 * 361 / 49, 0.25),
+  ]
+  cases = []
+  for gs, sims, moves, seeds, evaluation, alpha, eps in plan:
+    game = pyspiel.load_game(gs)
+    A = game.num_distinct_actions()
+    obs_size = int(np.prod(game.observation_tensor_shape()))
+    for seed in seeds:
+      config = {"uct_c": 2.0, "max_simulations": sims, "policy_epsilon": eps,
+                "policy_alpha": alpha}
+      model = ToyModel(obs_size, A)
+      bot = init_bot(config, game, evl.AlphaZeroEvaluator(game, model), evaluation)
+      bot._random_state.seed(seed)
+      state = game.new_initial_state()
+      searches = []
+      for _ in range(moves):
+        if state.is_terminal():
+          break
+        root = bot.mcts_search(state)
+        best = root.best_child()
+        out = lambda o: None if o is None else [float(x) for x in o]
+        searches.append({
+            "history": [int(a) for a in state.history()],
+            "root": {"explore_count": int(root.explore_count),
+                     "total_reward": float(root.total_reward), "outcome": out(root.outcome)},
+            "children": [[int(c.action), int(c.explore_count), float(c.total_reward),
+                          float(c.prior), out(c.outcome)] for c in root.children],
+            "best_action": int(best.action),
+            "rng_after": rs_state(bot._random_state),
+        })
+        state.apply_action(best.action)
+      cases.append({"game": gs, "seed": seed, "config": config, "evaluation": evaluation,
+                    "searches": searches})
+      print("%-32s seed %d: %d searches" % (gs, seed, len(searches)))
+  doc = {"_source": "tools/gen_az_python_goldens.py: unmodified reference "
+                    "python/algorithms/mcts.py + alpha_zero/evaluator.py + utils/lru_cache.py, "
+                    "bot as alpha_zero.py:181-192 _init_bot, model tests/az_toy_model.py; "
+                    "numpy %s" % np.__version__,
+         "cases": cases}
+  with open(os.path.join(GOLD, "python_az_bot.json"), "w") as f:
+    json.dump(doc, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+  main()
