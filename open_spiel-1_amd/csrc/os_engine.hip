@@ -264,8 +264,10 @@ int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t pol
   if (BigBoard(cfg)) return OS_LAYOUT_LANE;  // k_lsearch
   if (cfg.kind == kGo)
     return policy == OS_POLICY_CPP && R >= 16384 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
-  if (cfg.kind == kHex)
-    return policy == OS_POLICY_CPP && cfg.rows >= 3 ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
+  // hex: one wave per search under both policies (the numpy policy's
+  // playout draws found over a lane window, os_wave.h hex_rollout_lanes_np);
+  // boards below 3 x 3 have no lane-parallel playout.
+  if (cfg.kind == kHex) return cfg.rows >= 3 ? OS_LAYOUT_WAVE : OS_LAYOUT_LANE;
   return OS_LAYOUT_WAVE;
 }
 

@@ -1183,6 +1183,12 @@ __device__ __forceinline__ void hex_take(uint32_t& r, uint32_t k, uint32_t tau, 
 //          ds_bpermute, both cells of a lane in one packed-u16 dword.
 // The winner owns the minimising cell; the stream advances by the 2 (T + 1)
 // words the serial playout draws for its T + 1 moves.
+//
+// hex_fill_end: the fill and end steps, from the draws k0 / k1 of moves l and
+// l + 64; returns T + 1, the moves the serial playout plays (0: decline).
+__device__ inline int hex_fill_end(const Hex::State& s, const GameCfg& g, B128 empty, int n0,
+                                   uint32_t k0, uint32_t k1);
+
 template <class C>
 __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
   (void)ctx;
@@ -1217,6 +1223,85 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
     else k1 = k;
   }
   if (ballot(risky)) return kLanesDecline;
+  const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
+  if (tend == 0) return kLanesDecline;  // unreachable
+  const int winner = s.to_play ^ ((tend - 1) & 1);  // the mover of the last stone
+  ev.seek(q0 + 2 * tend);
+  ev.words.add(2 * tend);
+  return winner == 0 ? 1 : -1;
+}
+
+// The same playout under python/algorithms/mcts.py (RandomState.choice over
+// LegalActions(), mcts.py:56-63).  |LegalActions| before move j is still
+// n0 - j, but numpy's masked-rejection draw (os_rng.h NpChoice: no word when
+// n = 1, else 32-bit words until (w & mask) <= n - 1) takes a varying number
+// of words, so the draws are found serially over a 64-word window of tempered
+// words on the lanes: the accepted word of move j is the first lane at or
+// after the cursor whose word passes move j's test (one compare and ballot),
+// and lane j records the draw and the stream offset after it.  The fill and
+// end steps are the C++ playout's; the stream then moves to the offset after
+// the last move's draw.  A playout whose draws would read past what peek_raw
+// reaches declines to the serial loop.
+template <class C>
+__device__ int hex_rollout_lanes_np(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
+  (void)ctx;
+  s = make_uniform(s);
+  ev.uniformize();
+  if (Hex::terminal(s, g)) return s.result;
+  const int l = lane_id();
+  const B128 empty = g.board & ~(s.st[0] | s.st[1]);
+  const int n0 = popc(empty);
+  const int q0 = ev.offset();
+  const int qmax = kMtN + (kMtN - kMtM) + (kMtN - kMtM);  // peek_raw's reach
+  int wb = 0;  // window base, relative to q0
+  auto load = [&](int b) {
+    const int q = q0 + b + l;
+    return MtStream::temper(ev.peek_raw(q < qmax ? q : qmax - 1));
+  };
+  uint32_t win = load(0);
+  int cur = 0;                             // next unread word: lane cur of the window
+  uint32_t k0 = 0, k1 = 0, e0 = 0, e1 = 0;  // draw / offset after it, moves l and l + 64
+  for (int j = 0; j < n0; ++j) {
+    const uint32_t rng = static_cast<uint32_t>(n0 - j - 1);
+    uint32_t k = 0;
+    if (rng != 0) {
+      const uint32_t mask = np_mask(rng);
+      for (;;) {
+        const uint64_t ok = ballot((win & mask) <= rng) & (cur < 64 ? ~0ull << cur : 0ull);
+        if (ok) {
+          const int idx = ctz64(ok);
+          k = rl32(win, idx) & mask;
+          cur = idx + 1;
+          break;
+        }
+        wb += 64;
+        cur = 0;
+        if (q0 + wb + 64 > qmax) return kLanesDecline;
+        win = load(wb);
+      }
+    }
+    const uint32_t e = static_cast<uint32_t>(wb + cur);
+    if (j < 64) {
+      k0 = wl32(k, j, k0);
+      e0 = wl32(e, j, e0);
+    } else {
+      k1 = wl32(k, j - 64, k1);
+      e1 = wl32(e, j - 64, e1);
+    }
+  }
+  const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
+  if (tend == 0) return kLanesDecline;  // unreachable
+  const int winner = s.to_play ^ ((tend - 1) & 1);
+  const int used = static_cast<int>(tend <= 64 ? rl32(e0, tend - 1) : rl32(e1, tend - 65));
+  ev.seek(q0 + used);
+  ev.words.add(used);
+  return winner == 0 ? 1 : -1;
+}
+
+__device__ inline int hex_fill_end(const Hex::State& s, const GameCfg& g, B128 empty, int n0,
+                                   uint32_t k0, uint32_t k1) {
+  const int l = lane_id();
+  const int n = g.rows;
   // Fill times of cells l (t0) and l + 64 (t1); ranks among the empty cells.
   uint32_t t0 = 0, t1 = 0;
   uint32_t r0 = ((empty.lo >> l) & 1) ? lanes_below(empty.lo) : 0x40000000u;
@@ -1314,11 +1399,8 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
     v = o < v ? o : v;
   }
   const uint32_t tend = rl32(v, 0);
-  if (tend == 0 || tend > static_cast<uint32_t>(n0)) return kLanesDecline;  // unreachable
-  const int winner = p ^ static_cast<int>((tend - 1) & 1);  // the mover of the last stone
-  ev.seek(q0 + 2 * static_cast<int>(tend));
-  ev.words.add(2 * tend);
-  return winner == 0 ? 1 : -1;
+  if (tend == 0 || tend > static_cast<uint32_t>(n0)) return 0;  // unreachable
+  return static_cast<int>(tend);
 }
 
 // breakthrough random playout (mcts.cc:46-55) with lanes as board squares.
@@ -1685,11 +1767,12 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
 #if OS_GO_LANES
   if constexpr (std::is_same<G, Go>::value) return go_rollout_wave<Policy>(s, g, ctx, ev);
 #endif
-  if constexpr (Policy == kPolicyCpp && std::is_same<G, Hex>::value) {
+  if constexpr (std::is_same<G, Hex>::value) {
     // n >= 3: on n <= 2 the reference's wrap filter (hex.cc:206-222) leaves
     // filled boards without a winner, so the end-of-fill argument fails.
     if (g.rows >= 3) {
-      const int r = hex_rollout_lanes(s, g, ctx, ev);
+      const int r = Policy == kPolicyCpp ? hex_rollout_lanes(s, g, ctx, ev)
+                                         : hex_rollout_lanes_np(s, g, ctx, ev);
       if (r != kLanesDecline) return r;
     }
   }
