@@ -54,6 +54,17 @@ OS_HD int rollout_ret0_chance(typename G::State s, const GameCfg& g, typename G:
   return G::ret0(s, g, ctx);
 }
 
+// The playout a search runs at a leaf: the serial one above, unless a
+// kernel's stream type has a faster equivalent (os_wave.h specialises this
+// for pig on the wave layout).  Same words drawn, same result.
+template <class G, int Policy, class Rng>
+struct ChanceRollout {
+  OS_HD static int run(const typename G::State& s, const GameCfg& g, typename G::Ctx& ctx,
+                       Rng& ev) {
+    return rollout_ret0_chance<G, Policy>(s, g, ctx, ev);
+  }
+};
+
 OS_HD int reward_player(int p, int root_player) { return p < 0 ? root_player : p; }
 
 // Evaluate()'s return vector (mcts.cc:42-71) for up to G::kMaxPlayers
@@ -199,7 +210,7 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
         const int leaf_mark = ctx.mark();
         for (int k = 0; k < sp.n_rollouts; ++k) {
           if (k) ctx.rewind(leaf_mark);
-          const int code = rollout_ret0_chance<G, Policy>(s, g, ctx, ev);
+          const int code = ChanceRollout<G, Policy, Rng>::run(s, g, ctx, ev);
           if (k) ret.add(code, g);
           else ret.set(code, g);
         }

@@ -23,6 +23,7 @@
 #ifndef OS_WAVE_H_
 #define OS_WAVE_H_
 
+#include "os_chance.h"
 #include "os_mcts.h"
 
 // Where wave-uniformity of the playout / walk state is re-asserted with
@@ -1402,6 +1403,139 @@ __device__ inline int hex_fill_end(const Hex::State& s, const GameCfg& g, B128 e
   if (tend == 0 || tend > static_cast<uint32_t>(n0)) return 0;  // unreachable
   return static_cast<int>(tend);
 }
+
+// pig random playout (mcts.cc:42-71 / mcts.py:56-67) on the wave.  The
+// serial playout, run wave-uniformly, spent ~100 scalar and vector
+// instructions per move on the generic n-player state machine (every score
+// updated, every player tested for a win, f64 chance sampling on the vector
+// unit feeding scalar branches).  Here:
+//   * each 64-word window of the stream is decoded once on the lanes: lane i
+//     holds, for words (i, i + 1), the chance outcome that a chance node
+//     drawing at word i would sample (SampleAction over absl::Uniform(0, 1)
+//     under the C++ policy, RandomState.choice(p=) under numpy; os_rng.h) and
+//     the roll / stop bit a two-action decision drawing there would take
+//     (absl: the low word's bit; numpy: the word's bit);
+//   * the move loop keeps the turn in scalars -- turn player, turn total,
+//     that player's score, the move count -- with the scores on the lanes
+//     (lane p = player p, read once per turn): a decision reads one packed
+//     lane value, a stop writes one lane, and only the stopping player can
+//     have reached the winning score (pig.cc:180-223: the others have not
+//     changed since the last test).
+// Words drawn per move are those of the serial playout: decisions 2 (absl,
+// either action count) or 1 / 0 (numpy, two / one action), chance nodes 2.
+template <int Policy>
+__device__ int pig_rollout_wave(Pig::State s, const GameCfg& g, WaveMt& ev) {
+  s = make_uniform(s);
+  ev.uniformize();
+  NoCtx nctx;
+  if (Pig::terminal(s, g)) return Pig::ret0(s, g, nctx);
+  const int l = lane_id();
+  uint32_t sc = 0;  // lane p: score of player p
+#pragma unroll
+  for (int i = 0; i < Pig::kMaxPlayers; ++i) sc = l == i ? static_cast<uint32_t>(s.score[i]) : sc;
+  const int win = g.pig_win, hz = g.pig_horizon, np = g.pig_players, dice = g.pig_dice;
+  const double p = 1.0 / dice;  // Pig::chance_prob
+  int tp = s.turn_player, tt = s.turn_total, moves = s.moves;
+  bool at_chance = s.cur < 0;
+  int cs = static_cast<int>(rl32(sc, tp));
+  int wb = ev.offset();  // stream offset of the window's word 0 (current block)
+  int c = 0;             // cursor in the window
+  int used = 0;          // words drawn
+  uint32_t pk = 0;       // per lane: chance outcome | decision bit << 8
+  auto load = [&]() {
+    const uint32_t w0 = MtStream::temper(ev.peek_raw(wb + l));
+    const uint32_t w1 = MtStream::temper(ev.peek_raw(wb + l + 1));
+    int k;
+    uint32_t bit;
+    if (Policy == kPolicyCpp) {
+      uint64_t bits = (static_cast<uint64_t>(w0) << 32) | w1;  // AbslUniformDouble01
+      double u = 0.0;
+      if (bits != 0) {
+        const int clz = __clzll(static_cast<long long>(bits));
+        bits <<= clz;
+        const uint64_t val = (static_cast<uint64_t>(1022 - clz) << 52) |
+                             ((bits >> 11) & ((1ull << 52) - 1));
+        __builtin_memcpy(&u, &val, 8);
+      }
+      k = SampleEquiprobable(dice, p, u);
+      bit = w1 & 1u;  // AbslUniform(2): the second word's low bit
+    } else {
+      const double u = ((w0 >> 5) * 67108864.0 + (w1 >> 6)) / 9007199254740992.0;
+      double last = 0.0, acc = 0.0;  // NpChoiceEquiprobable
+      for (int j = 0; j < dice; ++j) last = acc = acc + p;
+      k = 0;
+      acc = 0.0;
+      for (int j = 0; j < dice; ++j) {
+        acc = acc + p;
+        k += (acc / last <= u) ? 1 : 0;
+      }
+      bit = w0 & 1u;  // NpChoice(2): mask 1, never rejected
+    }
+    pk = static_cast<uint32_t>(k) | (bit << 8);
+  };
+  auto need = [&](int n) {  // the next n words must lie in the window
+    if (c + n <= 64) return;
+    wb += c;
+    c = 0;
+    if (wb >= kMtN) {  // the window left the block: twist it (seek), rebase
+      ev.seek(wb);
+      wb -= kMtN;
+    }
+    load();
+  };
+  load();
+  for (;;) {
+    if (moves >= hz) break;  // terminal (a winner ends the loop where it is made)
+    if (!at_chance) {
+      const bool only_stop = cs + tt >= win;  // Pig::legal: stop alone
+      const int nw = Policy == kPolicyCpp ? 2 : (only_stop ? 0 : 1);
+      need(nw);
+      const int a = only_stop ? 1 : static_cast<int>((rl32(pk, c) >> 8) & 1u);
+      c += nw;
+      used += nw;
+      moves++;
+      if (a == 0) {  // roll
+        at_chance = true;
+        continue;
+      }
+      cs += tt;  // stop: bank the turn total
+      sc = l == tp ? static_cast<uint32_t>(cs) : sc;
+      tt = 0;
+      tp = tp + 1 < np ? tp + 1 : 0;
+      if (cs >= win) break;
+      cs = static_cast<int>(rl32(sc, tp));
+    } else {
+      need(2);
+      const int a = static_cast<int>(rl32(pk, c) & 0xffu) + 1;  // ChanceOutcomes()[k]: k + 1
+      c += 2;
+      used += 2;
+      at_chance = false;
+      if (a == 1) {  // pig.cc:208-213
+        tt = 0;
+        tp = tp + 1 < np ? tp + 1 : 0;
+        cs = static_cast<int>(rl32(sc, tp));
+      } else {
+        tt += a + 1;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < Pig::kMaxPlayers; ++i) s.score[i] = static_cast<int32_t>(rl32(sc, i));
+  s.turn_total = tt;
+  s.turn_player = tp;
+  s.cur = at_chance ? -1 : tp;
+  s.moves = moves;
+  ev.seek(wb + c);
+  ev.words.add(used);
+  return Pig::ret0(s, g, nctx);
+}
+
+template <int Policy>
+struct ChanceRollout<Pig, Policy, WaveMt> {
+  __device__ static int run(const Pig::State& s, const GameCfg& g, NoCtx&, WaveMt& ev) {
+    return pig_rollout_wave<Policy>(s, g, ev);
+  }
+};
 
 // breakthrough random playout (mcts.cc:46-55) with lanes as board squares.
 // The legal set changes every move, so the moves stay serial, but the board
