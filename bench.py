@@ -101,6 +101,10 @@ def parse():
   ap.add_argument("--az-layout", default="auto", choices=("auto", "wave", "lane"),
                   help="az: one wavefront per search (k_waz_step), one lane per search "
                        "(k_az_step) or auto (wave unless GC can fire)")
+  ap.add_argument("--az-overlap", type=int, default=1,
+                  help="az: stage step k+1's host work (root replay, Dirichlet draws; "
+                       "os_az_stage) on a worker thread while step k searches (1), or "
+                       "prepare each step serially (0)")
   ap.add_argument("--az-requests", default="fused", choices=("fused", "separate"),
                   help="az: one evaluator round per simulation (pure evaluator) or "
                        "the reference's separate Prior / Evaluate rounds")
@@ -704,12 +708,35 @@ def bench_az(args, ctx, layout):
     parity = {"roots_checked": pr, "evaluator": "exact toy (tests/test_az.py)",
               "bit_exact": not bad, "mismatch_fields": bad}
 
+  stage_kw = dict(puct=True, max_simulations=sims, uct_c=c, dirichlet_alpha=alpha,
+                  dirichlet_epsilon=eps, block_size=args.block)
+  pool = None
+  pending = []
+  if args.az_overlap:
+    # Step k's batch was staged (host work: root replay, Dirichlet draws)
+    # while step k-1 searched; step k stages step k+1's the same way.  The
+    # first batch is staged before the warmup, the last staged batch is
+    # never run (its host work is still inside the timed region).
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=1)
+    search.stage(acts, offs, seeds, **stage_kw)
+
+  def stage_next():
+    pending.append(pool.submit(search.stage, acts, offs, seeds, **stage_kw))
+
   def step():
-    search.run(acts, offs, seeds, net, graph=args.az_graph, **kw)
+    if pool is None:
+      search.run(acts, offs, seeds, net, graph=args.az_graph, **kw)
+      return
+    search.run(acts, offs, seeds, net, graph=args.az_graph, staged=True,
+               after_prepare=stage_next, **kw)
+    pending.pop().result()  # the next batch is staged
 
   for _ in range(args.warmup):
     step()
   elapsed, _ = ctx.timed(step, args.steps)
+  if pool is not None:
+    pool.shutdown()
   # One more instrumented run: per-launch k_az_step time and the tree stats.
   search.run(acts, offs, seeds, net, time_steps=True, **kw)
   step_ms = search.step_ms()
@@ -750,6 +777,8 @@ def bench_az(args, ctx, layout):
                         "searches_per_wave": 1 if search.eng_az_wave() else (args.block or 64),
                         "evaluator_requests": args.az_requests,
                         "rounds": "hip graph replay" if args.az_graph else "eager",
+                        "host_prepare": ("staged on a worker thread during the previous "
+                                         "step's search" if args.az_overlap else "serial"),
                         "sims_per_step_per_gpu": sims_step,
                         "units_per_launch": requests / max(launches, 1)})
   line["az"] = {"launches_per_step": launches, "requests_per_step": requests,

@@ -230,7 +230,10 @@ int os_engine_set_rollout_layout(os_engine* e, int32_t layout);
  * dirichlet_epsilon, mcts.h:152-159; dirichlet_noise mcts.cc:177-192, used at
  * :265-273); alpha = 0 disables it.  Noise with a memory budget small enough
  * for GC to fire (the root could be re-expanded) is OS_ERR_UNSUPPORTED.
- * All five games (go's superko set travels in the continuation); C++ policy. */
+ * All five games (go's superko set travels in the continuation).  p->policy
+ * OS_POLICY_CPP: the C++ MCTSBot; OS_POLICY_NUMPY: python/algorithms/mcts.py
+ * (RandomState.shuffle expansions, no single-child stop, no GC; its root
+ * noise comes from the caller through os_az_set_noise, alpha must be 0). */
 int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
                   const int64_t* root_actions, const int64_t* root_offsets,
                   const uint32_t* bot_seeds, double dirichlet_alpha,
@@ -251,6 +254,21 @@ int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,
                            uint8_t* dev_legal, const double* dev_prior, const double* dev_value,
                            int32_t* dev_pending);
 int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos);
+/* os_az_prepare in two halves, so a batch's host work overlaps the device
+ * work of the batch before it.  os_az_stage does only host work (no HIP call:
+ * it replays the roots into their device records and draws the root noise)
+ * into the engine's staging area; it may run on another host thread while
+ * os_az_step_async / os_az_fetch drive the engine's current batch, but not
+ * concurrently with another os_az_stage or os_az_prepare*.
+ * os_az_prepare_staged then uploads the staged batch and binds the request /
+ * response buffers: the same batch os_az_prepare(the staged arguments) would
+ * prepare.  C++ policy, seeded bots. */
+int os_az_stage(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
+                const int64_t* root_actions, const int64_t* root_offsets,
+                const uint32_t* bot_seeds, double dirichlet_alpha, double dirichlet_epsilon);
+int os_az_prepare_staged(os_engine* e, int32_t* dev_kind, float* dev_obs, uint8_t* dev_legal,
+                         const double* dev_prior, const double* dev_value,
+                         int32_t* dev_pending);
 /* Request mode of the next os_az_prepare*.  OS_AZ_REQUESTS_SEPARATE (default)
  * asks exactly what the reference MCTSBot asks, when it asks it: Prior at an
  * expansion, Evaluate at a leaf -- two evaluator rounds per simulation.

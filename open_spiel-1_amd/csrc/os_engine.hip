@@ -492,10 +492,66 @@ struct Stager {
   }
 };
 
+// Host side of a batch's roots: every history replayed into its device
+// state record (+ go's hash set); `nlegal` (optional): each root's
+// |LegalActions|.  Host-only (no HIP call), so os_az_stage can run it while
+// the device works on another batch.
+int ReplayRoots(const os_engine* e, int64_t R, const int64_t* root_actions,
+                const int64_t* root_offsets, std::vector<unsigned char>* roots,
+                std::vector<uint64_t>* rh, std::vector<int32_t>* rnh,
+                std::vector<int32_t>* nlegal = nullptr) {
+  const GameCfg& cfg = e->game.cfg;
+  const int sb = e->game.state_bytes;
+  const bool go = cfg.kind == kGo;
+  const int64_t hs_stride = go ? cfg.max_game_length + 2 : 1;
+  roots->assign(static_cast<size_t>(std::max<int64_t>(R, 1)) * sb, 0);
+  rh->clear();
+  rnh->clear();
+  if (go) {
+    rh->assign(static_cast<size_t>(std::max<int64_t>(R, 1)) * hs_stride, 0);
+    rnh->assign(std::max<int64_t>(R, 1), 0);
+  }
+  if (nlegal) nlegal->assign(std::max<int64_t>(R, 1), 0);
+  return ParallelChunks(R, 1024, [&](int64_t lo, int64_t hi) {
+    std::vector<int64_t> la;
+    for (int64_t r = lo; r < hi; ++r) {
+      HostState hs;
+      std::string err;
+      if (!ReplayRoot(e->game, root_actions + root_offsets[r],
+                      root_offsets[r + 1] - root_offsets[r], &hs, &err))
+        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
+      if (StateTerminal(hs))
+        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
+      if (StateIsChance(hs))  // a bot is only asked to move at decision nodes
+        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is a chance node");
+      std::memcpy(roots->data() + r * sb, hs.raw, sb);
+      if (go) {
+        const int64_t nh = static_cast<int64_t>(hs.hashes.size());
+        if (nh > hs_stride) return Fail(OS_ERR_CAPACITY, "go hash history too long");
+        std::memcpy(rh->data() + r * hs_stride, hs.hashes.data(), nh * 8);
+        (*rnh)[r] = static_cast<int32_t>(nh);
+      }
+      if (nlegal) {
+        StateLegal(hs, &la);
+        (*nlegal)[r] = static_cast<int32_t>(la.size());
+      }
+    }
+    return 0;
+  });
+}
+
+// A batch's replayed roots, handed to Prepare instead of the histories.
+struct PreRoots {
+  const std::vector<unsigned char>* roots;
+  const std::vector<uint64_t>* rh;
+  const std::vector<int32_t>* rnh;
+};
+
 // Uploads roots / seeds, sizes and allocates the arena and outputs.
 int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
             const int64_t* root_actions, const int64_t* root_offsets,
-            const uint32_t* bot_seeds, const uint32_t* eval_seeds, bool search = true) {
+            const uint32_t* bot_seeds, const uint32_t* eval_seeds, bool search = true,
+            const PreRoots* pre = nullptr) {
   int rc = CheckParams(e, p, search);
   if (rc) return rc;
   if (R < 0) return Fail(OS_ERR_INVALID, "num_roots < 0");
@@ -516,37 +572,18 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
 
   // Root states (+ go hash sets) on the host.
   const int sb = e->game.state_bytes;
-  std::vector<unsigned char> roots(static_cast<size_t>(std::max<int64_t>(R, 1)) * sb);
   const bool go = cfg.kind == kGo;
   e->hash_stride = go ? cfg.max_game_length + 2 : 1;
-  std::vector<uint64_t> rh;
-  std::vector<int32_t> rnh;
-  if (go) {
-    rh.assign(static_cast<size_t>(std::max<int64_t>(R, 1)) * e->hash_stride, 0);
-    rnh.assign(std::max<int64_t>(R, 1), 0);
+  std::vector<unsigned char> own_roots;
+  std::vector<uint64_t> own_rh;
+  std::vector<int32_t> own_rnh;
+  if (!pre) {
+    if ((rc = ReplayRoots(e, R, root_actions, root_offsets, &own_roots, &own_rh, &own_rnh)))
+      return rc;
   }
-  rc = ParallelChunks(R, 1024, [&](int64_t lo, int64_t hi) {
-    for (int64_t r = lo; r < hi; ++r) {
-      HostState hs;
-      std::string err;
-      if (!ReplayRoot(e->game, root_actions + root_offsets[r],
-                      root_offsets[r + 1] - root_offsets[r], &hs, &err))
-        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + ": " + err);
-      if (StateTerminal(hs))
-        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is terminal");
-      if (StateIsChance(hs))  // a bot is only asked to move at decision nodes
-        return Fail(OS_ERR_INVALID, "root " + std::to_string(r) + " is a chance node");
-      std::memcpy(roots.data() + r * sb, hs.raw, sb);
-      if (go) {
-        const int64_t nh = static_cast<int64_t>(hs.hashes.size());
-        if (nh > e->hash_stride) return Fail(OS_ERR_CAPACITY, "go hash history too long");
-        std::memcpy(rh.data() + r * e->hash_stride, hs.hashes.data(), nh * 8);
-        rnh[r] = static_cast<int32_t>(nh);
-      }
-    }
-    return 0;
-  });
-  if (rc) return rc;
+  const std::vector<unsigned char>& roots = pre ? *pre->roots : own_roots;
+  const std::vector<uint64_t>& rh = pre ? *pre->rh : own_rh;
+  const std::vector<int32_t>& rnh = pre ? *pre->rnh : own_rnh;
   const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
   if ((rc = e->d_roots.ensure(Rz * sb))) return rc;
   if ((rc = e->d_bseed.ensure(Rz * 4)) || (rc = e->d_eseed.ensure(Rz * 4))) return rc;
@@ -883,11 +920,35 @@ int SpFetch(os_engine* e, int64_t* actions, int32_t* length, double* returns,
 
 // bot_keys / bot_pos (both or neither): each search continues a bot rng_
 // held in numpy's (key[624], pos) form instead of seeding one.
+// Dirichlet root noise of a batch (os_az.h): per root, the normalised
+// std::gamma_distribution draws of a fresh MCTSBot(seed) -- or of the stream
+// (keys, pos) -- over its nlegal[r] legal actions, and the words they took.
+int DrawRootNoise(const os_engine* e, int64_t R, const std::vector<int32_t>& nlegal,
+                  const uint32_t* bot_seeds, const uint32_t* bot_keys, const int32_t* bot_pos,
+                  double alpha, std::vector<double>* noise, std::vector<int32_t>* skip) {
+  const int mc = e->game.cfg.max_children;
+  const size_t Rz = static_cast<size_t>(std::max<int64_t>(R, 1));
+  noise->assign(Rz * mc, 0.0);
+  skip->assign(Rz, 0);
+  return ParallelChunks(R, 512, [&](int64_t lo, int64_t hi) {
+    for (int64_t r = lo; r < hi; ++r) {
+      const int64_t w =
+          bot_keys ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r], nlegal[r], alpha,
+                                         noise->data() + r * mc)
+                   : DirichletNoise(bot_seeds[r], nlegal[r], alpha, noise->data() + r * mc);
+      if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
+      (*skip)[r] = static_cast<int32_t>(w);
+    }
+    return 0;
+  });
+}
+
 int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
               const int64_t* root_actions, const int64_t* root_offsets,
               const uint32_t* bot_seeds, double alpha, double eps, int32_t* kind, float* obs,
               uint8_t* legal, const double* prior, const double* value, int32_t* pending,
-              const uint32_t* bot_keys = nullptr, const int32_t* bot_pos = nullptr) {
+              const uint32_t* bot_keys = nullptr, const int32_t* bot_pos = nullptr,
+              const os_engine::AzStaged* stg = nullptr) {
   if (!p) return Fail(OS_ERR_INVALID, "null params");
   const bool import = bot_keys != nullptr;
   std::vector<uint32_t> zero_seeds;
@@ -915,8 +976,21 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   q.n_rollouts = 2;  // f64 node rewards (Node<double>): values are not integral
   q.child_selection = OS_SELECT_UCT;  // `puct` selects; the LUT stays log(N)
   q.layout = OS_LAYOUT_LANE;
-  int rc = Prepare(e, &q, R, root_actions, root_offsets, bot_seeds, bot_seeds,
-                   /*search=*/false);  // buffers only: k_az_step runs the search
+  // The roots' host work: replayed once (records, go hash sets, legal counts
+  // for the noise), or taken from os_az_stage.
+  int rc = CheckParams(e, &q, false);
+  if (rc) return rc;
+  if (R < 0) return Fail(OS_ERR_INVALID, "num_roots < 0");
+  std::vector<unsigned char> own_roots;
+  std::vector<uint64_t> own_rh;
+  std::vector<int32_t> own_rnh, nlegal;
+  if (!stg && (rc = ReplayRoots(e, R, root_actions, root_offsets, &own_roots, &own_rh, &own_rnh,
+                                alpha > 0.0 ? &nlegal : nullptr)))
+    return rc;
+  const PreRoots pre = stg ? PreRoots{&stg->roots, &stg->rh, &stg->rnh}
+                           : PreRoots{&own_roots, &own_rh, &own_rnh};
+  rc = Prepare(e, &q, R, root_actions, root_offsets, bot_seeds, bot_seeds,
+               /*search=*/false, &pre);  // buffers only: k_az_step runs the search
   if (rc) return rc;
   if (e->chunk_roots < R)
     return Fail(OS_ERR_CAPACITY, "external-evaluator searches must all fit in HBM at once");
@@ -943,29 +1017,13 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     if (max_nodes > 1 && worst >= max_nodes)
       return Fail(OS_ERR_UNSUPPORTED,
                   "Dirichlet noise with a max_memory_mb small enough for GC to fire");
-    const int mc = e->game.cfg.max_children;
-    std::vector<double> noise(Rz * mc, 0.0);
-    std::vector<int32_t> skip(Rz, 0);
-    rc = ParallelChunks(R, 512, [&](int64_t lo, int64_t hi) {
-      std::vector<int64_t> acts;
-      for (int64_t r = lo; r < hi; ++r) {
-        HostState hs;
-        std::string err;
-        ReplayRoot(e->game, root_actions + root_offsets[r],
-                   root_offsets[r + 1] - root_offsets[r], &hs, &err);
-        StateLegal(hs, &acts);
-        const int64_t w =
-            import ? DirichletNoiseState(bot_keys + r * kMtN, bot_pos[r],
-                                         static_cast<int>(acts.size()), alpha,
-                                         noise.data() + r * mc)
-                   : DirichletNoise(bot_seeds[r], static_cast<int>(acts.size()), alpha,
-                                    noise.data() + r * mc);
-        if (w > 0x7FFFFFFF) return Fail(OS_ERR_CAPACITY, "Dirichlet draw too long");
-        skip[r] = static_cast<int32_t>(w);
-      }
-      return 0;
-    });
-    if (rc) return rc;
+    std::vector<double> own_noise;
+    std::vector<int32_t> own_skip;
+    if (!stg && (rc = DrawRootNoise(e, R, nlegal, bot_seeds, import ? bot_keys : nullptr,
+                                    bot_pos, alpha, &own_noise, &own_skip)))
+      return rc;
+    const std::vector<double>& noise = stg ? stg->noise : own_noise;
+    const std::vector<int32_t>& skip = stg ? stg->skip : own_skip;
     if ((rc = e->d_az_noise.ensure(noise.size() * 8)) || (rc = e->d_az_skip.ensure(Rz * 4)))
       return rc;
     HIP_TRY(hipMemcpy(e->d_az_noise.p, noise.data(), noise.size() * 8, hipMemcpyHostToDevice));
@@ -1525,6 +1583,53 @@ int os_az_prepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t n
   return AzPrepare(e, p, puct, num_roots, root_actions, root_offsets, bot_seeds,
                    dirichlet_alpha, dirichlet_epsilon, dev_kind, dev_obs, dev_legal, dev_prior,
                    dev_value, dev_pending);
+}
+
+int os_az_stage(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t num_roots,
+                const int64_t* root_actions, const int64_t* root_offsets,
+                const uint32_t* bot_seeds, double dirichlet_alpha, double dirichlet_epsilon) {
+  if (!e || !p) return Fail(OS_ERR_INVALID, "null argument");
+  if (num_roots < 0 || (num_roots > 0 && (!root_offsets || !bot_seeds)))
+    return Fail(OS_ERR_INVALID, "bad batch");
+  if (p->policy != OS_POLICY_CPP)
+    return Fail(OS_ERR_UNSUPPORTED, "os_az_stage: C++-policy batches (seeded bots)");
+  if (!(dirichlet_alpha >= 0.0) || !(dirichlet_epsilon >= 0.0) || dirichlet_epsilon > 1.0)
+    return Fail(OS_ERR_INVALID, "dirichlet_alpha must be >= 0 and epsilon in [0, 1]");
+  os_engine::AzStaged& st = e->az_staged;
+  st.ready = false;
+  const int64_t R = num_roots;
+  st.p = *p;
+  st.puct = puct;
+  st.R = R;
+  st.alpha = dirichlet_alpha;
+  st.eps = dirichlet_epsilon;
+  st.offs.assign(root_offsets, root_offsets + R + 1);
+  st.acts.assign(root_actions, root_actions + (R > 0 ? root_offsets[R] : 0));
+  st.seeds.assign(bot_seeds, bot_seeds + R);
+  std::vector<int32_t> nlegal;
+  int rc = ReplayRoots(e, R, st.acts.data(), st.offs.data(), &st.roots, &st.rh, &st.rnh,
+                       dirichlet_alpha > 0.0 ? &nlegal : nullptr);
+  if (rc) return rc;
+  st.noise.clear();
+  st.skip.clear();
+  if (dirichlet_alpha > 0.0 &&
+      (rc = DrawRootNoise(e, R, nlegal, st.seeds.data(), nullptr, nullptr, dirichlet_alpha,
+                          &st.noise, &st.skip)))
+    return rc;
+  st.ready = true;
+  return OS_OK;
+}
+
+int os_az_prepare_staged(os_engine* e, int32_t* dev_kind, float* dev_obs, uint8_t* dev_legal,
+                         const double* dev_prior, const double* dev_value,
+                         int32_t* dev_pending) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  os_engine::AzStaged& st = e->az_staged;
+  if (!st.ready) return Fail(OS_ERR_INVALID, "no os_az_stage batch");
+  st.ready = false;  // consumed
+  return AzPrepare(e, &st.p, st.puct, st.R, st.acts.data(), st.offs.data(), st.seeds.data(),
+                   st.alpha, st.eps, dev_kind, dev_obs, dev_legal, dev_prior, dev_value,
+                   dev_pending, nullptr, nullptr, &st);
 }
 
 int os_az_prepare_stateful(os_engine* e, const os_mcts_params* p, int32_t puct,

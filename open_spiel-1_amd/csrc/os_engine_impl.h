@@ -328,6 +328,22 @@ struct os_engine {
   bool az_ready = false;
   int32_t az_puct = 0;
   int32_t az_np = 0;  // OS_POLICY_NUMPY external-evaluator batch
+  // os_az_stage: the host work of the NEXT os_az_prepare_staged batch, done
+  // ahead (inputs, replayed root records + go hash sets, root noise).
+  struct AzStaged {
+    bool ready = false;
+    os_mcts_params p{};
+    int32_t puct = 0;
+    int64_t R = 0;
+    double alpha = 0.0, eps = 0.0;
+    std::vector<int64_t> acts, offs;
+    std::vector<uint32_t> seeds;
+    std::vector<unsigned char> roots;
+    std::vector<uint64_t> rh;
+    std::vector<int32_t> rnh;
+    std::vector<double> noise;
+    std::vector<int32_t> skip;
+  } az_staged;
   int32_t* az_kind = nullptr;
   float* az_obs = nullptr;
   uint8_t* az_legal = nullptr;

@@ -177,6 +177,9 @@ _sig("os_az_heads_async", ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _vp, 
 _sig("os_az_set_requests", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_az_set_layout", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_az_get_layout", ctypes.c_int, [_vp, _P])
+_sig("os_az_stage", ctypes.c_int, [_vp, ctypes.POINTER(MctsParams), _i32, _i64, _P, _P, _P,
+                                   ctypes.c_double, ctypes.c_double])
+_sig("os_az_prepare_staged", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp])
 _sig("os_az_set_noise", ctypes.c_int, [_vp, _P, _i64, ctypes.c_double])
 _sig("os_az_tree_priors", ctypes.c_int, [_vp, _i64, _i64, _P])
 AZ_REQUESTS_SEPARATE, AZ_REQUESTS_FUSED = 0, 1

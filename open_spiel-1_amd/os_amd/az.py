@@ -101,7 +101,7 @@ class ExternalEvaluatorSearch:
           max_simulations=100, uct_c=2.0, solve=True, max_memory_mb=1000,
           dirichlet_alpha=0.0, dirichlet_epsilon=0.0, stream=None, time_steps=False,
           bot_rng=None, requests="fused", graph=False, graph_batch=8, block_size=0,
-          layout="auto", policy="cpp", root_noise=None):
+          layout="auto", policy="cpp", root_noise=None, staged=False, after_prepare=None):
     """Runs every search to completion; returns the os_mcts_batch outputs.
 
     The evaluator may be called once more after the last step, with every
@@ -127,6 +127,12 @@ class ExternalEvaluatorSearch:
     draw: pass it as root_noise ([R][>= max_children] float64, root r's j-th
     legal action) with dirichlet_epsilon, and the stream after the draw as
     bot_rng (dirichlet_alpha stays 0; os_az_set_noise).
+
+    staged=True: the batch was staged ahead by `stage()` (its host work done,
+    possibly while the previous batch ran); the staged arguments are used
+    and the ones passed here must describe the same batch.  after_prepare: a
+    callable run once the batch is on the device, before its first step (e.g.
+    one that stages the next batch on a worker thread).
 
     graph=True: after two eager rounds, one round (k_az_step + the evaluator +
     the response copies) is captured into a HIP graph and replayed
@@ -162,7 +168,13 @@ class ExternalEvaluatorSearch:
     if layout not in _LAYOUTS:
       raise ValueError("layout must be 'auto', 'wave' or 'lane'")
     check(lib.os_az_set_layout(self.eng._h, _LAYOUTS[layout]))
-    if bot_rng is None:
+    if staged:
+      if bot_rng is not None or root_noise is not None:
+        raise ValueError("staged batches are seeded C++-policy batches")
+      check(lib.os_az_prepare_staged(self.eng._h, kind.data_ptr(), obs.data_ptr(),
+                                     legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
+                                     pending.data_ptr()))
+    elif bot_rng is None:
       bs = _lib.u32(bot_seeds)
       check(lib.os_az_prepare(self.eng._h, ctypes.byref(p), 1 if puct else 0, R, ptr(acts),
                               ptr(offs), ptr(bs), float(dirichlet_alpha),
@@ -182,6 +194,8 @@ class ExternalEvaluatorSearch:
       if rn.ndim != 2 or rn.shape[0] != R or rn.shape[1] < self.eng.max_children:
         raise ValueError("root_noise must be [R][>= max_children]")
       check(lib.os_az_set_noise(self.eng._h, ptr(rn), rn.shape[1], float(dirichlet_epsilon)))
+    if after_prepare is not None:
+      after_prepare()
     # the kernel the engine chose (AUTO: wave unless GC can fire)
     lay = np.zeros(1, np.int32)
     check(lib.os_az_get_layout(self.eng._h, ptr(lay)))
@@ -256,6 +270,22 @@ class ExternalEvaluatorSearch:
           break
     st.synchronize()
     self.requests += int(total.item())
+
+  def stage(self, root_actions, root_offsets, bot_seeds, puct=True, max_simulations=100,
+            uct_c=2.0, solve=True, max_memory_mb=1000, dirichlet_alpha=0.0,
+            dirichlet_epsilon=0.0, block_size=0):
+    """The host half of the next run(staged=True) (os_az_stage): roots
+    replayed, root noise drawn; no device call, so it may run on another
+    thread while this search's current batch runs (ctypes releases the GIL)."""
+    p = E.make_params(uct_c=uct_c, max_simulations=max_simulations,
+                      max_memory_mb=max_memory_mb, solve=solve, block_size=block_size)
+    acts = _lib.i64(root_actions)
+    offs = _lib.i64(root_offsets)
+    bs = _lib.u32(bot_seeds)
+    self._stage_keep = (p, acts, offs, bs)
+    check(lib.os_az_stage(self.eng._h, ctypes.byref(p), 1 if puct else 0, len(offs) - 1,
+                          ptr(acts), ptr(offs), ptr(bs), float(dirichlet_alpha),
+                          float(dirichlet_epsilon)))
 
   def tree(self, r=0):
     """Search r's tree after run(): os_engine_tree's flat arrays plus the

@@ -434,3 +434,39 @@ def test_heads_abi_rejects_bad_shapes():
   assert L.os_az_heads_async(None, 0, 4, 7, 7, None, None, None, None) != 0  # ld < A + 1
   assert L.os_az_heads_async(None, 2, 4, 7, 8, None, None, None, None) != 0  # dtype
   assert L.os_az_heads_async(None, 0, 4, 7, 8, None, None, None, None) != 0  # null buffers
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("game", ["connect_four", "go(board_size=5)"])
+def test_gpu_staged_batch_matches_oracle(require_gpu, game):
+  """os_az_stage (host half, run on a worker thread while the previous batch
+  searches) + os_az_prepare_staged == os_az_prepare: the bench's overlapped
+  az step."""
+  from concurrent.futures import ThreadPoolExecutor
+  from os_amd.az import ExternalEvaluatorSearch
+  og = oracle_lib.Game(game)
+  A = og.num_distinct_actions
+  R, sims = 96, 24
+  acts, offs = E.make_roots(game, R, seed_base=11, max_plies=4)
+  seeds = np.arange(R, dtype=np.uint32) * 5 + 2
+  kw = dict(puct=True, uct_c=1.25, max_simulations=sims, dirichlet_alpha=1.0,
+            dirichlet_epsilon=0.25)
+  ref = og.mcts_external(acts, offs, seeds, _oracle_eval_fn(game), max_children=A, **kw)
+  search = ExternalEvaluatorSearch(game)
+  ev = _gpu_toy_evaluator(A)
+  search.stage(acts, offs, seeds, **kw)
+  pool = ThreadPoolExecutor(max_workers=1)
+  futs = []
+  for _ in range(2):  # the second batch was staged while the first ran
+    got = search.run(acts, offs, seeds, ev, staged=True,
+                     after_prepare=lambda: futs.append(pool.submit(search.stage, acts, offs,
+                                                                   seeds, **kw)), **kw)
+    futs.pop().result()
+    mc = search.eng.max_children
+    for k in E.OUTPUT_KEYS:
+      r = ref[k][:, :mc] if ref[k].ndim == 2 else ref[k]
+      np.testing.assert_array_equal(got[k], r, err_msg=k)
+  pool.shutdown()
+  with pytest.raises(RuntimeError):  # a staged batch is consumed once
+    search.run(acts, offs, seeds, ev, staged=True, **kw)
+    search.run(acts, offs, seeds, ev, staged=True, **kw)
