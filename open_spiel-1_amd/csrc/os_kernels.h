@@ -387,7 +387,19 @@ struct WaveOcc<Hex> {
 // kPaged: the search may take pages from the pool (os_wave.h kPg*).  The
 // reserved-arena variant is a separate kernel: the cold page-switch path
 // costs the selection loop scalar registers (C2 +1.4% time).
-template <class G, class R, int Policy, bool kPaged, bool kPuct>
+// kLdsTree: the search's whole reserved arena has an LDS copy (NodeCache
+// kCacheAll, written through to HBM), so selection reads every child block
+// from LDS.  For batches of at most one search per CU -- a single bot's step
+// -- of the games whose reserved tree fits the CU's LDS (LdsTreeGame).
+template <class G>
+struct LdsTreeGame : std::false_type {};
+template <>
+struct LdsTreeGame<TicTacToe> : std::true_type {};
+template <>
+struct LdsTreeGame<ConnectFour> : std::true_type {};
+constexpr int64_t kLdsTreeMaxRoots = 256;  // one search per CU
+
+template <class G, class R, int Policy, bool kPaged, bool kPuct, bool kLdsTree = false>
 __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   const int64_t lr = blockIdx.x;
   if (lr >= a.num_roots) return;
@@ -435,10 +447,12 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
   if constexpr (std::is_same<G, Go>::value) ctx.sub = ph.c;
 #endif
   SearchResult res = shared
-      ? wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE, OS_PACE != 0>(
-            a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path, a.path_cap, ph, lcache)
-      : wave_search<G, R, Policy, kPaged, kPuct, OS_NODE_CACHE, OS_PACE != 0>(
-            a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path, a.path_cap, ph, lcache);
+      ? wave_search<G, R, Policy, kPaged, kPuct, kLdsTree ? kCacheAll : OS_NODE_CACHE,
+                    OS_PACE != 0>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
+                                  a.path_cap, ph, lcache)
+      : wave_search<G, R, Policy, kPaged, kPuct, kLdsTree ? kCacheAll : OS_NODE_CACHE,
+                    OS_PACE != 0>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                                  a.path_cap, ph, lcache);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
   ph.c[kPhTwist] = bot.twist_cycles + (shared ? 0u : ev.twist_cycles);
@@ -1807,10 +1821,38 @@ size_t LdsPerLane(int path_cap, int child_cap) {
          static_cast<size_t>(child_cap) * 2;
 }
 
+template <class G, class R, int Policy, bool kPuct>
+int LaunchWaveLdsTree(os_engine* e, DevArgs a, hipStream_t stream, size_t lds) {
+  if constexpr (LdsTreeGame<G>::value) {
+    auto kfn = &k_wsearch<G, R, Policy, false, kPuct, true>;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(lds)));
+    a.root_base = 0;
+    hipLaunchKernelGGL(kfn, dim3(static_cast<unsigned>(a.num_roots)), dim3(64), lds, stream, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess)
+      return Fail(OS_ERR_DEVICE, std::string("k_wsearch launch failed: ") +
+                                     hipGetErrorString(err));
+    return OS_OK;
+  } else {
+    (void)e; (void)a; (void)stream; (void)lds;
+    return Fail(OS_ERR_UNSUPPORTED, "no LDS-tree kernel for this game");
+  }
+}
+
 template <class G, class R, int Policy>
 int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   const size_t lds = WaveLdsBytes<G, R>(a.path_cap);
   if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
+  // A small batch of a small game: the whole tree in LDS (kLdsTree).
+  if (LdsTreeGame<G>::value && a.pages == nullptr && e->num_roots <= kLdsTreeMaxRoots &&
+      e->chunk_roots >= e->num_roots && OS_NODE_CACHE == 0) {
+    const size_t tree_lds = ((lds + 15) & ~size_t(15)) + static_cast<size_t>(a.cap) * sizeof(Node<R>);
+    if (tree_lds <= kLdsBytes)
+      return a.sp.puct ? LaunchWaveLdsTree<G, R, Policy, true>(e, a, stream, tree_lds)
+                       : LaunchWaveLdsTree<G, R, Policy, false>(e, a, stream, tree_lds);
+  }
   // Paged batches run the C++ policy only (SizeArena).
   constexpr bool kCanPage = Policy == kPolicyCpp;
   const bool paged = kCanPage && a.pages != nullptr;

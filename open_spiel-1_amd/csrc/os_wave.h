@@ -2077,19 +2077,26 @@ struct LanePath {
 // tree's top levels, which every simulation walks: selection reads a child
 // block that lies wholly below kCache from LDS instead of HBM / MALL.  Every
 // store to such a node is written through to both copies.
+// K = kCacheAll (-1): the whole arena is in LDS (k_wsearch kLdsTree: a small
+// batch whose reserved tree fits the CU's LDS), `k` = the arena's capacity,
+// so every block is an LDS block.
+constexpr int kCacheAll = -1;
 template <class R, int K>
 struct NodeCache {
   Node<R>* c;
-  __device__ __forceinline__ bool has(uint32_t i) const { return K > 0 && i < static_cast<uint32_t>(K); }
+  uint32_t k;
+  __device__ __forceinline__ bool has(uint32_t i) const {
+    return K == kCacheAll || (K > 0 && i < static_cast<uint32_t>(K));
+  }
   __device__ __forceinline__ bool block(uint32_t first, int n) const {
-    return K > 0 && first + static_cast<uint32_t>(n) <= static_cast<uint32_t>(K);
+    return K == kCacheAll || (K > 0 && first + static_cast<uint32_t>(n) <= static_cast<uint32_t>(K));
   }
 };
 
 // One search, executed by the whole wave.  `path` (LDS) has path_cap
 // entries.  Same contract as mcts_search; kPuct selects children by
 // PUCTValue (sp.log_lut then holds sqrt(N)); kCache > 0: `lcache` (LDS)
-// holds the first kCache nodes (NodeCache).
+// holds the first kCache nodes (NodeCache); kCache == kCacheAll: all `cap`.
 template <class G, class R, int Policy, bool kPageable = false, bool kPuct = false,
           int kCache = 0, bool kPace = false, class C>
 __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
@@ -2098,7 +2105,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     WaveMt& ev, PathEnt<R>* path, int path_cap,
                                     PhaseCycles& ph, Node<R>* lcache = nullptr) {
   const int l = lane_id();
-  const NodeCache<R, kCache> nc_ = {lcache};
+  const NodeCache<R, kCache> nc_ = {lcache, cap};
   const uint64_t t_begin = OS_PH_NOW();
   SearchResult res;
   res.status = kOk;
@@ -2120,7 +2127,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     nodes[0].action = 0;
     nodes[0].nchild = 0;
     nodes[0].out = kUnsolved;
-    if (kCache > 0) nc_.c[0] = nodes[0];
+    if (kCache != 0) nc_.c[0] = nodes[0];
   }
   // Root statistics persist in registers across simulations.
   uint32_t root_first = 0;
@@ -2536,7 +2543,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
       if (!kLP && l == 0) {
         nodes[0].n = root_n;
         nodes[0].w = root_w;
-        if (kCache > 0) {
+        if (kCache != 0) {
           nc_.c[0].n = root_n;
           nc_.c[0].w = root_w;
         }
@@ -2626,8 +2633,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
                                     (nodes_count > sp.max_nodes / 2 ? 1.25 : 0.9));
         if (gc_limit < 5) gc_limit = 5;
         __threadfence_block();
-        if (kCache > 0) {  // GC rewrote nchild fields: refresh the LDS copy
-          for (int i = l; i < kCache && i < static_cast<int>(used); i += 64) nc_.c[i] = nodes[i];
+        if (kCache != 0) {  // GC rewrote nchild fields: refresh the LDS copy
+          const int lim = kCache == kCacheAll ? static_cast<int>(cap) : kCache;
+          for (int i = l; i < lim && i < static_cast<int>(used); i += 64) nc_.c[i] = nodes[i];
           __builtin_amdgcn_wave_barrier();
         }
         root_nc = nodes[0].nchild;
