@@ -289,6 +289,12 @@ int os_az_set_layout(os_engine* e, int32_t layout);
 /* The kernel the last os_az_prepare* chose (OS_LAYOUT_WAVE or OS_LAYOUT_LANE),
  * AUTO resolved by the engine's own rule. */
 int os_az_get_layout(os_engine* e, int32_t* layout);
+/* Measurement: with timing on, every search run of the engine (the batch,
+ * stateful and rerun paths) is bracketed by a HIP event pair on its stream;
+ * os_engine_last_run_ms waits for the last one and returns its duration, so
+ * a caller can time a whole bot step and the kernel inside it in one run. */
+int os_engine_set_run_timing(os_engine* e, int32_t on);
+int os_engine_last_run_ms(os_engine* e, double* ms);
 /* Root Dirichlet noise drawn by the CALLER, for the batch of the last
  * os_az_prepare*: noise[r * stride + j] pairs with root r's j-th legal action
  * (ascending), mixed at the root's expansion as (1 - eps) * prior + eps *

@@ -640,7 +640,17 @@ int Run(os_engine* e, hipStream_t stream) {
   const GameLaunchers* L = LaunchersFor(e->game.cfg);
   if (!L) return Fail(OS_ERR_UNSUPPORTED, "unknown game kind");
   if (e->paged) HIP_TRY(hipMemsetAsync(e->d_page_next.p, 0, 4, stream));
-  return L->search(e, MakeArgs(e), stream);
+  if (!e->time_runs) return L->search(e, MakeArgs(e), stream);
+  // os_engine_set_run_timing: an event pair around the search launches
+  if (!e->run_ev[0]) {
+    HIP_TRY(hipEventCreate(&e->run_ev[0]));
+    HIP_TRY(hipEventCreate(&e->run_ev[1]));
+  }
+  HIP_TRY(hipEventRecord(e->run_ev[0], stream));
+  const int rc = L->search(e, MakeArgs(e), stream);
+  HIP_TRY(hipEventRecord(e->run_ev[1], stream));
+  e->run_timed = rc == OS_OK;
+  return rc;
 }
 
 // A paged batch in which some search ran out of pool pages is run again on
@@ -1651,6 +1661,24 @@ int os_az_set_layout(os_engine* e, int32_t layout) {
   if (layout != OS_LAYOUT_WAVE && layout != OS_LAYOUT_LANE && layout != OS_LAYOUT_AUTO)
     return Fail(OS_ERR_INVALID, "unknown layout");
   e->az_layout = layout;
+  return OS_OK;
+}
+
+int os_engine_set_run_timing(os_engine* e, int32_t on) {
+  if (!e) return Fail(OS_ERR_INVALID, "null engine");
+  e->time_runs = on != 0;
+  e->run_timed = false;
+  return OS_OK;
+}
+
+int os_engine_last_run_ms(os_engine* e, double* ms) {
+  if (!e || !ms) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->run_timed) return Fail(OS_ERR_INVALID, "no timed run (os_engine_set_run_timing)");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipEventSynchronize(e->run_ev[1]));
+  float f = 0.0f;
+  HIP_TRY(hipEventElapsedTime(&f, e->run_ev[0], e->run_ev[1]));
+  *ms = f;
   return OS_OK;
 }
 

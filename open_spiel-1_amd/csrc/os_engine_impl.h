@@ -387,6 +387,10 @@ struct os_engine {
   const void* lut_at = nullptr;
   const void* zob_at = nullptr;
   osx::PinBuf h_stage;
+  // os_engine_set_run_timing: HIP events around each search launch
+  bool time_runs = false;
+  bool run_timed = false;
+  hipEvent_t run_ev[2] = {nullptr, nullptr};
   int64_t arena_reruns = 0;     // batches rerun on the reserved arena
   int64_t arena_overflows = 0;  // searches that ran out of pool pages
   ~os_engine() {
@@ -401,6 +405,8 @@ struct os_engine {
     (void)hipSetDevice(device);
     for (osx::DevBuf* b : all) b->release();
     h_stage.release();
+    for (hipEvent_t& ev : run_ev)
+      if (ev) (void)hipEventDestroy(ev);
   }
 };
 

@@ -5,9 +5,10 @@ For each game, from the initial position, at the reference's simulation
 count (1000, python/examples/mcts.py and SURVEY §8d C1):
   cpp_step_ms     pyspiel.MCTSBot.step (C++ MCTSBot semantics), wall
   py_step_ms      open_spiel.python.algorithms.mcts.MCTSBot.step (numpy), wall
-  kernel_ms       the same search's device time alone: os_engine_run_async
-                  bracketed by HIP events on the launch stream
-  host_overhead   cpp_step_ms - kernel_ms, and its fraction of kernel_ms
+  kernel_ms       the device time of the search inside each timed step: the
+                  engine brackets its launch with HIP events
+                  (os_engine_set_run_timing), read after the step returns
+  host_overhead   median over reps of (step - that step's kernel time)
   oracle_1core_ms the oracle MCTSBot (reference-faithful restatement of
                   mcts.cc) for the same search on one host core
 Writes JSON + a markdown table to --out (default profiles/r04/step_latency).
@@ -60,51 +61,37 @@ def measure(gs, sims, reps, torch):
     return mcts.MCTSBot(game, 2.0, sims, mcts.RandomRolloutEvaluator(1, rs), random_state=rs,
                         solve=True, backend="hip")
 
-  def first_step_ms(make):
-    ts = []
+  acts = np.array(hist, np.int64)
+  offs = np.array([0, len(hist)], np.int64)
+  # Step and kernel in the SAME run: the engine the bots drive brackets each
+  # search launch with a HIP event pair (os_engine_set_run_timing); every rep
+  # reads its own step's kernel time after the step returns.
+  from os_amd import _lib
+  eng = pyspiel._engine_for(game)
+  _lib.check(_lib.lib.os_engine_set_run_timing(eng._h, 1))
+  kms = np.zeros(1, np.float64)
+
+  def step_and_kernel(make):
+    steps, kernels = [], []
     for _ in range(reps):
       bot = make()
       t0 = time.perf_counter()
       bot.step(st)
-      ts.append((time.perf_counter() - t0) * 1e3)
-    return float(np.median(ts))
+      steps.append((time.perf_counter() - t0) * 1e3)
+      _lib.check(_lib.lib.os_engine_last_run_ms(eng._h, _lib.ptr(kms)))
+      kernels.append(float(kms[0]))
+    return steps, kernels
 
-  cpp_bot().step(st)
-  cpp_ms = first_step_ms(cpp_bot)
+  cpp_bot().step(st)  # warm the engine and its arena
+  cpp_steps, cpp_kernels = step_and_kernel(cpp_bot)
   py_bot().step(st)
-  py_ms = first_step_ms(py_bot)
-  # the kernel alone: the same search through the device-resident pipeline
-  eng = E.Engine(game.game_string if hasattr(game, "game_string") else gs)
-  acts = np.array(hist, np.int64)
-  offs = np.array([0, len(hist)], np.int64)
-  eng.prepare(acts, offs, [3], [7], uct_c=2.0, max_simulations=sims)
-  stream = torch.cuda.current_stream()
-  ks = []
-  for _ in range(reps + 1):
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    eng.run_async(stream.cuda_stream)
-    e1.record(stream)
-    e1.synchronize()
-    ks.append(e0.elapsed_time(e1))
-  eng.fetch()
-  kernel_ms = float(np.median(ks[1:]))
-  # the numpy-policy search (mcts.MCTSBot's kernel: np.random draws, one stream)
-  from os_amd import _lib
-  eng.prepare(acts, offs, [3], [3], uct_c=2.0, max_simulations=sims, max_memory_mb=0,
-              policy=_lib.POLICY_NUMPY)
-  ks = []
-  for _ in range(reps + 1):
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    eng.run_async(stream.cuda_stream)
-    e1.record(stream)
-    e1.synchronize()
-    ks.append(e0.elapsed_time(e1))
-  eng.fetch()
-  np_kernel_ms = float(np.median(ks[1:]))
+  py_steps, py_kernels = step_and_kernel(py_bot)
+  _lib.check(_lib.lib.os_engine_set_run_timing(eng._h, 0))
+  cpp_ms, kernel_ms = float(np.median(cpp_steps)), float(np.median(cpp_kernels))
+  py_ms, np_kernel_ms = float(np.median(py_steps)), float(np.median(py_kernels))
+  # per-rep host overhead (step - its own kernel), median
+  cpp_over = float(np.median(np.array(cpp_steps) - np.array(cpp_kernels)))
+  py_over = float(np.median(np.array(py_steps) - np.array(py_kernels)))
   # oracle, one core
   og = O.Game(gs)
   osecs = []
@@ -113,10 +100,12 @@ def measure(gs, sims, reps, torch):
                                max_simulations=sims, threads=1)
     osecs.append(s * 1e3)
   return {"game": gs, "sims": sims, "cpp_step_ms": cpp_ms, "py_step_ms": py_ms,
-          "kernel_ms": kernel_ms, "host_overhead_ms": cpp_ms - kernel_ms,
-          "host_overhead_frac": (cpp_ms - kernel_ms) / kernel_ms,
-          "np_kernel_ms": np_kernel_ms, "py_overhead_ms": py_ms - np_kernel_ms,
-          "py_overhead_frac": (py_ms - np_kernel_ms) / np_kernel_ms,
+          "kernel_ms": kernel_ms, "host_overhead_ms": cpp_over,
+          "host_overhead_frac": cpp_over / kernel_ms,
+          "np_kernel_ms": np_kernel_ms, "py_overhead_ms": py_over,
+          "py_overhead_frac": py_over / np_kernel_ms,
+          "cpp_steps_ms": cpp_steps, "cpp_kernels_ms": cpp_kernels,
+          "py_steps_ms": py_steps, "py_kernels_ms": py_kernels,
           "oracle_1core_ms": float(np.median(osecs)),
           "gpu_over_oracle": float(np.median(osecs)) / cpp_ms}
 
@@ -126,7 +115,7 @@ def main():
   ap.add_argument("--sims", type=int, default=1000)
   ap.add_argument("--reps", type=int, default=10)
   ap.add_argument("--games", default=",".join(GAMES))
-  ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04", "step_latency"))
+  ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05", "step_latency"))
   args = ap.parse_args()
   import torch
   torch.cuda.init()
