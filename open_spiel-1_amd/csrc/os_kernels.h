@@ -1829,6 +1829,7 @@ int LaunchWaveLdsTree(os_engine* e, DevArgs a, hipStream_t stream, size_t lds) {
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 static_cast<int>(lds)));
     a.root_base = 0;
+    a.num_roots = e->num_roots;  // one chunk (the caller checked chunk_roots)
     hipLaunchKernelGGL(kfn, dim3(static_cast<unsigned>(a.num_roots)), dim3(64), lds, stream, a);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess)
