@@ -67,7 +67,8 @@ def measure(gs, sims, reps, torch):
   # search launch with a HIP event pair (os_engine_set_run_timing); every rep
   # reads its own step's kernel time after the step returns.
   from os_amd import _lib
-  eng = pyspiel._engine_for(game)
+  from os_amd import pyspiel as ospy
+  eng = ospy._engine_for(game)
   _lib.check(_lib.lib.os_engine_set_run_timing(eng._h, 1))
   kms = np.zeros(1, np.float64)
 
