@@ -986,7 +986,14 @@ __device__ __forceinline__ uint64_t row_scan_or_stride2(uint64_t v) {
 // moves (one DPP row); a pair the table cannot answer (window edge, possible
 // absl rejection) is drawn by the exact serial path as a 1-move run.  Every
 // move, word and outcome is the serial rollout's (tests/test_gpu_parity.py).
-template <class C>
+//
+// Under the numpy policy (RandomState.choice, mcts.py:56-63) a run's draws
+// all test their words against the same mask and bound (n is fixed), so the
+// run's draws are the window's accepted words in order: one ballot marks
+// them, ds_permute sends each accepted word's index to the lane of its rank
+// (the others to the top lanes), and move i reads its word from there; the
+// stream moves past the last draw taken.  n = 1 draws nothing.
+template <int Policy = kPolicyCpp, class C>
 __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
   (void)ctx;
   s = make_uniform(s);
@@ -1031,20 +1038,44 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
   uint64_t b0 = s.bb[0], b1 = s.bb[1];
   for (;;) {
     const int n = popc64(legal);
-    int K = (ev.valid - ev.pos) >> 1;
-    if (K > 16) K = 16;
-    if (K > 42 - moves) K = 42 - moves;
-    uint32_t k;
+    int K;
+    uint32_t k = 0;
     bool serial = false;
-    if (K > 0) {
-      const uint32_t pk = static_cast<uint32_t>(
-          __builtin_amdgcn_ds_bpermute((ev.pos + 2 * i) << 2, static_cast<int>(ev.pre7)));
-      const uint64_t fl = ballot(l < K && (pk >> 31) != 0);
-      if (fl) K = ctz64(fl);  // lanes before the first unanswerable pair
-      k = (pk >> (3 * (n - 1))) & 7u;
+    uint32_t widx = 0;  // numpy: window index of move i's word (lane i)
+    if constexpr (Policy == kPolicyCpp) {
+      K = (ev.valid - ev.pos) >> 1;
+      if (K > 16) K = 16;
+      if (K > 42 - moves) K = 42 - moves;
+      if (K > 0) {
+        const uint32_t pk = static_cast<uint32_t>(
+            __builtin_amdgcn_ds_bpermute((ev.pos + 2 * i) << 2, static_cast<int>(ev.pre7)));
+        const uint64_t fl = ballot(l < K && (pk >> 31) != 0);
+        if (fl) K = ctz64(fl);  // lanes before the first unanswerable pair
+        k = (pk >> (3 * (n - 1))) & 7u;
+      }
+    } else {
+      K = 42 - moves < 16 ? 42 - moves : 16;
+      if (n > 1) {
+        const uint32_t rng = static_cast<uint32_t>(n - 1), m = np_mask(rng);
+        const bool a = l >= ev.pos && l < ev.valid && (ev.cur & m) <= rng;
+        const uint64_t acc = ballot(a);
+        const int avail = popc64(acc);
+        if (avail < K) K = avail;
+        if (K > 0) {
+          const uint32_t r = lanes_below(acc);
+          const uint32_t dst = a ? r : 63u - (static_cast<uint32_t>(l) - r);
+          const uint32_t wi = static_cast<uint32_t>(
+              __builtin_amdgcn_ds_permute(static_cast<int>(dst << 2), l));
+          widx = static_cast<uint32_t>(
+              __builtin_amdgcn_ds_bpermute(static_cast<int>(i << 2), static_cast<int>(wi)));
+          k = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(
+                  static_cast<int>(widx << 2), static_cast<int>(ev.cur))) & m;
+        }
+      }
     }
     if (K == 0) {  // one exact serial draw (refills the window as needed)
-      k = ev.uniform_small(static_cast<uint32_t>(n));
+      k = Policy == kPolicyCpp ? ev.uniform_small(static_cast<uint32_t>(n))
+                               : NpChoice(ev, static_cast<uint32_t>(n));
       K = 1;
       serial = true;
     }
@@ -1070,20 +1101,21 @@ __device__ int c4_rollout_lanes(ConnectFour::State s, C& ctx, WaveMt& ev) {
     const bool win = ConnectFour::has_four(mine);
 #endif
     const uint64_t term = ballot(l < Kr && (win || moves + i + 1 == 42));
+    // stream offset in the window after move t's draw (not in serial runs)
+    auto advance = [&](int t) {
+      int np = ev.pos + 2 * (t + 1);
+      if constexpr (Policy != kPolicyCpp) np = n > 1 ? static_cast<int>(rl32(widx, t)) + 1 : ev.pos;
+      ev.words.add(np - ev.pos);
+      ev.pos = np;
+    };
     if (term) {
       const int t = ctz64(term);
-      if (!serial) {
-        ev.pos += 2 * (t + 1);
-        ev.words.add(2 * (t + 1));
-      }
+      if (!serial) advance(t);
       const uint64_t wins = ballot(win);
       const int winner = p ^ (t & 1);
       return ((wins >> t) & 1) ? (winner == 0 ? 1 : -1) : 0;
     }
-    if (!serial) {
-      ev.pos += 2 * Kr;
-      ev.words.add(2 * Kr);
-    }
+    if (!serial) advance(Kr - 1);
     const int last = Kr - 1;
     const uint64_t blast = rl64(mine, last);
     const int plast = p ^ (last & 1);
@@ -1898,6 +1930,8 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
   if constexpr (Policy == kPolicyCpp && SmallAbsl<G>::value) {
     if (ev.use7) return c4_rollout_lanes(s, ctx, ev);
   }
+  if constexpr (Policy == kPolicyNumpy && std::is_same<G, ConnectFour>::value)
+    return c4_rollout_lanes<kPolicyNumpy>(s, ctx, ev);
 #if OS_GO_LANES
   if constexpr (std::is_same<G, Go>::value) return go_rollout_wave<Policy>(s, g, ctx, ev);
 #endif
