@@ -944,6 +944,12 @@ __device__ __forceinline__ double puct_value_sel(const Node<R>& c, bool in, int 
   return in ? v : -__builtin_huge_val();
 }
 
+// Set bits of the wave-uniform mask m in the lanes below this one.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
 // Inclusive prefix (OR / sum) over the 16 lanes of each DPP row; lanes that
 // would read across the row boundary read 0 (bound_ctrl), the identity.
 template <int Shift>
@@ -1156,11 +1162,6 @@ __device__ __forceinline__ uint64_t wave_scan_or64(uint64_t v) {
   const uint32_t lo = wave_scan_or32(static_cast<uint32_t>(v));
   const uint32_t hi = wave_scan_or32(static_cast<uint32_t>(v >> 32));
   return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-// Set bits of the wave-uniform mask m in the lanes below this one.
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
 
 // Not a playout return value: the lane-parallel playout declines and the
