@@ -157,6 +157,11 @@ __device__ __forceinline__ double rld(double v, int lane) {
 __device__ __forceinline__ uint32_t wl32(uint32_t v, int lane, uint32_t old) {
   return lane_id() == lane ? v : old;  // v_cmp + v_cndmask
 }
+// v_writelane: `v` (wave-uniform) into lane `lane` (wave-uniform) of `old`.
+__device__ __forceinline__ uint32_t wlu(uint32_t v, int lane, uint32_t old) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_writelane(static_cast<int>(v), lane, static_cast<int>(old)));
+}
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
 // An instrumentation counter kept in lane 0 of a VGPR rather than in an
@@ -694,6 +699,77 @@ __device__ __forceinline__ void wave_shuffle_cpp(LaneArr& a, int n, Mt& g) {
   a.a1 = n1;
 }
 
+// numpy RandomState.shuffle (os_rng.h NpShuffle: j_i = random_interval(i)
+// for i = n - 1 .. 1, swap(a[i], a[j_i])) of a lane-distributed array, for
+// long lists (hex, breakthrough, go expansions):
+//   draws   found over the stream's 64-word window as in hex_rollout_lanes_np
+//           (the mask only halves when i falls below its top bit; one
+//           ballot per draw), lane x holding j_{n-1-x};
+//   swaps   each lane traces its final position back through the
+//           transpositions (i = 1 first) to the position its element came
+//           from, and one gather moves the elements.
+// The stream is consumed exactly as the serial shuffle consumes it.
+template <class Mt>
+__device__ void np_shuffle_lanes(LaneArr& a, int n, Mt& g) {
+  if (n <= 1) return;
+  g.uniformize();
+  const int l = lane_id();
+  uint32_t rng = static_cast<uint32_t>(n - 1), mask = np_mask(rng);
+  auto window_avail = [&]() -> uint64_t {
+    const uint64_t below_valid = g.valid >= 64 ? ~0ull : ((1ull << g.valid) - 1ull);
+    return g.pos >= 64 ? 0ull : (below_valid & (~0ull << g.pos));
+  };
+  uint64_t avail = window_avail();
+  uint32_t v = g.cur & mask;
+  uint32_t j0 = 0, j1 = 0;
+  for (int x = 0; x < n - 1; ++x, --rng) {
+    if (rng <= (mask >> 1)) {
+      mask >>= 1;
+      v = g.cur & mask;
+    }
+    uint64_t ok = ballot(v <= rng) & avail;
+    while (!ok) {  // the window's unread words are all rejected
+      g.words.add(static_cast<uint32_t>(g.valid - g.pos));
+      g.pos = g.valid;
+      g.refill();
+      avail = window_avail();
+      v = g.cur & mask;
+      ok = ballot(v <= rng) & avail;
+    }
+    const int idx = ctz64(ok);
+    const uint64_t low = ok & (0ull - ok);
+    avail &= ~((low << 1) - 1ull);
+    g.words.add(static_cast<uint32_t>(idx + 1 - g.pos));
+    g.pos = idx + 1;
+    const uint32_t jv = rl32(v, idx);
+    if (x < 64) j0 = wlu(jv, x, j0);
+    else j1 = wlu(jv, x - 64, j1);
+  }
+  // final position -> source position (transpositions undone last-first)
+  uint32_t p0 = static_cast<uint32_t>(l), p1 = static_cast<uint32_t>(l + 64);
+  for (int i = 1; i <= n - 1; ++i) {
+    const int x = n - 1 - i;
+    const uint32_t ji = x < 64 ? rl32(j0, x) : rl32(j1, x - 64);
+    const uint32_t iu = static_cast<uint32_t>(i);
+    p0 = p0 == iu ? ji : (p0 == ji ? iu : p0);
+    if (n > 64) p1 = p1 == iu ? ji : (p1 == ji ? iu : p1);
+  }
+  const uint32_t s00 = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(static_cast<int>((p0 & 63) << 2), static_cast<int>(a.a0)));
+  const uint32_t s01 = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(static_cast<int>((p0 & 63) << 2), static_cast<int>(a.a1)));
+  uint32_t n1 = a.a1;
+  if (n > 64) {
+    const uint32_t s10 = static_cast<uint32_t>(
+        __builtin_amdgcn_ds_bpermute(static_cast<int>((p1 & 63) << 2), static_cast<int>(a.a0)));
+    const uint32_t s11 = static_cast<uint32_t>(
+        __builtin_amdgcn_ds_bpermute(static_cast<int>((p1 & 63) << 2), static_cast<int>(a.a1)));
+    n1 = p1 < 64 ? s10 : s11;
+  }
+  a.a0 = p0 < 64 ? s00 : s01;
+  a.a1 = n1;
+}
+
 template <int Policy, class Rng>
 __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
   if constexpr (Policy == kPolicyCpp && std::is_base_of<WaveMt, Rng>::value) {
@@ -713,7 +789,14 @@ __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
       a.swap(i + 1, static_cast<int>(x - q * b1));
       i += 2;
     }
-  } else {  // numpy RandomState.shuffle
+  } else if constexpr (std::is_base_of<WaveMt, Rng>::value) {  // numpy RandomState.shuffle
+    if (n > 16) {
+      np_shuffle_lanes(a, n, g);
+    } else {
+      for (int i = n - 1; i >= 1; --i)
+        a.swap(i, static_cast<int>(NpRandomInterval(g, static_cast<uint32_t>(i))));
+    }
+  } else {
     for (int i = n - 1; i >= 1; --i)
       a.swap(i, static_cast<int>(NpRandomInterval(g, static_cast<uint32_t>(i))));
   }
@@ -1293,35 +1376,51 @@ __device__ int hex_rollout_lanes_np(Hex::State s, const GameCfg& g, C& ctx, Wave
     return MtStream::temper(ev.peek_raw(q < qmax ? q : qmax - 1));
   };
   uint32_t win = load(0);
-  int cur = 0;                             // next unread word: lane cur of the window
+  // Draw j tests (w & mask) <= rng with rng = n0 - 1 - j: the mask only
+  // halves when rng falls below its top bit, so the masked words `v` are
+  // recomputed then, and `avail` keeps the window's unread words.
+  uint32_t rng = static_cast<uint32_t>(n0 - 1), mask = np_mask(rng);
+  uint32_t v = win & mask;
+  uint64_t avail = ~0ull;
+  int cur = 0;                             // next unread word, relative to q0
   uint32_t k0 = 0, k1 = 0, e0 = 0, e1 = 0;  // draw / offset after it, moves l and l + 64
-  for (int j = 0; j < n0; ++j) {
-    const uint32_t rng = static_cast<uint32_t>(n0 - j - 1);
-    uint32_t k = 0;
-    if (rng != 0) {
-      const uint32_t mask = np_mask(rng);
-      for (;;) {
-        const uint64_t ok = ballot((win & mask) <= rng) & (cur < 64 ? ~0ull << cur : 0ull);
-        if (ok) {
-          const int idx = ctz64(ok);
-          k = rl32(win, idx) & mask;
-          cur = idx + 1;
-          break;
-        }
-        wb += 64;
-        cur = 0;
-        if (q0 + wb + 64 > qmax) return kLanesDecline;
-        win = load(wb);
+  bool fail = false;
+  auto draw = [&]() -> uint32_t {
+    if (rng == 0) return 0u;  // one legal action: no word
+    if (rng <= (mask >> 1)) {
+      mask >>= 1;
+      v = win & mask;
+    }
+    uint64_t ok = ballot(v <= rng) & avail;
+    while (!ok) {  // the rest of the window is rejected: the next 64 words
+      wb += 64;
+      if (q0 + wb + 64 > qmax) {
+        fail = true;
+        return 0u;
       }
+      win = load(wb);
+      v = win & mask;
+      avail = ~0ull;
+      ok = ballot(v <= rng);
     }
-    const uint32_t e = static_cast<uint32_t>(wb + cur);
-    if (j < 64) {
-      k0 = wl32(k, j, k0);
-      e0 = wl32(e, j, e0);
-    } else {
-      k1 = wl32(k, j - 64, k1);
-      e1 = wl32(e, j - 64, e1);
-    }
+    const int idx = ctz64(ok);
+    const uint64_t low = ok & (0ull - ok);
+    avail &= ~((low << 1) - 1ull);  // words up to idx are read (idx = 63: all)
+    cur = wb + idx + 1;
+    return rl32(v, idx);
+  };
+  const int nlo = n0 < 64 ? n0 : 64;
+  for (int j = 0; j < nlo; ++j, --rng) {
+    const uint32_t k = draw();
+    if (fail) return kLanesDecline;
+    k0 = wlu(k, j, k0);
+    e0 = wlu(static_cast<uint32_t>(cur), j, e0);
+  }
+  for (int j = 64; j < n0; ++j, --rng) {
+    const uint32_t k = draw();
+    if (fail) return kLanesDecline;
+    k1 = wlu(k, j - 64, k1);
+    e1 = wlu(static_cast<uint32_t>(cur), j - 64, e1);
   }
   const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
   if (tend == 0) return kLanesDecline;  // unreachable
