@@ -159,8 +159,9 @@ __device__ __forceinline__ uint32_t wl32(uint32_t v, int lane, uint32_t old) {
 }
 // v_writelane: `v` (wave-uniform) into lane `lane` (wave-uniform) of `old`.
 __device__ __forceinline__ uint32_t wlu(uint32_t v, int lane, uint32_t old) {
-  return static_cast<uint32_t>(
-      __builtin_amdgcn_writelane(static_cast<int>(v), lane, static_cast<int>(old)));
+  uint32_t r;
+  asm("v_writelane_b32 %0, %1, %2" : "=v"(r) : "s"(v), "s"(lane), "0"(old));
+  return r;
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
