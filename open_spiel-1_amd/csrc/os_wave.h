@@ -157,12 +157,6 @@ __device__ __forceinline__ double rld(double v, int lane) {
 __device__ __forceinline__ uint32_t wl32(uint32_t v, int lane, uint32_t old) {
   return lane_id() == lane ? v : old;  // v_cmp + v_cndmask
 }
-// v_writelane: `v` (wave-uniform) into lane `lane` (wave-uniform) of `old`.
-__device__ __forceinline__ uint32_t wlu(uint32_t v, int lane, uint32_t old) {
-  uint32_t r;
-  asm("v_writelane_b32 %0, %1, %2" : "=v"(r) : "s"(v), "s"(lane), "0"(old));
-  return r;
-}
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
 // An instrumentation counter kept in lane 0 of a VGPR rather than in an
@@ -743,8 +737,8 @@ __device__ void np_shuffle_lanes(LaneArr& a, int n, Mt& g) {
     g.words.add(static_cast<uint32_t>(idx + 1 - g.pos));
     g.pos = idx + 1;
     const uint32_t jv = rl32(v, idx);
-    if (x < 64) j0 = wlu(jv, x, j0);
-    else j1 = wlu(jv, x - 64, j1);
+    if (x < 64) j0 = wl32(jv, x, j0);
+    else j1 = wl32(jv, x - 64, j1);
   }
   // final position -> source position (transpositions undone last-first)
   uint32_t p0 = static_cast<uint32_t>(l), p1 = static_cast<uint32_t>(l + 64);
@@ -1414,14 +1408,14 @@ __device__ int hex_rollout_lanes_np(Hex::State s, const GameCfg& g, C& ctx, Wave
   for (int j = 0; j < nlo; ++j, --rng) {
     const uint32_t k = draw();
     if (fail) return kLanesDecline;
-    k0 = wlu(k, j, k0);
-    e0 = wlu(static_cast<uint32_t>(cur), j, e0);
+    k0 = wl32(k, j, k0);
+    e0 = wl32(static_cast<uint32_t>(cur), j, e0);
   }
   for (int j = 64; j < n0; ++j, --rng) {
     const uint32_t k = draw();
     if (fail) return kLanesDecline;
-    k1 = wlu(k, j - 64, k1);
-    e1 = wlu(static_cast<uint32_t>(cur), j - 64, e1);
+    k1 = wl32(k, j - 64, k1);
+    e1 = wl32(static_cast<uint32_t>(cur), j - 64, e1);
   }
   const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
   if (tend == 0) return kLanesDecline;  // unreachable
