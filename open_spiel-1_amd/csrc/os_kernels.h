@@ -1353,7 +1353,8 @@ __global__ __launch_bounds__(64) void k_waz_step(AzArgs a) {
       legal_lanes(lg, acts);
       perm.a0 = static_cast<uint32_t>(l);
       perm.a1 = static_cast<uint32_t>(l + 64);
-      if (a.np_policy) wave_shuffle<kPolicyNumpy>(perm, nc, bot);  // mcts.py:320
+      if (a.np_policy)  // mcts.py:320
+        wave_shuffle<kPolicyNumpy, WaveMtRow, !std::is_same<G, Go>::value>(perm, nc, bot);
       else wave_shuffle<kPolicyCpp>(perm, nc, bot);
       const uint32_t first = from_raw ? parked_first : used;
       WAZ_CHECK(nc >= 1 && nc <= 128, 5);

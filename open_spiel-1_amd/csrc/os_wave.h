@@ -765,7 +765,10 @@ __device__ void np_shuffle_lanes(LaneArr& a, int n, Mt& g) {
   a.a1 = n1;
 }
 
-template <int Policy, class Rng>
+// kLaneNp: long numpy shuffles take np_shuffle_lanes (not in go's search
+// kernels, where the extra live registers cost the wave kernel its
+// occupancy and put state in scratch memory).
+template <int Policy, class Rng, bool kLaneNp = true>
 __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
   if constexpr (Policy == kPolicyCpp && std::is_base_of<WaveMt, Rng>::value) {
     wave_shuffle_cpp(a, n, g);
@@ -784,7 +787,7 @@ __device__ void wave_shuffle(LaneArr& a, int n, Rng& g) {
       a.swap(i + 1, static_cast<int>(x - q * b1));
       i += 2;
     }
-  } else if constexpr (std::is_base_of<WaveMt, Rng>::value) {  // numpy RandomState.shuffle
+  } else if constexpr (kLaneNp && std::is_base_of<WaveMt, Rng>::value) {  // numpy shuffle
     if (n > 16) {
       np_shuffle_lanes(a, n, g);
     } else {
@@ -2460,7 +2463,7 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         acts.a0 = l < nc ? static_cast<uint32_t>(lg.kth(l)) : 0u;
 #endif
         acts.a1 = l + 64 < nc ? static_cast<uint32_t>(lg.kth(l + 64)) : 0u;
-        wave_shuffle<Policy>(acts, nc, bot);
+        wave_shuffle<Policy, WaveMt, !std::is_same<G, Go>::value>(acts, nc, bot);
         if (used + static_cast<uint32_t>(nc) > cap) {
           bool ok = false;
           if constexpr (kPageable) {  // next page of the pool, if there is one
