@@ -697,7 +697,7 @@ __device__ __forceinline__ void wave_shuffle_cpp(LaneArr& a, int n, Mt& g) {
 // numpy RandomState.shuffle (os_rng.h NpShuffle: j_i = random_interval(i)
 // for i = n - 1 .. 1, swap(a[i], a[j_i])) of a lane-distributed array, for
 // long lists (hex, breakthrough, go expansions):
-//   draws   found over the stream's 64-word window as in hex_rollout_lanes_np
+//   draws   found over the stream's 64-word window as in fill_draws_np
 //           (the mask only halves when i falls below its top bit; one
 //           ballot per draw), lane x holding j_{n-1-x};
 //   swaps   each lane traces its final position back through the
@@ -1304,18 +1304,23 @@ __device__ __forceinline__ void hex_take(uint32_t& r, uint32_t k, uint32_t tau, 
 __device__ inline int hex_fill_end(const Hex::State& s, const GameCfg& g, B128 empty, int n0,
                                    uint32_t k0, uint32_t k1);
 
-template <class C>
-__device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
-  (void)ctx;
-  s = make_uniform(s);
-  ev.uniformize();
-  if (Hex::terminal(s, g)) return s.result;
+// Draws of a fill playout (every move fills one empty cell, so move j draws
+// over n0 - j legal actions whatever was played): k0 / k1 = the draws of moves
+// l and l + 64, from the stream at offset q0 (WaveMt::offset; words past the
+// block come from peek_raw).  false: decline to the serial playout.
+//   C++ (absl::Uniform(0, n), os_rng.h AbslUniform): two words per move, lane
+//     j reads the pair at 2j; a pair absl might reject (P mod 2^64 < n)
+//     declines.
+//   numpy (RandomState.choice, mcts.py:56-63; os_rng.h NpChoice: no word when
+//     n = 1, else 32-bit words until (w & mask) <= n - 1): the words taken vary,
+//     so the draws are found serially over a 64-word window of tempered words
+//     on the lanes -- the accepted word of move j is the first unread lane
+//     whose word passes move j's test (one compare and ballot; the mask only
+//     halves when n - 1 falls below its top bit) -- and e0 / e1 record the
+//     offset (from q0) after each move's draw.
+__device__ inline bool fill_draws_cpp(WaveMt& ev, int q0, int n0, uint32_t& k0, uint32_t& k1) {
   const int l = lane_id();
-  const int n = g.rows;
-  const B128 empty = g.board & ~(s.st[0] | s.st[1]);
-  const int n0 = popc(empty);
-  const int q0 = ev.offset();
-  uint32_t k0 = 0, k1 = 0;  // draws of moves l and l + 64
+  k0 = k1 = 0;
   bool risky = false;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1337,36 +1342,12 @@ __device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt&
     if (h == 0) k0 = k;
     else k1 = k;
   }
-  if (ballot(risky)) return kLanesDecline;
-  const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
-  if (tend == 0) return kLanesDecline;  // unreachable
-  const int winner = s.to_play ^ ((tend - 1) & 1);  // the mover of the last stone
-  ev.seek(q0 + 2 * tend);
-  ev.words.add(2 * tend);
-  return winner == 0 ? 1 : -1;
+  return !ballot(risky);
 }
 
-// The same playout under python/algorithms/mcts.py (RandomState.choice over
-// LegalActions(), mcts.py:56-63).  |LegalActions| before move j is still
-// n0 - j, but numpy's masked-rejection draw (os_rng.h NpChoice: no word when
-// n = 1, else 32-bit words until (w & mask) <= n - 1) takes a varying number
-// of words, so the draws are found serially over a 64-word window of tempered
-// words on the lanes: the accepted word of move j is the first lane at or
-// after the cursor whose word passes move j's test (one compare and ballot),
-// and lane j records the draw and the stream offset after it.  The fill and
-// end steps are the C++ playout's; the stream then moves to the offset after
-// the last move's draw.  A playout whose draws would read past what peek_raw
-// reaches declines to the serial loop.
-template <class C>
-__device__ int hex_rollout_lanes_np(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
-  (void)ctx;
-  s = make_uniform(s);
-  ev.uniformize();
-  if (Hex::terminal(s, g)) return s.result;
+__device__ inline bool fill_draws_np(WaveMt& ev, int q0, int n0, uint32_t& k0, uint32_t& k1,
+                                     uint32_t& e0, uint32_t& e1) {
   const int l = lane_id();
-  const B128 empty = g.board & ~(s.st[0] | s.st[1]);
-  const int n0 = popc(empty);
-  const int q0 = ev.offset();
   const int qmax = kMtN + (kMtN - kMtM) + (kMtN - kMtM);  // peek_raw's reach
   int wb = 0;  // window base, relative to q0
   auto load = [&](int b) {
@@ -1374,14 +1355,11 @@ __device__ int hex_rollout_lanes_np(Hex::State s, const GameCfg& g, C& ctx, Wave
     return MtStream::temper(ev.peek_raw(q < qmax ? q : qmax - 1));
   };
   uint32_t win = load(0);
-  // Draw j tests (w & mask) <= rng with rng = n0 - 1 - j: the mask only
-  // halves when rng falls below its top bit, so the masked words `v` are
-  // recomputed then, and `avail` keeps the window's unread words.
   uint32_t rng = static_cast<uint32_t>(n0 - 1), mask = np_mask(rng);
   uint32_t v = win & mask;
-  uint64_t avail = ~0ull;
-  int cur = 0;                             // next unread word, relative to q0
-  uint32_t k0 = 0, k1 = 0, e0 = 0, e1 = 0;  // draw / offset after it, moves l and l + 64
+  uint64_t avail = ~0ull;  // unread words of the window
+  int cur = 0;             // next unread word, relative to q0
+  k0 = k1 = e0 = e1 = 0;
   bool fail = false;
   auto draw = [&]() -> uint32_t {
     if (rng == 0) return 0u;  // one legal action: no word
@@ -1410,22 +1388,101 @@ __device__ int hex_rollout_lanes_np(Hex::State s, const GameCfg& g, C& ctx, Wave
   const int nlo = n0 < 64 ? n0 : 64;
   for (int j = 0; j < nlo; ++j, --rng) {
     const uint32_t k = draw();
-    if (fail) return kLanesDecline;
+    if (fail) return false;
     k0 = wl32(k, j, k0);
     e0 = wl32(static_cast<uint32_t>(cur), j, e0);
   }
   for (int j = 64; j < n0; ++j, --rng) {
     const uint32_t k = draw();
-    if (fail) return kLanesDecline;
+    if (fail) return false;
     k1 = wl32(k, j - 64, k1);
     e1 = wl32(static_cast<uint32_t>(cur), j - 64, e1);
   }
-  const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
-  if (tend == 0) return kLanesDecline;  // unreachable
-  const int winner = s.to_play ^ ((tend - 1) & 1);
-  const int used = static_cast<int>(tend <= 64 ? rl32(e0, tend - 1) : rl32(e1, tend - 65));
+  return true;
+}
+
+// Moves the stream past the first `tend` moves' draws of a fill playout.
+template <int Policy>
+__device__ inline void fill_seek(WaveMt& ev, int q0, int tend, uint32_t e0, uint32_t e1) {
+  const int used = Policy == kPolicyCpp
+                       ? 2 * tend
+                       : static_cast<int>(tend <= 64 ? rl32(e0, tend - 1) : rl32(e1, tend - 65));
   ev.seek(q0 + used);
   ev.words.add(used);
+}
+
+// hex under either policy (the numpy form: python/algorithms/mcts.py's
+// RandomState.choice playouts).
+template <int Policy, class C>
+__device__ int hex_rollout_lanes(Hex::State s, const GameCfg& g, C& ctx, WaveMt& ev) {
+  (void)ctx;
+  s = make_uniform(s);
+  ev.uniformize();
+  if (Hex::terminal(s, g)) return s.result;
+  const B128 empty = g.board & ~(s.st[0] | s.st[1]);
+  const int n0 = popc(empty);
+  const int q0 = ev.offset();
+  uint32_t k0, k1, e0 = 0, e1 = 0;
+  const bool ok = Policy == kPolicyCpp ? fill_draws_cpp(ev, q0, n0, k0, k1)
+                                       : fill_draws_np(ev, q0, n0, k0, k1, e0, e1);
+  if (!ok) return kLanesDecline;
+  const int tend = hex_fill_end(s, g, empty, n0, k0, k1);
+  if (tend == 0) return kLanesDecline;  // unreachable
+  const int winner = s.to_play ^ ((tend - 1) & 1);  // the mover of the last stone
+  fill_seek<Policy>(ev, q0, tend, e0, e1);
+  return winner == 0 ? 1 : -1;
+}
+
+// tic_tac_toe random playout, the same way: every move fills an empty cell,
+// so the draws, then the fill times (cell c = lane c), then the end -- the
+// earliest time a line's three cells hold one player's stones (the latest of
+// their fill times; a line already complete would have ended the game), or
+// the full board (a draw, tic_tac_toe.cc:80-150).
+constexpr uint32_t kTttLineA = 0x20210630u, kTttLineB = 0x44543741u, kTttLineC = 0x68876852u;
+template <int Policy>
+__device__ int ttt_rollout_lanes(TicTacToe::State s, const GameCfg& g, WaveMt& ev) {
+  s = make_uniform(s);
+  ev.uniformize();
+  if (TicTacToe::terminal(s, g)) return s.winner == 0 ? 1 : (s.winner == 1 ? -1 : 0);
+  const int l = lane_id();
+  const uint32_t b0 = s.b[0], b1 = s.b[1];
+  const uint32_t empty = 0x1FFu & ~(b0 | b1);
+  const int n0 = __builtin_popcount(empty);
+  const int q0 = ev.offset();
+  uint32_t k0, k1, e0 = 0, e1 = 0;
+  const bool ok = Policy == kPolicyCpp ? fill_draws_cpp(ev, q0, n0, k0, k1)
+                                       : fill_draws_np(ev, q0, n0, k0, k1, e0, e1);
+  if (!ok) return kLanesDecline;
+  // fill times (0: a stone of the state) and owners of cell l < 9
+  uint32_t t = 0;
+  const bool on = l < 9;
+  uint32_t r = (on && ((empty >> l) & 1u)) ? lanes_below(empty) : 0x40000000u;
+  for (int j = 0; j < n0; ++j) hex_take(r, rl32(k0, j), static_cast<uint32_t>(j + 1), t);
+  const int p = s.to_play;
+  const uint32_t own = t ? static_cast<uint32_t>(p ^ static_cast<int>((t - 1) & 1))
+                         : (on ? ((b1 >> l) & 1u) : 0u);
+  const uint32_t cell = t | (own << 8);  // fill time | owner << 8
+  // line l < 8: cells (A, B, C) from nibble l of the tables
+  const int sh = 4 * (l & 7);
+  auto at = [&](uint32_t tab) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(
+        static_cast<int>(((tab >> sh) & 15u) << 2), static_cast<int>(cell)));
+  };
+  const uint32_t ca = at(kTttLineA), cb = at(kTttLineB), cc = at(kTttLineC);
+  const bool same = ((ca ^ cb) >> 8) == 0 && ((ca ^ cc) >> 8) == 0;
+  const uint32_t ta = ca & 0xFFu, tb = cb & 0xFFu, tc = cc & 0xFFu;
+  uint32_t done = ta > tb ? ta : tb;
+  done = done > tc ? done : tc;
+  uint32_t v = (l < 8 && same) ? done : 0xFFu;  // lines of mixed owners never end it
+  for (int off = 4; off >= 1; off >>= 1) {      // minimum over lanes 0..7
+    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), off));
+    v = o < v ? o : v;
+  }
+  const uint32_t tw = rl32(v, 0);
+  const int tend = tw <= static_cast<uint32_t>(n0) ? static_cast<int>(tw) : n0;
+  fill_seek<Policy>(ev, q0, tend, e0, e1);
+  if (tw > static_cast<uint32_t>(n0)) return 0;  // full board, no line
+  const int winner = p ^ ((tend - 1) & 1);
   return winner == 0 ? 1 : -1;
 }
 
@@ -2030,6 +2087,10 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
   }
   if constexpr (Policy == kPolicyNumpy && std::is_same<G, ConnectFour>::value)
     return c4_rollout_lanes<kPolicyNumpy>(s, ctx, ev);
+  if constexpr (std::is_same<G, TicTacToe>::value) {
+    const int r = ttt_rollout_lanes<Policy>(s, g, ev);
+    if (r != kLanesDecline) return r;
+  }
 #if OS_GO_LANES
   if constexpr (std::is_same<G, Go>::value) return go_rollout_wave<Policy>(s, g, ctx, ev);
 #endif
@@ -2037,8 +2098,7 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
     // n >= 3: on n <= 2 the reference's wrap filter (hex.cc:206-222) leaves
     // filled boards without a winner, so the end-of-fill argument fails.
     if (g.rows >= 3) {
-      const int r = Policy == kPolicyCpp ? hex_rollout_lanes(s, g, ctx, ev)
-                                         : hex_rollout_lanes_np(s, g, ctx, ev);
+      const int r = hex_rollout_lanes<Policy>(s, g, ctx, ev);
       if (r != kLanesDecline) return r;
     }
   }
