@@ -2087,7 +2087,9 @@ __device__ int wave_rollout(typename G::State s, const GameCfg& g, C& ctx, Rng& 
   }
   if constexpr (Policy == kPolicyNumpy && std::is_same<G, ConnectFour>::value)
     return c4_rollout_lanes<kPolicyNumpy>(s, ctx, ev);
-  if constexpr (std::is_same<G, TicTacToe>::value) {
+  // C++ policy only: the numpy form's serial window draws cost more than
+  // the short serial playout they replace (3.56 -> 3.76 ms per 1000-sim step)
+  if constexpr (Policy == kPolicyCpp && std::is_same<G, TicTacToe>::value) {
     const int r = ttt_rollout_lanes<Policy>(s, g, ev);
     if (r != kLanesDecline) return r;
   }
