@@ -649,12 +649,13 @@ def _az_network(obs_size, A, torch, dev, hidden=256):
       return prior, value
 
     def evaluate_into(self, obs, legal, kind, prior, value):
-      # one GEMM for both heads, then the fused heads kernel writes the
-      # engine's response buffers (os_amd.az.heads_into)
-      from os_amd.az import heads_into
-      x = obs.reshape(obs.shape[0], -1).to(torch.bfloat16)
-      h = torch.relu_(x @ w1)
-      heads_into(h @ wpv, legal, prior, value)
+      # the whole round in one kernel: both products on the matrix cores,
+      # then the heads write the engine's response buffers
+      # (os_az_mlp_heads_async; the same network as __call__ above)
+      mlp.heads_into(obs, legal, prior, value)
+
+  from os_amd.az import MlpNetwork
+  mlp = MlpNetwork(w1, wpv)
   return Evaluator()
 
 

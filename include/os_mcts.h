@@ -333,6 +333,18 @@ int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32
 int os_az_heads_async(const void* logits, int32_t dtype, int64_t num_rows, int32_t num_actions,
                       int64_t ld, const uint8_t* legal, double* prior, double* value,
                       void* hip_stream);
+/* A whole evaluator round for a one-hidden-layer network, fused into one
+ * kernel on hip_stream: h = relu(bf16(obs) . W1) (f32 accumulation, bf16),
+ * logits = bf16(h . Wout), then the heads of os_az_heads_async (f64).  obs
+ * f32 [num_rows][obs_size] (the engine's dev_obs), w1t bf16 [hidden][128]
+ * (W1 transposed, K zero-padded to 128), wout bf16 [16][hidden] (row a =
+ * action a's logit weights, row num_actions = the value's, the rest zero).
+ * obs_size <= 128, hidden a multiple of 32 and <= 256, num_actions + 1 <= 16.
+ * Both products run on the matrix cores (v_mfma_f32_16x16x32_bf16). */
+int os_az_mlp_heads_async(const float* obs, int64_t num_rows, int32_t obs_size,
+                          const uint16_t* w1t, int32_t hidden, const uint16_t* wout,
+                          int32_t num_actions, const uint8_t* legal, double* prior,
+                          double* value, void* hip_stream);
 
 /* ---- Self-play -----------------------------------
  * num_games independent games, each played on the device the way

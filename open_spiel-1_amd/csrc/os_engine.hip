@@ -1786,6 +1786,124 @@ __global__ void k_az_heads(const void* logits, int32_t dtype, int64_t R, int32_t
   value[r] = tanh(get(A));
 }
 
+// A one-hidden-layer policy / value network fused with its heads, for a
+// batched external-evaluator round (the bench's stand-in network; an
+// evaluator may use it through os_az_mlp_heads_async):
+//   h      = relu(bf16(obs) . W1)            hidden units, f32 accumulation, bf16
+//   logits = bf16(h . Wout)                  A policy logits, then the value logit
+//   prior  = softmax over the legal actions, value = tanh   (k_az_heads, f64)
+// One wave owns 16 rows.  Both products run on the matrix cores
+// (v_mfma_f32_16x16x32_bf16) transposed -- H^T = W1^T . X^T, then
+// L^T = Wout^T . H^T -- so the first product's accumulators (hidden on the
+// register index, the row on the lane) are the second one's B operand with no
+// lane movement: lane group g of a 32-hidden chunk holds hidden units
+// {4g..4g+3} of its two 16-unit tiles, and the A operand (Wout) is read in that
+// same k order.  Weights: w1t bf16 [hidden][128] (K padded with zeros),
+// wout bf16 [16][hidden] (rows A + 1 .. 15 zero); obs_size <= 128,
+// hidden <= 256 and a multiple of 32, A + 1 <= 16.
+using AzFragAB = __attribute__((ext_vector_type(8))) short;
+using AzFragCD = __attribute__((ext_vector_type(4))) float;
+constexpr int kAzMlpK = 128;
+constexpr int kAzMlpMaxHidden = 256;
+
+__device__ __forceinline__ uint16_t az_bf16(float f) {  // round to nearest even
+  const uint32_t u = __float_as_uint(f);
+  return static_cast<uint16_t>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+__global__ __launch_bounds__(64) void k_az_mlp_heads(const float* obs, int64_t R, int32_t obs_size,
+                                                     const uint16_t* w1t, int32_t hidden,
+                                                     const uint16_t* wout, int32_t A,
+                                                     const uint8_t* legal, double* prior,
+                                                     double* value) {
+  __shared__ float lg[16][17];
+  const int l = threadIdx.x;
+  const int g = l >> 4, c16 = l & 15;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * 16;
+  const int64_t row = row0 + c16;
+  const bool live = row < R;
+  // X^T fragments (B of the first product): obs[row][32c + 8g + j], j < 8
+  AzFragAB xb[kAzMlpK / 32];
+#pragma unroll
+  for (int c = 0; c < kAzMlpK / 32; ++c) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * c + 8 * g + j;
+      const float v = (live && k < obs_size) ? obs[row * obs_size + k] : 0.0f;
+      xb[c][j] = static_cast<short>(az_bf16(v));
+    }
+  }
+  const int tiles = hidden / 16;
+  AzFragCD out = {0.0f, 0.0f, 0.0f, 0.0f};
+  // hidden chunk by chunk (two 16-unit tiles = 32 units): the chunk's H^T
+  // tiles, then their contribution to L^T
+  for (int c2 = 0; c2 < tiles / 2; ++c2) {
+    AzFragCD h[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = 2 * c2 + u;
+      AzFragCD acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      const uint16_t* wrow = w1t + static_cast<int64_t>(16 * t + c16) * kAzMlpK + 8 * g;
+#pragma unroll
+      for (int c = 0; c < kAzMlpK / 32; ++c) {
+        const AzFragAB a = *reinterpret_cast<const AzFragAB*>(wrow + 32 * c);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xb[c], acc, 0, 0, 0);
+      }
+      h[u] = acc;  // H^T[16t + 4g + r][row]
+    }
+    // B of the second product: element j <- hidden 32 c2 + (j < 4 ? 4g + j : 16 + 4g + j - 4)
+    AzFragAB hb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = h[j >> 2][j & 3];
+      hb[j] = static_cast<short>(az_bf16(v > 0.0f ? v : 0.0f));  // relu, bf16
+    }
+    // A of the second product: Wout^T[o = c16][same k order]
+    const uint16_t* wo = wout + static_cast<int64_t>(c16) * hidden + 32 * c2 + 4 * g;
+    AzFragAB ab;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ab[j] = static_cast<short>(wo[j]);
+      ab[4 + j] = static_cast<short>(wo[16 + j]);
+    }
+    out = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, hb, out, 0, 0, 0);
+  }
+  // L^T[o = 4g + r][row c16] -> LDS [row][o], rounded to bf16 like the GEMM's output
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    lg[c16][4 * g + r] = __uint_as_float(static_cast<uint32_t>(az_bf16(out[r])) << 16);
+  __syncthreads();
+  if (l >= 16 || !live) return;
+  // heads (k_az_heads' arithmetic)
+  const uint8_t* lm = legal + row * A;
+  double m = -__builtin_huge_val();
+  for (int a = 0; a < A; ++a) m = fmax(m, lm[a] ? static_cast<double>(lg[l][a]) : -1e32);
+  double sum = 0.0;
+  for (int a = 0; a < A; ++a) sum += exp((lm[a] ? static_cast<double>(lg[l][a]) : -1e32) - m);
+  double* pr = prior + row * A;
+  for (int a = 0; a < A; ++a) pr[a] = exp((lm[a] ? static_cast<double>(lg[l][a]) : -1e32) - m) / sum;
+  value[row] = tanh(static_cast<double>(lg[l][A]));
+}
+
+int os_az_mlp_heads_async(const float* obs, int64_t num_rows, int32_t obs_size,
+                          const uint16_t* w1t, int32_t hidden, const uint16_t* wout,
+                          int32_t num_actions, const uint8_t* legal, double* prior,
+                          double* value, void* hip_stream) {
+  if (num_rows < 0 || obs_size < 1 || obs_size > kAzMlpK || hidden < 32 ||
+      hidden > kAzMlpMaxHidden || hidden % 32 != 0 || num_actions < 1 || num_actions + 1 > 16)
+    return Fail(OS_ERR_INVALID, "bad network shape (obs <= 128, hidden % 32 == 0 and <= 256, "
+                                "actions + 1 <= 16)");
+  if (num_rows == 0) return OS_OK;
+  if (!obs || !w1t || !wout || !legal || !prior || !value)
+    return Fail(OS_ERR_INVALID, "null network buffer");
+  const unsigned blocks = static_cast<unsigned>((num_rows + 15) / 16);
+  hipLaunchKernelGGL(k_az_mlp_heads, dim3(blocks), dim3(64), 0,
+                     static_cast<hipStream_t>(hip_stream), obs, num_rows, obs_size, w1t, hidden,
+                     wout, num_actions, legal, prior, value);
+  HIP_TRY(hipGetLastError());
+  return OS_OK;
+}
+
 int os_az_heads_async(const void* logits, int32_t dtype, int64_t num_rows, int32_t num_actions,
                       int64_t ld, const uint8_t* legal, double* prior, double* value,
                       void* hip_stream) {

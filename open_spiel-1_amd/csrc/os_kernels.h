@@ -383,6 +383,13 @@ template <>
 struct WaveOcc<Hex> {
   static constexpr int value = OS_HEX_OCC;
 };
+#ifndef OS_BT_OCC
+#define OS_BT_OCC 1
+#endif
+template <>
+struct WaveOcc<Breakthrough> {
+  static constexpr int value = OS_BT_OCC;
+};
 
 // kPaged: the search may take pages from the pool (os_wave.h kPg*).  The
 // reserved-arena variant is a separate kernel: the cold page-switch path

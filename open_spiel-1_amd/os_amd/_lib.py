@@ -174,6 +174,8 @@ _sig("os_az_prepare_stateful", ctypes.c_int,
 _sig("os_az_export_rng", ctypes.c_int, [_vp, _P, _P])
 _sig("os_az_step_async", ctypes.c_int, [_vp, _vp])
 _sig("os_az_heads_async", ctypes.c_int, [_vp, _i32, _i64, _i32, _i64, _vp, _vp, _vp, _vp])
+_sig("os_az_mlp_heads_async", ctypes.c_int,
+     [_vp, _i64, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp, _vp])
 _sig("os_az_set_requests", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_az_set_layout", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_az_get_layout", ctypes.c_int, [_vp, _P])

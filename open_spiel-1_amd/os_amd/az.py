@@ -72,6 +72,45 @@ def heads_into(logits, legal, prior, value):
                               value.data_ptr(), st.cuda_stream))
 
 
+class MlpNetwork:
+  """Weights of a one-hidden-layer policy / value network in the layout of
+  os_az_mlp_heads_async, from w1 [obs_size, hidden] and w_out [hidden, A + 1]
+  (the policy logits' columns, then the value's): w1t bf16 [hidden][128]
+  and wout bf16 [16][hidden], zero-padded."""
+
+  def __init__(self, w1, w_out):
+    import torch
+    obs_size, hidden = w1.shape
+    a1 = w_out.shape[1]
+    if obs_size > 128 or hidden % 32 or hidden > 256 or a1 > 16 or w_out.shape[0] != hidden:
+      raise ValueError("network shape outside os_az_mlp_heads_async's bounds")
+    dev = w1.device
+    self.w1t = torch.zeros(hidden, 128, dtype=torch.bfloat16, device=dev)
+    self.w1t[:, :obs_size] = w1.t().to(torch.bfloat16)
+    self.wout = torch.zeros(16, hidden, dtype=torch.bfloat16, device=dev)
+    self.wout[:a1] = w_out.t().to(torch.bfloat16)
+    self.obs_size, self.hidden, self.num_actions = obs_size, hidden, a1 - 1
+
+  def heads_into(self, obs, legal, prior, value):
+    """One evaluator round fused into one kernel on the current stream:
+    relu(bf16(obs) . W1) . Wout, then softmax over the legal actions / tanh
+    (os_az_mlp_heads_async)."""
+    import torch
+    n, a = prior.shape
+    if a != self.num_actions or tuple(value.shape) != (n,) or tuple(legal.shape) != (n, a):
+      raise ValueError("prior [N, A], legal [N, A], value [N] expected")
+    if obs.dtype != torch.float32 or obs.numel() != n * self.obs_size or not obs.is_contiguous():
+      raise ValueError("obs must be contiguous float32 [N, obs_size]")
+    if legal.dtype != torch.uint8 or prior.dtype != torch.float64 or value.dtype != torch.float64:
+      raise ValueError("legal uint8, prior / value float64 expected")
+    if not (legal.is_contiguous() and prior.is_contiguous() and value.is_contiguous()):
+      raise ValueError("legal, prior and value must be contiguous")
+    st = torch.cuda.current_stream(prior.device)
+    check(lib.os_az_mlp_heads_async(obs.data_ptr(), n, self.obs_size, self.w1t.data_ptr(),
+                                    self.hidden, self.wout.data_ptr(), a, legal.data_ptr(),
+                                    prior.data_ptr(), value.data_ptr(), st.cuda_stream))
+
+
 def _evaluate(evaluator, obs, legal, kind, prior, value):
   """One evaluator round: in place when the evaluator supports it."""
   into = getattr(evaluator, "evaluate_into", None)

@@ -470,3 +470,64 @@ def test_gpu_staged_batch_matches_oracle(require_gpu, game):
   with pytest.raises(RuntimeError):  # a staged batch is consumed once
     search.run(acts, offs, seeds, ev, staged=True, **kw)
     search.run(acts, offs, seeds, ev, staged=True, **kw)
+
+
+def _bf16_round(x):
+  """float32 -> bfloat16 value (round to nearest even), as float64."""
+  u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+  r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+  return r.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("obs_size,hidden,A", [(126, 256, 7), (27, 64, 9), (83, 128, 15)])
+def test_gpu_mlp_heads_kernel_matches_exact_reference(require_gpu, obs_size, hidden, A):
+  """os_az_mlp_heads_async (both products on the matrix cores) against a
+  numpy restatement on integer-valued data: every f32 partial sum is an exact
+  integer, so the products are order-independent and the bf16 roundings
+  deterministic; the heads then agree to the device exp's rounding."""
+  import torch
+  from os_amd.az import MlpNetwork
+  rs = np.random.RandomState(obs_size + hidden)
+  N = 1000
+  obs = (rs.rand(N, obs_size) < 0.3).astype(np.float32)
+  w1 = rs.randint(-2, 3, size=(obs_size, hidden)).astype(np.float32)
+  wo = rs.randint(-2, 3, size=(hidden, A + 1)).astype(np.float32) / 64.0  # exact in bf16
+  legal = (rs.rand(N, A) < 0.6).astype(np.uint8)
+  legal[0] = 0
+  net = MlpNetwork(torch.from_numpy(w1).cuda(), torch.from_numpy(wo).cuda())
+  prior = torch.full((N, A), -7.0, dtype=torch.float64, device="cuda")
+  value = torch.full((N,), -7.0, dtype=torch.float64, device="cuda")
+  net.heads_into(torch.from_numpy(obs).cuda(), torch.from_numpy(legal).cuda(), prior, value)
+  h = np.maximum(obs.astype(np.float64) @ w1.astype(np.float64), 0.0)   # exact
+  h = _bf16_round(h)
+  logits = _bf16_round(h @ wo.astype(np.float64))
+  masked = np.where(legal == 1, logits[:, :A], -1e32)
+  m = masked.max(axis=1, keepdims=True)
+  e = np.exp(masked - m)
+  ref_p = e / e.sum(axis=1, keepdims=True)
+  ref_v = np.tanh(logits[:, A])
+  np.testing.assert_allclose(prior.cpu().numpy(), ref_p, rtol=1e-13, atol=1e-300)
+  np.testing.assert_allclose(value.cpu().numpy(), ref_v, rtol=1e-13, atol=1e-15)
+
+
+@pytest.mark.gpu
+def test_gpu_mlp_heads_kernel_matches_torch_network(require_gpu):
+  """The bench's random bf16 network: the fused kernel against the same
+  network in torch (bf16 GEMMs), to bf16 rounding."""
+  import torch
+  from os_amd.az import MlpNetwork, heads_into
+  g = torch.Generator().manual_seed(3)
+  N, O, H, A = 4096, 126, 256, 7
+  w1 = (torch.randn(O, H, generator=g) / O ** 0.5).to("cuda", torch.bfloat16)
+  wpv = (torch.randn(H, A + 1, generator=g) / H ** 0.5).to("cuda", torch.bfloat16)
+  obs = (torch.rand(N, O, generator=g) < 0.3).float().cuda()
+  legal = (torch.rand(N, A, generator=g) < 0.7).to(torch.uint8).cuda()
+  p1 = torch.zeros(N, A, dtype=torch.float64, device="cuda")
+  v1 = torch.zeros(N, dtype=torch.float64, device="cuda")
+  MlpNetwork(w1, wpv).heads_into(obs, legal, p1, v1)
+  p2 = torch.zeros_like(p1)
+  v2 = torch.zeros_like(v1)
+  heads_into(torch.relu(obs.to(torch.bfloat16) @ w1) @ wpv, legal, p2, v2)
+  torch.testing.assert_close(p1, p2, rtol=0.05, atol=0.02)
+  torch.testing.assert_close(v1, v2, rtol=0.05, atol=0.02)
