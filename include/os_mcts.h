@@ -289,6 +289,9 @@ int os_az_set_layout(os_engine* e, int32_t layout);
 /* The kernel the last os_az_prepare* chose (OS_LAYOUT_WAVE or OS_LAYOUT_LANE),
  * AUTO resolved by the engine's own rule. */
 int os_az_get_layout(os_engine* e, int32_t* layout);
+/* Evaluator requests the batch's steps have written so far (all steps since
+ * os_az_prepare*, counted on the device by the step's request reduction). */
+int os_az_requests(os_engine* e, int64_t* total);
 /* Measurement: with timing on, every search run of the engine (the batch,
  * stateful and rerun paths) is bracketed by a HIP event pair on its stream;
  * os_engine_last_run_ms waits for the last one and returns its duration, so

@@ -1071,7 +1071,7 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
   // (k_az_pending).  A single counter took every search's atomic at one
   // address: k_waz_step 0.208 -> 0.061 ms per launch at 16384 searches.
   {
-    const size_t sb = sizeof(int32_t) * osm::kAzShards * osm::kAzShardStride;
+    const size_t sb = sizeof(int32_t) * osm::kAzShards * osm::kAzShardStride + 64;  // + total
     if ((rc = e->d_az_shards.ensure(sb))) return rc;
     HIP_TRY(hipMemset(e->d_az_shards.p, 0, sb));
   }
@@ -1730,6 +1730,16 @@ int os_az_tree_priors(os_engine* e, int64_t r, int64_t count, double* prior) {
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipMemcpy(prior, static_cast<const double*>(e->d_az_prior.p) + r * e->cap, count * 8,
                     hipMemcpyDeviceToHost));
+  return OS_OK;
+}
+
+int os_az_requests(os_engine* e, int64_t* total) {
+  if (!e || !total) return Fail(OS_ERR_INVALID, "null argument");
+  if (!e->az_ready) return Fail(OS_ERR_INVALID, "no os_az_prepare batch");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(total, static_cast<int32_t*>(e->d_az_shards.p) + osm::kAzShards * osm::kAzShardStride,
+                    8, hipMemcpyDeviceToHost));
   return OS_OK;
 }
 

@@ -2073,7 +2073,8 @@ template <class G>
 size_t AzSlotBytes() { return sizeof(AzSlot<G>); }
 
 // Sums the step's request shards into *pending and zeroes them (one
-// workgroup, one shard per thread).
+// workgroup, one shard per thread); the batch's running request total (an
+// int64 after the shards, os_az_requests) grows by the same count.
 static __global__ __launch_bounds__(kAzShards) void k_az_pending(int32_t* shards, int32_t* pending) {
   __shared__ int32_t part[kAzShards / 64];
   const int t = threadIdx.x;
@@ -2086,6 +2087,7 @@ static __global__ __launch_bounds__(kAzShards) void k_az_pending(int32_t* shards
     int32_t s = 0;
     for (int i = 0; i < kAzShards / 64; ++i) s += part[i];
     *pending = s;
+    *reinterpret_cast<int64_t*>(shards + kAzShards * kAzShardStride) += s;
   }
 }
 

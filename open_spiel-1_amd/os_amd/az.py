@@ -277,6 +277,9 @@ class ExternalEvaluatorSearch:
         break
     o = E._alloc_outputs(R, self.eng.max_children)
     check(lib.os_az_fetch(self.eng._h, self.eng.max_children, *E._out_ptrs(o)))
+    tot = np.zeros(1, np.int64)  # every step's requests, counted on the device
+    check(lib.os_az_requests(self.eng._h, ptr(tot)))
+    self.requests = int(tot[0])
     if bot_rng is not None:
       keys = np.zeros((R, 624), np.uint32)
       pos = np.zeros(R, np.int32)
@@ -289,14 +292,12 @@ class ExternalEvaluatorSearch:
     """Captures one round into a HIP graph and replays it until no search
     is pending (checked every `batch` rounds)."""
     torch = self.torch
-    total = torch.zeros(1, dtype=torch.int64, device=self.device)
     g = torch.cuda.CUDAGraph()
     st.synchronize()
     with torch.cuda.graph(g):
       cs = torch.cuda.current_stream(self.device)
       check(lib.os_az_step_async(self.eng._h, cs.cuda_stream))
       _evaluate(evaluator, obs, legal, kind, prior, value)
-      total.add_(pending)
     with torch.cuda.stream(st):
       while True:
         for _ in range(batch):
@@ -308,7 +309,6 @@ class ExternalEvaluatorSearch:
         if int(pend_host[0]) == 0:
           break
     st.synchronize()
-    self.requests += int(total.item())
 
   def stage(self, root_actions, root_offsets, bot_seeds, puct=True, max_simulations=100,
             uct_c=2.0, solve=True, max_memory_mb=1000, dirichlet_alpha=0.0,
