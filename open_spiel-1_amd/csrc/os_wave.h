@@ -1676,13 +1676,27 @@ __device__ int pig_rollout_wave(Pig::State s, const GameCfg& g, WaveMt& ev) {
     if (!at_chance) {
       const bool only_stop = cs + tt >= win;  // Pig::legal: stop alone
       const int nw = Policy == kPolicyCpp ? 2 : (only_stop ? 0 : 1);
-      need(nw);
-      const int a = only_stop ? 1 : static_cast<int>((rl32(pk, c) >> 8) & 1u);
+      need(nw + 2);  // the decision's words and the chance pair a roll draws next
+      const uint32_t pd = rl32(pk, c), pc = rl32(pk, c + nw);
+      const int a = only_stop ? 1 : static_cast<int>((pd >> 8) & 1u);
       c += nw;
       used += nw;
       moves++;
-      if (a == 0) {  // roll
-        at_chance = true;
+      if (a == 0) {  // roll: the chance node follows in the same step
+        if (moves >= hz) {
+          at_chance = true;
+          break;
+        }
+        const int o = static_cast<int>(pc & 0xffu) + 1;  // ChanceOutcomes()[k]: k + 1
+        c += 2;
+        used += 2;
+        if (o == 1) {  // pig.cc:208-213
+          tt = 0;
+          tp = tp + 1 < np ? tp + 1 : 0;
+          cs = static_cast<int>(rl32(sc, tp));
+        } else {
+          tt += o + 1;
+        }
         continue;
       }
       cs += tt;  // stop: bank the turn total
