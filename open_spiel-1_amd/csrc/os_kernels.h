@@ -1765,8 +1765,12 @@ __global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
 #ifndef OS_ROLL_AOS
 #define OS_ROLL_AOS 0
 #endif
+// Minimum waves per SIMD asked of k_rollouts' register allocation (A/B knob).
+#ifndef OS_ROLL_OCC
+#define OS_ROLL_OCC 1
+#endif
 template <class G>
-__global__ __launch_bounds__(64) void k_rollouts(RollArgs a) {
+__global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   // OS_ROLL_MT (A/B): 0 MtStreamSoA, 1 MtStreamReg (first block from seed

@@ -243,9 +243,126 @@ int AzRunOne(const HostGame& game, const HostState& root, const SearchParams& sp
   *nd = sl->res.nodes;
   return 0;
 }
+// One python/algorithms/mcts.py search (numpy policy) with an external
+// evaluator, az_step on the host: the bot's RandomState continues from
+// (key, pos) and is written back; `noise` (or null) is the caller's
+// RandomState.dirichlet draw for the root's legal actions.
+template <class G>
+int AzRunNumpy(const HostGame& game, const HostState& root, const SearchParams& sp, int puct,
+               uint32_t* key, int32_t* pos, const double* noise, double eps, hc_az_cb cb,
+               int mc, int32_t* ca, int32_t* cn, double* cw, double* cp, int8_t* co,
+               int32_t* nch, int32_t* rn, double* rw, int64_t* ba) {
+  const int A = game.cfg.num_actions;
+  const int obs_size = ObservationShape(game, nullptr);
+  const uint32_t cap = 1 + static_cast<uint32_t>(sp.max_simulations) * game.cfg.max_children;
+  std::vector<Node<double>> nodes(cap);
+  std::vector<double> prior(cap);
+  MtStream bot{key, *pos, 1, 0};
+  std::vector<float> obs(obs_size);
+  std::vector<uint8_t> legal(A);
+  std::vector<double> pri(A);
+  double value = 0;
+  int32_t kind = 0;
+  AzIo io{&kind, obs.data(), legal.data(), pri.data(), &value};
+  auto sl = std::make_unique<AzSlot<G>>();
+  std::memset(sl.get(), 0, sizeof(AzSlot<G>));
+  const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
+  sl->s = rs;
+  typename G::Ctx ctx;
+  if constexpr (G::State::kNeedsLog) {
+    std::memset(static_cast<void*>(&ctx), 0, sizeof ctx);
+    ctx.zob = game.zob.data();
+    ctx.base = root.hashes.data();
+    ctx.n_base = static_cast<int32_t>(root.hashes.size());
+    ctx.n_heads = game.cfg.rows * game.cfg.cols + 1;
+  }
+  AzNoise nz{noise, 0, eps};
+  for (;;) {
+    az_step<G>(game.cfg, sp, puct, rs, *sl, nodes.data(), prior.data(), nullptr, cap, bot, io,
+               obs_size, A, ctx, nz, /*np_policy=*/true);
+    if (kind == kAzNone) break;
+    std::fill(pri.begin(), pri.end(), 0.0);
+    cb(obs.data(), obs_size, legal.data(), A, kind, pri.data(), &value);
+  }
+  if (sl->res.status != kOk) {
+    g_err = "search status " + std::to_string(sl->res.status);
+    return -4;
+  }
+  *pos = bot.idx >= kMtN ? kMtN : bot.idx;  // numpy (key, pos): the block is fully twisted
+  if (!bot.pre && bot.idx < kMtN) {
+    // a block being twisted in place: finish it (numpy keeps whole blocks)
+    for (int i = bot.idx; i < kMtN; ++i) {
+      const int i1 = (i + 1 == kMtN) ? 0 : i + 1;
+      const int im = (i + kMtM >= kMtN) ? i + kMtM - kMtN : i + kMtM;
+      const uint32_t y = (key[i] & 0x80000000u) | (key[i1] & 0x7fffffffu);
+      key[i] = key[im] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+  }
+  const int P0 = G::to_move(rs);
+  const Node<double>& r0 = nodes[0];
+  *nch = r0.nchild;
+  for (int k = 0; k < r0.nchild && k < mc; ++k) {
+    const Node<double>& c = nodes[r0.first + k];
+    ca[k] = c.action;
+    cn[k] = c.n;
+    cw[k] = c.w;
+    cp[k] = prior[r0.first + k];
+    co[k] = c.out == kUnsolved ? kUnsolved : (P0 == 0 ? c.out : -c.out);
+  }
+  *rn = r0.n;
+  *rw = r0.w;
+  const int b = best_child(nodes.data(), P0);
+  *ba = b < 0 ? -1 : nodes[r0.first + b].action;
+  return 0;
+}
 }  // namespace
 
 extern "C" {
+
+int hc_az_numpy(const char* game_string, const int64_t* history, int64_t n_history,
+                double uct_c, int32_t max_simulations, int32_t solve, int32_t puct,
+                uint32_t* key, int32_t* pos, const double* noise, double eps, hc_az_cb cb,
+                int32_t max_children, int32_t* child_action, int32_t* child_n, double* child_w,
+                double* child_prior, int8_t* child_out, int32_t* nchild, int32_t* root_n,
+                double* root_w, int64_t* best_action) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty()) {
+    g_err = err;
+    return -1;
+  }
+  std::vector<double> lut(max_simulations + 2);
+  for (size_t i = 0; i < lut.size(); ++i) lut[i] = std::log(static_cast<double>(i));
+  SearchParams sp;
+  std::memset(&sp, 0, sizeof sp);
+  sp.uct_c = uct_c;
+  sp.max_simulations = max_simulations;
+  sp.n_rollouts = 1;
+  sp.solve = solve;
+  sp.max_nodes = 1;  // mcts.py never garbage-collects
+  sp.policy = kPolicyNumpy;
+  sp.log_lut = lut.data();
+  HostState hs;
+  hs.game = &game;
+  StateInit(&hs);
+  for (int64_t i = 0; i < n_history; ++i) StateApply(&hs, history[i]);
+  int rc = 0;
+#define HC_AZN(G)                                                                            \
+  rc = AzRunNumpy<G>(game, hs, sp, puct, key, pos, noise, eps, cb, max_children, child_action, \
+                     child_n, child_w, child_prior, child_out, nchild, root_n, root_w,          \
+                     best_action)
+  switch (game.cfg.kind) {
+    case kTicTacToe: HC_AZN(TicTacToe); break;
+    case kConnectFour: HC_AZN(ConnectFour); break;
+    case kBreakthrough: HC_AZN(Breakthrough); break;
+    case kHex: HC_AZN(Hex); break;
+    case kGo: HC_AZN(Go); break;
+    default: g_err = "unsupported"; return -2;
+  }
+#undef HC_AZN
+  return rc;
+}
 
 int hc_az_batch(const char* game_string, int64_t num_roots, const int64_t* root_actions,
                 const int64_t* root_offsets, double uct_c, int32_t max_simulations,

@@ -254,3 +254,46 @@ def rollouts_go_bloom(game_string, history, seeds):
   if rc:
     raise RuntimeError(lib().hc_last_error().decode())
   return out
+
+
+def az_numpy(game_string, history, key, pos, eval_fn, max_children, uct_c=2.0,
+             max_simulations=100, solve=False, puct=True, noise=None, eps=0.0):
+  """One python/algorithms/mcts.py search with an external evaluator on the
+  host (csrc/os_az.h az_step, numpy policy): the bot RandomState continues
+  from (key, pos); returns (root outputs, key', pos').  noise: the caller's
+  RandomState.dirichlet draw for the root (legal order) or None."""
+  L = lib()
+  vp = ctypes.c_void_p
+  L.hc_az_numpy.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.c_double,
+                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp, vp,
+                            ctypes.c_double, AZ_CB, ctypes.c_int32] + [vp] * 9
+  mc = max_children
+  o = dict(child_action=np.full(mc, -1, np.int32), child_n=np.zeros(mc, np.int32),
+           child_w=np.zeros(mc, np.float64), child_prior=np.zeros(mc, np.float64),
+           child_out=np.full(mc, 2, np.int8), nchild=np.zeros(1, np.int32),
+           root_n=np.zeros(1, np.int32), root_w=np.zeros(1, np.float64),
+           best_action=np.zeros(1, np.int64))
+
+  def cb(obs, obs_size, legal, A, kind, prior_out, value_out):
+    ob = np.ctypeslib.as_array(obs, shape=(obs_size,)).copy()
+    lg = np.ctypeslib.as_array(legal, shape=(A,)).copy()
+    pr, v = eval_fn(ob, lg, int(kind))
+    for a in range(A):
+      prior_out[a] = float(pr[a])
+    value_out[0] = float(v)
+    return 0
+
+  fn = AZ_CB(cb)
+  h = np.ascontiguousarray(history, np.int64)
+  k = np.array(key, np.uint32).copy()
+  p = np.array([pos], np.int32)
+  nz = None if noise is None else np.ascontiguousarray(noise, np.float64)
+  rc = L.hc_az_numpy(game_string.encode(), h.ctypes.data, len(h), uct_c, max_simulations,
+                     int(solve), int(puct), k.ctypes.data, p.ctypes.data,
+                     None if nz is None else nz.ctypes.data, float(eps), fn, mc,
+                     *[o[x].ctypes.data for x in ("child_action", "child_n", "child_w",
+                                                  "child_prior", "child_out", "nchild",
+                                                  "root_n", "root_w", "best_action")])
+  if rc:
+    raise RuntimeError(L.hc_last_error().decode())
+  return o, k, int(p[0])

@@ -128,3 +128,47 @@ def test_gpu_az_bot_step_matches_search(require_gpu):
     assert a == want["best_action"]
     assert _rs_state(bot._random_state) == want["rng_after"]
     state.apply_action(a)
+
+
+@pytest.mark.parametrize("case", _cases(), ids=CASE_IDS)
+def test_host_compiled_az_kernel_equals_reference_az_bot(case):
+  """The device search's own code (csrc/os_az.h az_step with the numpy
+  policy), compiled for the host (tests/hostcheck), against the same
+  fixtures: the bot's RandomState draws the root noise where mcts.py:314-316
+  does, the engine continues the stream for the expansions' shuffles."""
+  import pyspiel
+  import hostcheck_lib as hc
+  game = pyspiel.load_game(case["game"])
+  A = game.num_distinct_actions()
+  model = ToyModel(int(np.prod(game.observation_tensor_shape())), A)
+
+  def ev(obs, legal, kind):
+    v, p = model.inference(obs[None].astype(np.float64), legal[None].astype(np.int64))
+    return p[0], v[0, 0]
+
+  cfg = case["config"]
+  rs = np.random.RandomState()
+  rs.seed(case["seed"])
+  state = game.new_initial_state()
+  mc = max(A, 1)
+  for want in case["searches"]:
+    noise = None
+    if not case["evaluation"] and cfg["max_simulations"] >= 2:
+      n = len(state.legal_actions())
+      noise = np.zeros(mc)
+      noise[:n] = rs.dirichlet([cfg["policy_alpha"]] * n)
+    st = rs.get_state()
+    o, key, pos = hc.az_numpy(case["game"], state.history(), st[1], st[2], ev, mc,
+                              uct_c=cfg["uct_c"], max_simulations=cfg["max_simulations"],
+                              solve=False, puct=True, noise=noise,
+                              eps=cfg["policy_epsilon"] if noise is not None else 0.0)
+    nc = int(o["nchild"][0])
+    got = [[int(o["child_action"][k]), int(o["child_n"][k]), float(o["child_w"][k]),
+            float(o["child_prior"][k])] for k in range(nc)]
+    assert got == [c[:4] for c in want["children"]], (case["game"], case["seed"])
+    assert int(o["root_n"][0]) == want["root"]["explore_count"]
+    assert float(o["root_w"][0]) == want["root"]["total_reward"]
+    assert int(o["best_action"][0]) == want["best_action"]
+    rs.set_state(("MT19937", key, pos, st[3], st[4]))
+    assert _rs_state(rs) == want["rng_after"]
+    state.apply_action(want["best_action"])

@@ -12,7 +12,7 @@ for c in $CFGS; do
   rm -rf "$R/gpurun_out/pmc"
   EXTRA=""
   [ "$c" = az ] && EXTRA="--az-graph 0"  # eager rounds: one traced dispatch per k_az_step
-  BENCH_ARGS="--config $c --steps 2 --warmup 1 --no-cpu-baseline --parity-roots 0 --no-parity-sweep $EXTRA" \
+  BENCH_ARGS="--config $c --steps 2 --warmup 1 --no-cpu-baseline --parity-roots 0 --no-parity-sweep --no-configs $EXTRA" \
     bash "$R/tools/pmc.sh" "$P1" "$P2" FETCH_SIZE WRITE_SIZE || exit 1
   rm -rf "$R/gpurun_out/pmc_$c"
   mv "$R/gpurun_out/pmc" "$R/gpurun_out/pmc_$c"
