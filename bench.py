@@ -242,14 +242,13 @@ def main():
     ctx.dist.destroy_process_group()
 
 
-def _resolved_layout(game, R, layout):
-  """Mirror of ResolveLayout (os_engine.hip) for reporting."""
+def _resolved_layout(eng):
+  """The layout the engine ran the last prepared batch on (os_engine_get_layout:
+  OS_LAYOUT_AUTO resolved by the engine's own rule)."""
   from os_amd import _lib
-  if layout != _lib.LAYOUT_AUTO:
-    return "wave" if layout == _lib.LAYOUT_WAVE else "lane"
-  if game.startswith("go") and R >= 16384:
-    return "lane"  # k_lsearch (C++ policy)
-  return "wave"  # hex included: C++ policy, board_size 11
+  if not hasattr(eng, "layout"):  # --rehearse-host's host engine: the line
+    return "wave"                  # is a plumbing check, never a result
+  return "wave" if eng.layout() == _lib.LAYOUT_WAVE else "lane"
 
 
 def _base_line(args, ctx, metric, value, unit, elapsed, config):
@@ -326,6 +325,7 @@ def bench_search(args, ctx, layout):
   eng = ctx.engine(game)
   eng.set_arena_mode("reserved" if args.arena == "reserved" else "paged")
   eng.prepare(acts, offs, bot_seeds, eval_seeds, **params)
+  lay = _resolved_layout(eng)
   handle = ctx.handle
   for _ in range(max(args.warmup, 1)):  # at least one: it sizes the arena / page pool
     eng.run_async(handle)
@@ -380,7 +380,6 @@ def bench_search(args, ctx, layout):
                               args.cpu_seconds)
   if ctx.rank != 0:
     return None
-  lay = _resolved_layout(game, R, layout)
   metric = ("MCTS simulations/sec (random rollout) on connect_four at 1/2/4/8 MI355X"
             if args.config == "c2" else
             "MCTS simulations/sec (random rollout) on %s" % game)
@@ -440,6 +439,7 @@ def bench_root_parallel(args, ctx, layout):
     v, w = step()
     out = be.eng.fetch()
   arena0 = be.eng.arena_info()
+  lay = _resolved_layout(be.eng)
   sims_per_step = be.eng.last_sims()
   alg_bytes = be.eng.algorithmic_bytes(T)
   stats = be.eng.stats()
@@ -480,7 +480,6 @@ def bench_root_parallel(args, ctx, layout):
                               args.cpu_seconds)
   if ctx.rank != 0:
     return None
-  lay = _resolved_layout(game, T, layout)
   line = _base_line(args, ctx, "MCTS simulations/sec (random rollout) on %s, "
                     "root-parallel" % game, total_sims / elapsed, "sims/s", elapsed, {
                         "workload": "%s initial position, %d trees x %d sims per GPU, "

@@ -203,6 +203,11 @@ int os_engine_arena_info(os_engine* e, int64_t* out);
 int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
                       int64_t n_actions, int64_t n, int32_t n_rollouts,
                       const uint32_t* seeds, double* out_returns);
+/* The kernel layout the last os_engine_prepare ran the batch on
+ * (OS_LAYOUT_WAVE or OS_LAYOUT_LANE; OS_LAYOUT_AUTO resolved by the engine's
+ * own rule: go from 16384 C++-policy roots and boards above 11 x 11 take the
+ * lane layout, hex below 3 x 3 too, everything else the wave layout). */
+int os_engine_get_layout(os_engine* e, int32_t* layout);
 /* Kernel layout for os_rollouts_batch: OS_LAYOUT_LANE (default: one lane per
  * evaluator) or OS_LAYOUT_WAVE (one wave per evaluator, uniform game code). */
 int os_engine_set_rollout_layout(os_engine* e, int32_t layout);

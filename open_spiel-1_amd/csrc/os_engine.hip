@@ -558,6 +558,7 @@ int Prepare(os_engine* e, const os_mcts_params* p, int64_t R,
   HIP_TRY(hipSetDevice(e->device));
   e->params = *p;
   e->params.layout = ResolveLayout(e->game.cfg, p->layout, R, p->policy);
+  e->search_layout = e->params.layout;
   e->num_roots = R;
   const GameCfg& cfg = e->game.cfg;
   e->max_children = cfg.max_children;
@@ -1363,6 +1364,13 @@ int os_engine_fetch(os_engine* e, int32_t max_children, int32_t* child_action,
 }
 
 int64_t os_engine_last_sims(os_engine* e) { return e ? e->last_sims : -1; }
+
+int os_engine_get_layout(os_engine* e, int32_t* layout) {
+  if (!e || !layout) return Fail(OS_ERR_INVALID, "null argument");
+  if (e->search_layout < 0) return Fail(OS_ERR_INVALID, "no os_engine_prepare batch");
+  *layout = e->search_layout;
+  return OS_OK;
+}
 
 int os_engine_set_rollout_layout(os_engine* e, int32_t layout) {
   if (!e) return Fail(OS_ERR_INVALID, "null engine");

@@ -308,6 +308,7 @@ struct os_engine {
   int32_t hash_stride = 1;
   bool import_state = false;
   bool shared_stream = false;
+  int32_t search_layout = -1;  // layout of the last os_engine_prepare (AUTO resolved)
   int32_t rollout_layout = OS_LAYOUT_LANE;  // 4-140x faster than WAVE (profiles/r01)
   // prepared rollout batch
   int64_t roll_n = 0;

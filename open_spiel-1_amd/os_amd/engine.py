@@ -298,6 +298,12 @@ class Engine:
     check(lib.os_engine_fetch(self._h, self.max_children, *_out_ptrs(o)))
     return o
 
+  def layout(self):
+    """Kernel layout of the last prepared batch (_lib.LAYOUT_WAVE / LAYOUT_LANE)."""
+    out = np.zeros(1, np.int32)
+    check(lib.os_engine_get_layout(self._h, ptr(out)))
+    return int(out[0])
+
   def last_sims(self):
     return int(lib.os_engine_last_sims(self._h))
 

@@ -49,3 +49,27 @@ def test_engine_without_gpu_fails_loudly():
   from os_amd import engine
   with pytest.raises(RuntimeError):
     engine.Engine("connect_four")
+
+
+@pytest.mark.gpu
+def test_gpu_engine_reports_resolved_layout(require_gpu):
+  """os_engine_get_layout: the layout the last prepare resolved (AUTO by the
+  engine's own rule), which bench.py reports instead of a mirror of it."""
+  import numpy as np
+  from os_amd import _lib
+  from os_amd import engine as E
+  cases = (("connect_four", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_WAVE),
+           ("connect_four", 8, _lib.LAYOUT_LANE, _lib.LAYOUT_LANE),
+           ("hex(board_size=5)", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_WAVE),
+           ("hex(board_size=2)", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_LANE),
+           ("go(board_size=5)", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_WAVE),
+           ("go(board_size=5)", 16384, _lib.LAYOUT_AUTO, _lib.LAYOUT_LANE))
+  for game, R, asked, want in cases:
+    eng = E.Engine(game)
+    with pytest.raises(RuntimeError):
+      eng.layout()  # nothing prepared yet
+    acts = np.zeros(0, np.int64)
+    offs = np.zeros(R + 1, np.int64)
+    seeds = np.arange(R, dtype=np.uint32)
+    eng.prepare(acts, offs, seeds, seeds + np.uint32(1), max_simulations=4, layout=asked)
+    assert eng.layout() == want, (game, R, asked)
