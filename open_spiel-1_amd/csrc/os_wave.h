@@ -74,6 +74,18 @@
 #ifndef OS_PHASE_TIMING
 #define OS_PHASE_TIMING 0
 #endif
+// Phase builds only: the selection's parts for the non-go games, in the go
+// slots (tools/phase_single.py prints them as go_legal..go_score): before
+// the level loop, the level loop, after it (expansion included), and the
+// scoring inside the loop.
+#ifndef OS_PHASE_SEL
+#define OS_PHASE_SEL 0
+#endif
+// UCT screen: settle the argmax by one band ballot when the maximum is the
+// only child in the near-tie band (A/B knob; 0 = always the identity test).
+#ifndef OS_SCREEN_BAND
+#define OS_SCREEN_BAND 1
+#endif
 // Timing-only A/B switch (results not bit-exact): 1 skips the hex end-of-fill
 // relaxation, 2 the hex fill-order rank-select loop.
 #ifndef OS_AB_HEX
@@ -949,14 +961,25 @@ __device__ __forceinline__ int uct_argmax_screen_lf(const Node<int32_t>& c0, boo
   const float a1 = TwoSlots ? uct_screen_value(c1, in1, cp, lf, cf) : -__builtin_huge_valf();
   const int32_t k0 = f32_key(a0), k1 = f32_key(a1);
   const int32_t mk = wave_max_key<Lanes>(TwoSlots ? max(k0, k1) : k0);
+  const float e2 = (1.0f + fabsf(cf) * __builtin_amdgcn_sqrtf(lf)) * 0x1p-17f;  // 2E', lf >= 0
+  const float lo = key_f32(mk) - e2;
+#if OS_SCREEN_BAND
+  // The usual case: the maximum is the only child within the band, so no
+  // other child is near it and it is the argmax (the lane holding M is always
+  // in the band).  One ballot settles it; the identity test below runs only
+  // when two or more children share the band.
+  {
+    const uint64_t b0 = ballot(in0 && a0 >= lo);
+    const uint64_t b1 = TwoSlots ? ballot(in1 && a1 >= lo) : 0ull;
+    if (popc64(b0) + popc64(b1) == 1) return b0 ? static_cast<int>(ctz64(b0)) : 64 + static_cast<int>(ctz64(b1));
+  }
+#endif
   const uint64_t t0 = ballot(k0 == mk);
   const int j = t0 ? static_cast<int>(ctz64(t0)) : 64 + static_cast<int>(ctz64(ballot(k1 == mk)));
   const bool hi = TwoSlots && j >= 64;  // wave-uniform
   const int src = j & 63;
   const int32_t nj = rli(hi ? c1.n : c0.n, src), wj = rli(hi ? c1.w : c0.w, src);
   const int32_t oj = rli(static_cast<int32_t>(hi ? c1.out : c0.out), src);
-  const float e2 = (1.0f + fabsf(cf) * __builtin_amdgcn_sqrtf(lf)) * 0x1p-17f;  // 2E', lf >= 0
-  const float lo = key_f32(mk) - e2;
   const bool same0 = c0.n == nj && c0.w == wj && static_cast<int32_t>(c0.out) == oj;
   bool near = in0 && a0 >= lo && !same0;
   if (TwoSlots) {
@@ -2392,6 +2415,11 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
 #endif
     // ---- selection / expansion ----
     bool pending_expand = false;
+#if OS_PHASE_SEL
+    constexpr bool kSelPh = !std::is_same<G, Go>::value;
+    if (kSelPh) OS_PH_ADD(ph.c[kPhGoLegal], t_ph);
+    uint64_t t_loop = OS_PH_NOW();
+#endif
     for (;;) {
 #if OS_UNI_SEL == 1
       s = make_uniform(s);
@@ -2446,6 +2474,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
           if (!kLazyLog) lg1 = sp.log_lut[c1.n];
         }
       }
+#if OS_PHASE_SEL
+      const uint64_t t_sc = OS_PH_NOW();
+#endif
       if constexpr (kPuct) {
         // PUCTValue (mcts.cc:102-111): unvisited children are not +inf, so
         // every child is scored in f64 (cur_logN holds sqrt(N) here).
@@ -2484,6 +2515,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         chosen = wave_argmax2<WW::kLanes, WW::kTwoSlots>(v0, v1);
       }
       if (depth == 0) root_k = chosen;
+#if OS_PHASE_SEL
+      if (kSelPh) OS_PH_ADD(ph.c[kPhGoScore], t_sc);
+#endif
       const int src = chosen & 63;
       const bool hi = WW::kTwoSlots && chosen >= 64;  // wave-uniform
       const Node<R> bc = hi ? c1 : c0;
@@ -2522,6 +2556,10 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
         pe.w = c_w;
       }
     }
+#if OS_PHASE_SEL
+    if (kSelPh) OS_PH_ADD(ph.c[kPhGoApply], t_loop);
+    t_loop = OS_PH_NOW();
+#endif
     if (pending_expand) {
       int chosen;
       uint32_t c_action, c_first;
@@ -2651,6 +2689,9 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     }
     c_depth.max(depth);
     __builtin_amdgcn_wave_barrier();
+#if OS_PHASE_SEL
+    if (kSelPh) OS_PH_ADD(ph.c[kPhGoInsert], t_loop);
+#endif
     OS_PH_ADD(ph.c[kPhSelect], t_ph);
     t_ph = OS_PH_NOW();
     {
