@@ -129,7 +129,10 @@ enum PhaseId { kPhSelect = 0, kPhExpand, kPhRollout, kPhBackup, kPhSolver, kPhTa
                kPhTwist, kPhTotal,
                // go rollout breakdown (inside kPhRollout): legal + draw, apply
                // (with the superko insert), the insert alone, the final score
-               kPhGoLegal, kPhGoApply, kPhGoInsert, kPhGoScore, kNumPhases };
+               kPhGoLegal, kPhGoApply, kPhGoInsert, kPhGoScore,
+               // go apply on the wave (inside kPhGoApply): own chains joined,
+               // opponent chains (captures), the mover's chain, the rest
+               kPhX0, kPhX1, kPhX2, kPhX3, kNumPhases };
 struct PhaseCycles {
   uint64_t c[kNumPhases];
 };
@@ -2002,6 +2005,9 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const 
     sd.me = sd.them;
     sd.them = t;
   } else {
+#if OS_PHASE_TIMING
+    uint64_t tx = OS_PH_NOW();
+#endif
     const B128 pb = bit128(a);
     const B128 nb = nbl.at(a);
     const B128 own0 = sd.me;
@@ -2018,6 +2024,10 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const 
       lab.relabel(L, a);
     }
     lab.set(a, a);
+#if OS_PHASE_TIMING
+    OS_PH_ADD(ctx.sub[kPhX0], tx);
+    tx = OS_PH_NOW();
+#endif
     int captured = 0;
     int cap_pt = -1;
     B128 atari = s.atari;
@@ -2043,6 +2053,10 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const 
       }
       atari = (atari & ~ch) | sel128(popc(libs) == 1, ch, b128(0, 0));
     }
+#if OS_PHASE_TIMING
+    OS_PH_ADD(ctx.sub[kPhX1], tx);
+    tx = OS_PH_NOW();
+#endif
     // The mover's chain (label a) and, after captures, the own chains next to
     // the captured stones.  (Skipping the liberty counts where the atari set
     // or two empty neighbours settle them was measured slower here: 1.70e7 ->
@@ -2057,10 +2071,17 @@ __device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const 
         atari = (atari & ~cx) | sel128(popc(nbl.any(cx) & E) == 1, cx, b128(0, 0));
       }
     }
+#if OS_PHASE_TIMING
+    OS_PH_ADD(ctx.sub[kPhX2], tx);
+    tx = OS_PH_NOW();
+#endif
     s.atari = atari;
     sd.me = opp;  // the next player's stones
     sd.them = own;
     s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
+#if OS_PHASE_TIMING
+    OS_PH_ADD(ctx.sub[kPhX3], tx);
+#endif
     if (!ctx.insert(s.hash, captured > 0, popc(own) + popc(opp))) s.flags |= Go::kSuperko;
   }
   s.to_play = static_cast<uint8_t>(1 - c);

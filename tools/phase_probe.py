@@ -16,7 +16,7 @@ from os_amd import _lib  # noqa: E402
 from os_amd import engine as E  # noqa: E402
 
 PHASES = ("select", "expand", "rollout", "backup", "solver", "tail", "twist", "total",
-          "go_legal", "go_apply", "go_insert", "go_score")
+          "go_legal", "go_apply", "go_insert", "go_score", "x_own", "x_opp", "x_mover", "x_rest")
 GAMES = (("connect_four", 8), ("tic_tac_toe", 4), ("breakthrough", 6), ("hex", 6),
          ("go(board_size=9)", 6))
 
