@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Full-size parity: the BASELINE configs searched on the GPU at their full
+size and compared with the oracle on EVERY root, tree and playout (test
+infrastructure: the oracle is the checker, never timed here).
+
+  python tools/full_parity.py [--out profiles/r05/full_parity.json]
+
+- C2: connect_four, all 4096 roots x 1024 sims (every root checked);
+- C3: breakthrough 8x8, 65536 roots x 2048 sims, reserved arena and paged
+  arena: the two runs equal each other and the oracle on all 65536 roots;
+- C4: hex 11, 8192 trees x 2048 sims of the initial position (the trees a
+  root-parallel rank grows, tree t seeded t / t + 2^20), reserved and paged,
+  all 8192 trees;
+- C5: go 9x9, all 2^20 playouts (returns per seed);
+- g9: go 9x9, 65536 roots x 256 sims on the lane layout, all roots.
+Every output field (children in tree order, visit counts, rewards, solver
+outcomes, root statistics, best action) must be equal bit for bit.  The oracle
+runs on the host cores (ctypes releases the GIL, so C5's playouts are split
+over threads).
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "open_spiel-1_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import bench  # noqa: E402  (CONFIGS, EVAL_OFFSET, host_cores)
+import oracle_lib  # noqa: E402
+from os_amd import _lib  # noqa: E402
+from os_amd import engine as E  # noqa: E402
+
+
+CHUNK = 4096  # roots per oracle call
+
+
+def compare(out, ref, rows):
+  bad = {}
+  for k in E.OUTPUT_KEYS:
+    a = np.asarray(out[k])[rows]
+    b = np.asarray(ref[k])
+    if a.shape != b.shape:
+      bad[k] = "shape %r vs %r" % (a.shape, b.shape)
+      continue
+    diff = np.nonzero((a != b).reshape(len(rows), -1).any(axis=1))[0]
+    if len(diff):
+      bad[k] = int(len(diff))
+  return bad
+
+
+def oracle_batch(game, acts, offs, bot, ev, sims, max_children, threads):
+  return oracle_lib.Game(game).mcts_batch(acts, offs, bot, ev, uct_c=2.0, max_simulations=sims,
+                                          max_children=max_children, threads=threads)
+
+
+def sub_batch(acts, offs, lo, hi):
+  a = acts[offs[lo]:offs[hi]]
+  o = offs[lo:hi + 1] - offs[lo]
+  return a, o
+
+
+def search_case(name, game, R, sims, plies, threads, check, layout=_lib.LAYOUT_AUTO,
+                paged=False, initial=False):
+  t0 = time.time()
+  if initial:
+    acts, offs = np.zeros(0, np.int64), np.zeros(R + 1, np.int64)
+  else:
+    acts, offs = E.make_roots(game, R, seed_base=1000, max_plies=plies)
+  gid = np.arange(R, dtype=np.uint32)
+  bot, ev = gid, gid + np.uint32(bench.EVAL_OFFSET)
+  eng = E.Engine(game)
+  params = dict(uct_c=2.0, max_simulations=sims, n_rollouts=1, max_memory_mb=1000, solve=True,
+                layout=layout)
+  eng.prepare(acts, offs, bot, ev, **params)
+  eng.run_async()
+  out = eng.fetch()
+  res = {"roots": R, "sims": sims, "layout": "wave" if eng.layout() == _lib.LAYOUT_WAVE else "lane"}
+  if paged:  # the same batch again on the page pool the first run sized
+    eng.set_arena_mode("paged")
+    eng.prepare(acts, offs, bot, ev, **params)
+    eng.run_async()
+    out_p = eng.fetch()
+    res["arena"] = eng.arena_info()
+    bad = {k: int(np.count_nonzero((np.asarray(out[k]) != np.asarray(out_p[k])).reshape(R, -1)
+                                   .any(axis=1))) for k in E.OUTPUT_KEYS}
+    res["paged_equals_reserved_all_roots"] = not any(bad.values())
+    res["paged_vs_reserved_mismatch_roots"] = {k: v for k, v in bad.items() if v}
+  checked, bad = 0, {}
+  for lo0, hi0 in check:
+    for lo in range(lo0, hi0, CHUNK):  # a progress line per chunk
+      hi = min(lo + CHUNK, hi0)
+      a, o = sub_batch(acts, offs, lo, hi)
+      ref = oracle_batch(game, a, o, bot[lo:hi], ev[lo:hi], sims, eng.max_children, threads)
+      for k, v in compare(out, ref, np.arange(lo, hi)).items():
+        bad[k] = bad.get(k, 0) + (v if isinstance(v, int) else 0)
+      checked += hi - lo
+      print("  %s: %d / %d roots checked, mismatching fields %r" % (name, checked, R, bad),
+            flush=True)
+  res.update({"roots_checked": checked, "ranges": check, "bit_exact": not bad,
+              "mismatch_roots": bad, "seconds": round(time.time() - t0, 1)})
+  print(name, json.dumps(res), flush=True)
+  return res
+
+
+def playout_case(threads):
+  t0 = time.time()
+  game = "go(board_size=9)"
+  n = 1 << 20
+  seeds = np.arange(n, dtype=np.uint32)
+  eng = E.Engine(game)
+  eng.rollouts_prepare([], seeds)
+  eng.rollouts_run_async()
+  out = eng.rollouts_fetch()
+  chunks = np.array_split(np.arange(n), threads * 4)
+
+  def ref_chunk(ix):
+    return ix, oracle_lib.Game(game).rollouts([], seeds[ix])
+
+  mism = 0
+  with cf.ThreadPoolExecutor(threads) as pool:
+    for ix, r in pool.map(ref_chunk, chunks):
+      mism += int(np.count_nonzero((r != out[ix]).any(axis=1)))
+  res = {"playouts": n, "playouts_checked": n, "bit_exact": mism == 0, "mismatches": mism,
+         "seconds": round(time.time() - t0, 1)}
+  print("c5", json.dumps(res), flush=True)
+  return res
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "full_parity.json"))
+  ap.add_argument("--only", default="")
+  args = ap.parse_args()
+  threads = bench.host_cores()[0]
+  cases = {}
+  only = args.only.split(",") if args.only else None
+  want = lambda c: only is None or c in only  # noqa: E731
+  if want("c2"):
+    cases["c2"] = search_case("c2", "connect_four", 4096, 1024, 8, threads, [(0, 4096)])
+  if want("c5"):
+    cases["c5"] = playout_case(threads)
+  if want("g9"):
+    cases["g9"] = search_case("g9", "go(board_size=9)", 65536, 256, 6, threads,
+                              [(0, 65536)], layout=_lib.LAYOUT_LANE)
+  if want("c4"):
+    cases["c4"] = search_case("c4", "hex(board_size=11)", 8192, 2048, 0, threads,
+                              [(0, 8192)], initial=True, paged=True)
+  if want("c3"):
+    cases["c3"] = search_case("c3", "breakthrough(rows=8,columns=8)", 65536, 2048, 6, threads,
+                              [(0, 65536)], paged=True)
+  summary = {"host_threads": threads, "all_bit_exact": all(c["bit_exact"] and
+                                                            c.get("paged_equals_reserved_all_roots",
+                                                                  True)
+                                                            for c in cases.values()),
+             "cases": cases}
+  os.makedirs(os.path.dirname(args.out), exist_ok=True)
+  with open(args.out, "w") as f:
+    json.dump(summary, f, indent=1)
+  print("full parity all_bit_exact=%s" % summary["all_bit_exact"], flush=True)
+  return 0 if summary["all_bit_exact"] else 1
+
+
+if __name__ == "__main__":
+  sys.exit(main())
