@@ -12,7 +12,9 @@ infrastructure: the oracle is the checker, never timed here).
   root-parallel rank grows, tree t seeded t / t + 2^20), reserved and paged,
   all 8192 trees;
 - C5: go 9x9, all 2^20 playouts (returns per seed);
-- g9: go 9x9, 65536 roots x 256 sims on the lane layout, all roots.
+- g9: go 9x9, 65536 roots x 256 sims on the lane layout, all roots;
+- sp: connect_four self-play, all 4096 games x 256 sims per move (moves,
+  lengths, returns and per-move visit rows).
 Every output field (children in tree order, visit counts, rewards, solver
 outcomes, root statistics, best action) must be equal bit for bit.  The oracle
 runs on the host cores (ctypes releases the GIL, so C5's playouts are split
@@ -133,6 +135,39 @@ def playout_case(threads):
   return res
 
 
+def selfplay_case(threads):
+  t0 = time.time()
+  _, game, G, sims, plies = bench.CONFIGS["sp"]
+  acts, offs = E.make_roots(game, G, seed_base=1000, max_plies=plies)
+  gid = np.arange(G, dtype=np.uint32)
+  bot = np.stack([2 * gid, 2 * gid + 1], axis=1).astype(np.uint32)
+  ev = gid + np.uint32(bench.EVAL_OFFSET)
+  eng = E.Engine(game)
+  L = eng.max_game_length
+  eng.selfplay_prepare(acts, offs, bot, ev, max_len=L, record_visits=True,
+                       max_simulations=sims, uct_c=2.0)
+  eng.selfplay_run_async()
+  out = eng.selfplay_fetch()
+  bad, checked = {}, 0
+  for lo in range(0, G, 1024):
+    hi = min(lo + 1024, G)
+    a, o = sub_batch(acts, offs, lo, hi)
+    ref = oracle_lib.Game(game).selfplay(a, o, bot[lo:hi], ev[lo:hi], L, max_simulations=sims,
+                                         threads=threads)
+    for k in ("actions", "length", "returns", "visits"):
+      n = int(np.count_nonzero((np.asarray(out[k][lo:hi]) != ref[k]).reshape(hi - lo, -1)
+                               .any(axis=1)))
+      if n:
+        bad[k] = bad.get(k, 0) + n
+    checked += hi - lo
+    print("  sp: %d / %d games checked, mismatching fields %r" % (checked, G, bad), flush=True)
+  res = {"games": G, "sims_per_move": sims, "moves": int(out["length"].sum()),
+         "games_checked": checked, "bit_exact": not bad, "mismatch_games": bad,
+         "seconds": round(time.time() - t0, 1)}
+  print("sp", json.dumps(res), flush=True)
+  return res
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "full_parity.json"))
@@ -149,6 +184,8 @@ def main():
   if want("g9"):
     cases["g9"] = search_case("g9", "go(board_size=9)", 65536, 256, 6, threads,
                               [(0, 65536)], layout=_lib.LAYOUT_LANE)
+  if want("sp"):
+    cases["sp"] = selfplay_case(threads)
   if want("c4"):
     cases["c4"] = search_case("c4", "hex(board_size=11)", 8192, 2048, 0, threads,
                               [(0, 8192)], initial=True, paged=True)
