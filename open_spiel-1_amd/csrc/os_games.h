@@ -530,6 +530,49 @@ struct GoCtxT {
   // LDS next to the bucket heads).
   uint32_t* bloom = nullptr;
   static constexpr int kBloomWords = 16;  // 512 bits, 2 bits per position
+  // Optional write-combining of the log (k_lsearch; nullptr: none).  A lane's
+  // log entries land in lines no other lane shares, one 12-byte entry per
+  // move, so the L2 writes back partly written lines; with wlog / wlink set,
+  // the open group of kWg entries lives in LDS (entry e at [(e % kWg) * wst])
+  // and goes out as whole 64-byte (hashes) / 32-byte (links) stores once full.
+  // Entries below the open group are in memory, those in it only in LDS.
+  uint64_t* wlog = nullptr;
+  L* wlink = nullptr;
+  int32_t wst = 64;
+  static constexpr int kWg = 8;
+
+  OS_HD bool in_wbuf(int e) const { return wlog != nullptr && e >= (n_log & ~(kWg - 1)); }
+  OS_HD uint64_t log_at(int e) const {
+    return in_wbuf(e) ? wlog[(e & (kWg - 1)) * wst] : log[static_cast<int64_t>(e) * stride];
+  }
+  OS_HD L link_at(int e) const {
+    return in_wbuf(e) ? wlink[(e & (kWg - 1)) * wst] : link[static_cast<int64_t>(e) * stride];
+  }
+  OS_HD void flush_group(int g) {  // entries g .. g + kWg - 1 to memory
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (stride == 1 && sizeof(L) == 4) {
+      uint4* dl = reinterpret_cast<uint4*>(log + g);
+#pragma unroll
+      for (int q = 0; q < kWg / 2; ++q) {
+        const uint64_t a = wlog[(2 * q) * wst], b = wlog[(2 * q + 1) * wst];
+        dl[q] = make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32),
+                           static_cast<uint32_t>(b), static_cast<uint32_t>(b >> 32));
+      }
+      uint4* dk = reinterpret_cast<uint4*>(link + g);
+#pragma unroll
+      for (int q = 0; q < kWg / 4; ++q)
+        dk[q] = make_uint4(static_cast<uint32_t>(wlink[(4 * q) * wst]),
+                           static_cast<uint32_t>(wlink[(4 * q + 1) * wst]),
+                           static_cast<uint32_t>(wlink[(4 * q + 2) * wst]),
+                           static_cast<uint32_t>(wlink[(4 * q + 3) * wst]));
+      return;
+    }
+#endif
+    for (int k = 0; k < kWg; ++k) {
+      log[static_cast<int64_t>(g + k) * stride] = wlog[k * wst];
+      link[static_cast<int64_t>(g + k) * stride] = wlink[k * wst];
+    }
+  }
 
   OS_HD static int bbit0(uint64_t h) { return static_cast<int>(h & 511u); }
   OS_HD static int bbit1(uint64_t h) { return static_cast<int>((h >> 9) & 511u); }
@@ -575,8 +618,7 @@ struct GoCtxT {
 #if OS_DEBUG_GOLOG
     int steps = 0;
 #endif
-    for (int e = head[stones * head_stride]; e;
-         e = static_cast<int>(link[static_cast<int64_t>(e - 1) * stride] & 0xFFFFu)) {
+    for (int e = head[stones * head_stride]; e; e = static_cast<int>(link_at(e - 1) & 0xFFFFu)) {
 #if OS_DEBUG_GOLOG
       if (++steps > cap + 2) {
         printf("golog cycle: stones %d head %d e %d n_log %d link %x\n", stones,
@@ -584,7 +626,7 @@ struct GoCtxT {
         return false;
       }
 #endif
-      if (log[static_cast<int64_t>(e - 1) * stride] == h) return true;
+      if (log_at(e - 1) == h) return true;
     }
     return false;
   }
@@ -594,14 +636,24 @@ struct GoCtxT {
   OS_HD int mark() const { return n_log; }
   OS_HD void rewind(int m) {
     static_assert(sizeof(L) == 4, "rewind needs the stone count in the link");
+    const int g0 = n_log & ~(kWg - 1);  // the open group before the rewind
     while (n_log > m) {
       --n_log;
-      const uint32_t lk = link[static_cast<int64_t>(n_log) * stride];
+      const uint32_t lk = (wlog && n_log >= g0) ? wlink[(n_log & (kWg - 1)) * wst]
+                                                 : link[static_cast<int64_t>(n_log) * stride];
       head[static_cast<int>(lk >> 16) * head_stride] = static_cast<H>(lk & 0xFFFFu);
+    }
+    if (wlog) {  // an earlier group is open now: its kept entries back into LDS
+      const int g = n_log & ~(kWg - 1);
+      if (g < g0)
+        for (int e = g; e < n_log; ++e) {
+          wlog[(e & (kWg - 1)) * wst] = log[static_cast<int64_t>(e) * stride];
+          wlink[(e & (kWg - 1)) * wst] = link[static_cast<int64_t>(e) * stride];
+        }
     }
     if (bloom) {  // a Bloom filter cannot forget: rebuilt from the entries kept
       bloom_clear();
-      for (int e = 0; e < n_log; ++e) bloom_add(log[static_cast<int64_t>(e) * stride]);
+      for (int e = 0; e < n_log; ++e) bloom_add(log_at(e));
     }
   }
   // Logs the position after a non-pass move; false if it was already present
@@ -612,14 +664,23 @@ struct GoCtxT {
     if (n_log < cap) {
       const int64_t e = static_cast<int64_t>(n_log) * stride;
       const int hk = stones * head_stride;
-      log[e] = h;
+      L lk;
       if constexpr (sizeof(L) == 4)
-        link[e] = (static_cast<uint32_t>(stones) << 16) | head[hk];
+        lk = (static_cast<uint32_t>(stones) << 16) | head[hk];
       else
-        link[e] = static_cast<L>(head[hk]);
+        lk = static_cast<L>(head[hk]);
+      if (wlog) {
+        const int w = (n_log & (kWg - 1)) * wst;
+        wlog[w] = h;
+        wlink[w] = lk;
+      } else {
+        log[e] = h;
+        link[e] = lk;
+      }
       head[hk] = static_cast<H>(n_log + 1);
       if (bloom) bloom_add(h);
       ++n_log;
+      if (wlog && (n_log & (kWg - 1)) == 0) flush_group(n_log - kWg);
     }
     return true;
   }

@@ -243,6 +243,16 @@ struct LCtx<Go> {
   }
 };
 
+// k_lsearch's go superko log written 8 entries at a time (GoCtxT::wlog; 1)
+// or entry by entry (0).  A/B knob.
+#ifndef OS_LS_LOGWC
+#define OS_LS_LOGWC 1
+#endif
+// k_lsearch's MT19937 streams: MtStreamWc (words stored 16 at a time; 1) or
+// MtStreamPf (word by word; 0).  A/B knob.
+#ifndef OS_LS_WC
+#define OS_LS_WC 1
+#endif
 // Timing-only attribution switches for k_lsearch's HBM traffic (results are
 // NOT the reference's; A/B builds only): bit 0 draws the MT19937 words from a
 // register xorshift (no stream memory), bit 1 logs no superko positions.
@@ -285,6 +295,11 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   // touch a new cache line per word; contiguous, a search reuses its lines.
 #if OS_LS_AB & 1
   MtStreamNoMem bot, ev;
+#elif OS_LS_WC
+  // twisted words written 16 at a time from a lane-interleaved LDS buffer
+  __shared__ uint32_t mt_wb[2 * 16 * 64];
+  MtStreamWc bot{{a.mt + lr * 2 * kMtN, 1, 0, 0}, mt_wb + (threadIdx.x & 63), 64};
+  MtStreamWc ev{{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0}, mt_wb + 16 * 64 + (threadIdx.x & 63), 64};
 #else
   MtStreamPf bot{a.mt + lr * 2 * kMtN, 1, 0, 0};
   MtStreamPf ev{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0};
@@ -299,6 +314,17 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
   auto ctx = LCtx<G>::make(a, gr, lr, heads, lbloom);
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
+#if OS_LS_LOGWC
+  // go: the superko log's open 8-entry group in LDS (GoCtxT::wlog)
+  constexpr bool kLogWc = std::is_same<G, Go>::value;
+  __shared__ uint64_t ls_wlog[kLogWc ? GoCtx::kWg * 64 : 1];
+  __shared__ uint32_t ls_wlink[kLogWc ? GoCtx::kWg * 64 : 1];
+  if constexpr (kLogWc) {
+    ctx.wlog = ls_wlog + (threadIdx.x & 63);
+    ctx.wlink = ls_wlink + (threadIdx.x & 63);
+    ctx.wst = 64;
+  }
+#endif
 #if OS_LS_AB & 2
   if constexpr (G::State::kNeedsLog) ctx.cap = 0;
 #endif

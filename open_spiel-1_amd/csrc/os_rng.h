@@ -343,6 +343,87 @@ struct MtStreamPf {
   }
 };
 
+// MtStreamPf whose twisted words reach memory 16 at a time.  A lane of
+// k_lsearch runs its own search, so its stream stores land one word at a time
+// in lines the other 63 lanes never share; between two words of one lane the
+// wave writes 63 other lines, and the L2 evicts partly written lines --
+// written back as whole sectors (profiles/r04/g9_traffic: the streams were
+// about 2/3 of the written lines).  Here each word goes to a 16-word buffer
+// (wb, LDS, lane-interleaved: wb[k * wst]) and every 16th word writes the
+// group out as four 16-byte stores (stride 1; 624 = 39 x 16, so a block ends on
+// a full group).  Every word the twist reads back as "new" (s[i + 397 - 624],
+// s[0] for i = 623, the next block's read-ahead) lies in an earlier, already
+// stored group, and the "old" words it reads (s[i + 1], s[i + 397] below 624)
+// are not yet rewritten, so the stream is std::mt19937's word for word.
+struct MtStreamWc : MtStreamPf {
+  uint32_t* wb;
+  int wst;
+
+  OS_HD void flush(int c, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (n == 16 && stride == 1) {
+      uint4* d = reinterpret_cast<uint4*>(s + c);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        d[q] = make_uint4(wb[(4 * q) * wst], wb[(4 * q + 1) * wst], wb[(4 * q + 2) * wst],
+                          wb[(4 * q + 3) * wst]);
+      return;
+    }
+#endif
+    for (int k = 0; k < n; ++k) at(c + k) = wb[k * wst];
+  }
+  OS_HD void put(int i, uint32_t v) {
+    wb[(i & 15) * wst] = v;
+    if ((i & 15) == 15) flush(i - 15, 16);
+  }
+  OS_HD int finalize() {
+    if (pre) return idx;
+    if (blk0 || idx == 0) {
+      if (blk0 && (idx & 15)) flush(idx & ~15, idx & 15);  // the block-0 words drawn so far
+      return blk0 ? idx : kMtN;
+    }
+    if (idx & 15) flush(idx & ~15, idx & 15);  // the group being filled
+    return MtStreamPf::finalize();
+  }
+  OS_HD uint32_t next() {
+    ++words;
+    if (pre) {
+      if (idx < kMtN) return MtStream::temper(at(idx++));
+      pre = 0;
+      idx = 0;
+      prefetch0();
+    }
+    const int i = idx;
+    uint32_t v;
+    if (blk0) {
+      const uint32_t b = (i + 1 == kMtN) ? at(0) : lo1;
+      const uint32_t m = (i + kMtM < kMtN) ? hi : at(i + kMtM - kMtN);
+      const uint32_t y = (lo0 & 0x80000000u) | (b & 0x7fffffffu);
+      v = m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      put(i, v);
+      lo0 = lo1;
+      lo1 = MtStreamSoA::seed_step(lo1, i + 2);
+      hi = MtStreamSoA::seed_step(hi, i + kMtM + 1);
+      if (i + 1 == kMtN) {
+        blk0 = 0;
+        prefetch0();
+      }
+    } else {
+      const uint32_t y = (a_i & 0x80000000u) | (a_i1 & 0x7fffffffu);
+      v = a_im ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      put(i, v);
+      const int j = (i + 1 == kMtN) ? 0 : i + 1;
+      const int j1 = (j + 1 == kMtN) ? 0 : j + 1;
+      const int jm = (j + kMtM >= kMtN) ? j + kMtM - kMtN : j + kMtM;
+      a_i = a_i1;
+      a_i1 = at(j1);
+      a_im = at(jm);
+    }
+    idx = (i + 1 == kMtN) ? 0 : i + 1;
+    return MtStream::temper(v);
+  }
+};
+
 OS_HD uint64_t umulhi64(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __umul64hi(a, b);

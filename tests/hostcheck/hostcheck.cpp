@@ -14,6 +14,10 @@
 #include "os_chance.h"
 #include "os_mcts.h"
 
+// 1: searches keep the go superko log's open group in a side buffer as
+// k_lsearch does (hc_set_log_wc).
+static int g_log_wc = 0;
+
 using namespace osm;
 
 namespace {
@@ -34,6 +38,8 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
   uint16_t actbuf[kMaxChildren];
   typename G::Ctx ctx;
   HostGoLog logbuf;
+  uint64_t wlog[8];
+  uint32_t wlink[8];
   if constexpr (G::State::kNeedsLog) {
     std::memset(static_cast<void*>(&ctx), 0, sizeof ctx);
     ctx.zob = game.zob.data();
@@ -41,6 +47,11 @@ int RunOne(const HostGame& game, const HostState& root, const SearchParams& sp,
     ctx.n_base = static_cast<int32_t>(root.hashes.size());
     logbuf.bind(&ctx, 248, game.cfg.rows * game.cfg.cols);
     ctx.init_filters();
+    if (g_log_wc) {  // k_lsearch's write-combined log (GoCtxT::wlog)
+      ctx.wlog = wlog;
+      ctx.wlink = wlink;
+      ctx.wst = 1;
+    }
   }
   const typename G::State& rs = *reinterpret_cast<const typename G::State*>(root.raw);
   SearchResult res;
@@ -446,6 +457,24 @@ void hc_mt_words_pf(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
 // MtStreamPf continuing a numpy (key, pos) state for k draws, exported back.
 void hc_mt_pf_roundtrip(uint32_t* key, int32_t* pos, int64_t k, uint32_t* out) {
   MtStreamPf g{key, 1, 0, 0};
+  g.init_import(*pos);
+  for (int64_t i = 0; i < k; ++i) out[i] = g.next();
+  *pos = g.finalize();
+}
+void hc_set_log_wc(int on) { g_log_wc = on; }
+// k_lsearch's write-combined stream (MtStreamWc: 16-word groups), same
+// interleaving.
+void hc_mt_words_wc(uint32_t seed, int64_t stride, int64_t n, uint32_t* out) {
+  std::vector<uint32_t> s(kMtN * stride, 0xdeadbeefu);
+  uint32_t wb[16];
+  MtStreamWc g{{s.data() + stride - 1, stride, 0, 0}, wb, 1};
+  g.seed(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = g.next();
+}
+// MtStreamWc continuing a numpy (key, pos) state for k draws, exported back.
+void hc_mt_wc_roundtrip(uint32_t* key, int32_t* pos, int64_t k, uint32_t* out) {
+  uint32_t wb[16];
+  MtStreamWc g{{key, 1, 0, 0}, wb, 1};
   g.init_import(*pos);
   for (int64_t i = 0; i < k; ++i) out[i] = g.next();
   *pos = g.finalize();

@@ -35,6 +35,9 @@ def lib():
     L.hc_mt_words_pf.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
     L.hc_mt_words_reg.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
     L.hc_mt_pf_roundtrip.argtypes = [vp, vp, ctypes.c_int64, vp]
+    L.hc_mt_words_wc.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64, vp]
+    L.hc_mt_wc_roundtrip.argtypes = [vp, vp, ctypes.c_int64, vp]
+    L.hc_set_log_wc.argtypes = [ctypes.c_int]
     L.hc_absl_uniform.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp]
     L.hc_cpp_shuffle.argtypes = [ctypes.c_uint32, ctypes.c_int32, vp]
     L.hc_np_ops.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, vp, vp,
@@ -117,6 +120,18 @@ def mt_words_pf(seed, stride, n):
   return out
 
 
+def set_log_wc(on):
+  """Searches keep the go superko log's open 8-entry group in a side buffer
+  (GoCtxT::wlog, as k_lsearch does)."""
+  lib().hc_set_log_wc(1 if on else 0)
+
+
+def mt_words_wc(seed, stride, n):
+  out = np.zeros(n, np.uint32)
+  lib().hc_mt_words_wc(seed, stride, n, out.ctypes.data)
+  return out
+
+
 def absl_uniform(seed, n, k):
   out = np.zeros(k, np.uint64)
   lib().hc_absl_uniform(seed, n, k, out.ctypes.data)
@@ -163,6 +178,14 @@ def mt_pf_roundtrip(key, pos, k):
   p = np.array([pos], dtype=np.int32)
   out = np.zeros(k, np.uint32)
   lib().hc_mt_pf_roundtrip(key.ctypes.data, p.ctypes.data, k, out.ctypes.data)
+  return out, key, int(p[0])
+
+
+def mt_wc_roundtrip(key, pos, k):
+  key = np.array(key, dtype=np.uint32).copy()
+  p = np.array([pos], dtype=np.int32)
+  out = np.zeros(k, np.uint32)
+  lib().hc_mt_wc_roundtrip(key.ctypes.data, p.ctypes.data, k, out.ctypes.data)
   return out, key, int(p[0])
 
 

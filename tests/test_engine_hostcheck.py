@@ -61,6 +61,29 @@ def test_rollout_count_solver_and_uct_variants(gs, n_rollouts, solve, uct_c):
   _check(got, ref)
 
 
+@pytest.mark.parametrize("gs,R,plies", [("go(board_size=5,komi=0.5)", 8, 4),
+                                        ("go(board_size=7,komi=4.5)", 6, 6),
+                                        ("go(board_size=9)", 4, 8)])
+@pytest.mark.parametrize("n_rollouts", [1, 3])
+def test_write_combined_go_log_matches_oracle(gs, R, plies, n_rollouts):
+  """k_lsearch's superko log with its open 8-entry group in LDS
+  (GoCtxT::wlog): lookups, inserts, group write-outs and the rewinds of
+  several rollouts per leaf give the oracle's trees."""
+  from os_amd import pyspiel
+  maxc = pyspiel.load_game(gs)._info.max_children
+  acts, offs = _roots(gs, R, plies)
+  bs = np.arange(R, dtype=np.uint32) * 5 + 2
+  es = bs + np.uint32(77)
+  kw = dict(uct_c=2.0, max_simulations=160, n_rollouts=n_rollouts)
+  ref = O.Game(gs).mcts_batch(acts, offs, bs, es, max_children=maxc, **kw)
+  H.set_log_wc(True)
+  try:
+    got = H.mcts_batch(gs, acts, offs, bs, es, maxc, **kw)
+  finally:
+    H.set_log_wc(False)
+  _check(got, ref)
+
+
 @pytest.mark.parametrize("gs,sims", [("go(board_size=9)", 700), ("hex", 2200)])
 def test_garbage_collection_path(gs, sims):
   """max_memory_mb=1 -> max_nodes_ = 13108: GC fires (mcts.cc:402-424)."""

@@ -38,6 +38,14 @@ def test_read_ahead_stream_matches_std_mt19937(seed, stride):
   assert np.array_equal(H.mt_words_pf(seed, stride, 2600), O.mt19937(seed, 2600))
 
 
+@pytest.mark.parametrize("seed", [0, 1, 42, 5489, 2**32 - 1])
+@pytest.mark.parametrize("stride", [1, 3, 64])
+def test_write_combined_stream_matches_std_mt19937(seed, stride):
+  # k_lsearch's stream with its stores in 16-word groups (MtStreamWc): every
+  # word it reads back as rewritten lies in a stored group.
+  assert np.array_equal(H.mt_words_wc(seed, stride, 2600), O.mt19937(seed, 2600))
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 48, 82, 121, 768])
 def test_absl_uniform_matches_oracle(n):
   for seed in (3, 99):
@@ -85,6 +93,22 @@ def test_read_ahead_stream_numpy_roundtrip(skip, k):
   rs.randint(0, 2**32, size=skip, dtype=np.uint64)
   st = rs.get_state()
   out, key, pos = H.mt_pf_roundtrip(st[1], st[2], k)
+  ref = rs.randint(0, 2**32, size=k, dtype=np.uint64).astype(np.uint32)
+  assert np.array_equal(out, ref)
+  st2 = rs.get_state()
+  assert pos == st2[2]
+  assert np.array_equal(key, st2[1])
+
+
+@pytest.mark.parametrize("skip", [0, 37, 600, 624])
+@pytest.mark.parametrize("k", [0, 1, 15, 16, 17, 100, 587, 588, 624, 625, 1500])
+def test_write_combined_stream_numpy_roundtrip(skip, k):
+  # MtStreamWc continuing an imported (key, pos) state and exporting it back,
+  # a partly filled 16-word group included.
+  rs = np.random.RandomState(11)
+  rs.randint(0, 2**32, size=skip, dtype=np.uint64)
+  st = rs.get_state()
+  out, key, pos = H.mt_wc_roundtrip(st[1], st[2], k)
   ref = rs.randint(0, 2**32, size=k, dtype=np.uint64).astype(np.uint32)
   assert np.array_equal(out, ref)
   st2 = rs.get_state()
