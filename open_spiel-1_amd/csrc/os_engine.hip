@@ -162,6 +162,10 @@ DevArgs MakeArgs(os_engine* e) {
   a.hash_stride = e->hash_stride;
   a.lstride = e->chunk_roots;
   a.lpath = e->d_lpath.p;
+  // k_lsearch writes each search's log row in whole 8-entry groups with
+  // 16-byte stores (GoCtxT::flush_group): rows of kGoLogCap entries keep
+  // every group 64 B (hashes) / 32 B (links) aligned.
+  static_assert(kGoLogCap % GoCtx::kWg == 0, "log rows of whole write groups");
   a.lglog = static_cast<uint64_t*>(e->d_glog.p);
   a.lglink = static_cast<uint32_t*>(e->d_glink.p);
   a.lheads = static_cast<uint16_t*>(e->d_lheads.p);
