@@ -272,8 +272,15 @@ class ExternalEvaluatorSearch:
         break
       self.requests += n
       if eager_rounds is not None and self.steps >= eager_rounds:
+        # Fused requests: a search asks at most once per simulation, so it is
+        # done after max_simulations + 1 rounds; the first replay batch runs
+        # up to there before the host looks (rounds past a search's end are
+        # idle for it).
+        first = graph_batch
+        if requests == "fused":
+          first = max(graph_batch, max_simulations + 1 - self.steps)
         self._replay(st, evaluator, kind, obs, legal, prior, value, pending, pend_host,
-                     done, graph_batch)
+                     done, graph_batch, first)
         break
     o = E._alloc_outputs(R, self.eng.max_children)
     check(lib.os_az_fetch(self.eng._h, self.eng.max_children, *E._out_ptrs(o)))
@@ -288,9 +295,9 @@ class ExternalEvaluatorSearch:
     return o
 
   def _replay(self, st, evaluator, kind, obs, legal, prior, value, pending, pend_host, done,
-              batch):
+              batch, first=None):
     """Captures one round into a HIP graph and replays it until no search
-    is pending (checked every `batch` rounds)."""
+    is pending (checked after `first` rounds, then every `batch` rounds)."""
     torch = self.torch
     g = torch.cuda.CUDAGraph()
     st.synchronize()
@@ -298,11 +305,13 @@ class ExternalEvaluatorSearch:
       cs = torch.cuda.current_stream(self.device)
       check(lib.os_az_step_async(self.eng._h, cs.cuda_stream))
       _evaluate(evaluator, obs, legal, kind, prior, value)
+    n = first or batch
     with torch.cuda.stream(st):
       while True:
-        for _ in range(batch):
+        for _ in range(n):
           g.replay()
           self.steps += 1
+        n = batch
         pend_host.copy_(pending, non_blocking=True)
         done.record(st)
         done.synchronize()
