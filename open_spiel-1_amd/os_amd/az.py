@@ -175,8 +175,10 @@ class ExternalEvaluatorSearch:
 
     graph=True: after two eager rounds, one round (k_az_step + the evaluator +
     the response copies) is captured into a HIP graph and replayed
-    `graph_batch` times per host check of the pending count, so the host
-    neither launches each op nor waits on every round.  The evaluator must be
+    `graph_batch` times per host check of the pending count (fused requests:
+    the first check only after max_simulations + 1 rounds, the most any
+    search can ask for), so the host neither launches each op nor waits on
+    every round.  The evaluator must be
     capturable (static shapes, no host synchronisation); rounds replayed after
     the last search finished see only idle (kind 0) entries.  Not with
     time_steps.
