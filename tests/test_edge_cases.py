@@ -93,3 +93,27 @@ def test_gpu_terminal_rollouts(E):
   ref = O.Game("tic_tac_toe").rollouts(TTT_WON, seeds)
   assert np.array_equal(got, ref)
   assert np.all(got[:, 0] == 1.0)
+
+
+@pytest.mark.gpu
+def test_gpu_empty_selfplay_and_external_evaluator_batches(E):
+  """Zero games of self-play and zero external-evaluator searches: empty
+  outputs, no launch errors."""
+  import torch
+  from os_amd.az import ExternalEvaluatorSearch
+  eng = E.Engine("connect_four")
+  out = eng.selfplay(np.zeros(0, np.int64), np.zeros(1, np.int64), np.zeros((0, 2), np.uint32),
+                     np.zeros(0, np.uint32), max_simulations=16)
+  assert len(out["length"]) == 0 and out["actions"].shape[0] == 0
+  search = ExternalEvaluatorSearch("connect_four")
+  A = search.num_actions
+
+  def evaluator(obs, legal, kind):
+    n = obs.shape[0]
+    return (torch.full((n, A), 1.0 / A, dtype=torch.float64, device=obs.device),
+            torch.zeros(n, dtype=torch.float64, device=obs.device))
+
+  got = search.run(np.zeros(0, np.int64), np.zeros(1, np.int64), np.zeros(0, np.uint32),
+                   evaluator, max_simulations=8)
+  for k in E.OUTPUT_KEYS:
+    assert len(got[k]) == 0, k
