@@ -40,6 +40,13 @@
 #ifndef OS_UNI_MT
 #define OS_UNI_MT 0
 #endif
+// connect_four's walk state needs no entry re-assertion: its selection loop
+// is short and the readfirstlanes cost more than the SGPR copies save
+// (profiles/r05/ab_knobs: C2 and self-play faster with mode 0; breakthrough
+// and go slower), so the mode is a per-game trait.
+#ifndef OS_UNI_SEL_C4
+#define OS_UNI_SEL_C4 0
+#endif
 // 1: connect_four's win test in the tree walk on the vector unit (WaveApply).
 #ifndef OS_WAVE_APPLY
 #define OS_WAVE_APPLY 1
@@ -124,6 +131,11 @@ namespace osm {
 #if OS_PACE
 static __device__ unsigned long long g_pace;  // internal linkage: one per game TU
 #endif
+
+template <class G>
+struct UniSel { static constexpr int kMode = OS_UNI_SEL; };
+template <>
+struct UniSel<ConnectFour> { static constexpr int kMode = OS_UNI_SEL_C4; };
 
 enum PhaseId { kPhSelect = 0, kPhExpand, kPhRollout, kPhBackup, kPhSolver, kPhTail,
                kPhTwist, kPhTotal,
@@ -2425,15 +2437,15 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     int cur_nc = root_nc;
     double cur_logN = root_logN;  // log(N) of the node being scanned (mcts.cc:99)
     int depth = 0;
-#if OS_UNI_SEL == 2
-    s = make_uniform(s);
-    cur_n = __builtin_amdgcn_readfirstlane(cur_n);
-    cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
-    cur_first = static_cast<uint32_t>(
-        __builtin_amdgcn_readfirstlane(static_cast<int>(cur_first)));
-    cur_logN = make_uniform(cur_logN);
-    bot.uniformize();
-#endif
+    if constexpr (UniSel<G>::kMode == 2) {
+      s = make_uniform(s);
+      cur_n = __builtin_amdgcn_readfirstlane(cur_n);
+      cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
+      cur_first = static_cast<uint32_t>(
+          __builtin_amdgcn_readfirstlane(static_cast<int>(cur_first)));
+      cur_logN = make_uniform(cur_logN);
+      bot.uniformize();
+    }
     // ---- selection / expansion ----
     bool pending_expand = false;
 #if OS_PHASE_SEL
@@ -2442,16 +2454,16 @@ __device__ SearchResult wave_search(const GameCfg& g, const SearchParams& sp,
     uint64_t t_loop = OS_PH_NOW();
 #endif
     for (;;) {
-#if OS_UNI_SEL == 1
-      s = make_uniform(s);
-      cur_n = __builtin_amdgcn_readfirstlane(cur_n);
-      cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
-      cur_first = static_cast<uint32_t>(
-          __builtin_amdgcn_readfirstlane(static_cast<int>(cur_first)));
-      cur_idx = static_cast<uint32_t>(
-          __builtin_amdgcn_readfirstlane(static_cast<int>(cur_idx)));
-      depth = __builtin_amdgcn_readfirstlane(depth);
-#endif
+      if constexpr (UniSel<G>::kMode == 1) {
+        s = make_uniform(s);
+        cur_n = __builtin_amdgcn_readfirstlane(cur_n);
+        cur_nc = __builtin_amdgcn_readfirstlane(cur_nc);
+        cur_first = static_cast<uint32_t>(
+            __builtin_amdgcn_readfirstlane(static_cast<int>(cur_first)));
+        cur_idx = static_cast<uint32_t>(
+            __builtin_amdgcn_readfirstlane(static_cast<int>(cur_idx)));
+        depth = __builtin_amdgcn_readfirstlane(depth);
+      }
       if (G::terminal(s, g) || cur_n <= 0) break;
       // The node to expand ends the descent (its first child is fresh): the
       // expansion runs after the loop, so the per-level loop carries only
