@@ -389,7 +389,8 @@ def bench_search(args, ctx, layout):
       "n_rollouts": 1, "solve": True, "max_memory_mb": 1000,
       "root_plies": "k~U[0,%d] from mt19937(1000+i)" % plies,
       "parallelism": "dp%d (independent roots, no collective)" % ctx.world,
-      "layout": lay, "block_size": args.block or (64 if lay == "wave" else 16),
+      "layout": lay,
+      "searches_per_wave": eng.searches_per_wave() if hasattr(eng, "searches_per_wave") else 1,
       "sims_per_step_per_gpu": sims_per_step})
   kern = "k_lsearch" if game.startswith("go") and lay == "lane" else KERNEL[lay]
   line["roofline"] = _roofline(kern, game, alg_bytes, kernel_ms, sims_per_step, "sim")

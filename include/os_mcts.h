@@ -205,9 +205,13 @@ int os_rollouts_batch(os_engine* e, const int64_t* root_actions,
                       const uint32_t* seeds, double* out_returns);
 /* The kernel layout the last os_engine_prepare ran the batch on
  * (OS_LAYOUT_WAVE or OS_LAYOUT_LANE; OS_LAYOUT_AUTO resolved by the engine's
- * own rule: go from 16384 C++-policy roots and boards above 11 x 11 take the
+ * own rule: go from 32768 C++-policy roots and boards above 11 x 11 take the
  * lane layout, hex below 3 x 3 too, everything else the wave layout). */
 int os_engine_get_layout(os_engine* e, int32_t* layout);
+/* Searches per wavefront of the last search launch: 1 on the wave layout, the
+ * lane layout's block width otherwise (go 9 x 9 .. 11 x 11: 16 up to 32768
+ * roots, 32 above).  Reporting only (no reference counterpart). */
+int os_engine_get_searches_per_wave(os_engine* e, int32_t* searches);
 /* Kernel layout for os_rollouts_batch: OS_LAYOUT_LANE (default: one lane per
  * evaluator) or OS_LAYOUT_WAVE (one wave per evaluator, uniform game code). */
 int os_engine_set_rollout_layout(os_engine* e, int32_t layout);

@@ -256,9 +256,11 @@ int CheckParams(const os_engine* e, const os_mcts_params* p, bool search = true)
 // hex_rollout_lanes: 6.5e7 vs 1.4e7 sims/s at 4096 roots, profiles/r01).
 // Breakthrough at C3's 65536 roots: wave 8.3e7 vs lane 3.3e7 sims/s
 // (profiles/r02), so a large batch no longer switches to the lane layout.
-// go9 at 256 sims (profiles/r03/g9_*): wave 5.0e6 / 6.3e6 sims/s at 4096 /
-// 16384 roots, lane (k_lsearch) 2.2e6 / 8.6e6 -- the lane layout needs enough
-// searches to fill the chip, so go takes it from 16384 roots.
+// go9 at 256 sims (profiles/r06/g9_lanes): wave 1.70e7 / 1.74e7 sims/s at
+// 4096 / 8192 roots (about 1.75e7 at 16384, the wave time grows linearly),
+// lane (k_lsearch, 16 lanes per wave) 3.7e6 / 5.4e6 / 1.57e7 at 4096 / 8192 /
+// 16384 and 2.5e7 at 32768 -- the lane layout needs enough searches to fill
+// the chip, so go takes it from 32768 roots.
 int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t policy) {
   if (layout != OS_LAYOUT_AUTO) return layout;
   // pig (chance nodes): one wave per search (k_wsearch_chance) beats a lane
@@ -267,7 +269,7 @@ int32_t ResolveLayout(const GameCfg& cfg, int32_t layout, int64_t R, int32_t pol
   if (cfg.kind == kPig) return OS_LAYOUT_WAVE;
   if (BigBoard(cfg)) return OS_LAYOUT_LANE;  // k_lsearch
   if (cfg.kind == kGo)
-    return policy == OS_POLICY_CPP && R >= 16384 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
+    return policy == OS_POLICY_CPP && R >= 32768 ? OS_LAYOUT_LANE : OS_LAYOUT_WAVE;
   // hex: one wave per search under both policies (the numpy policy's
   // playout draws found over a lane window, os_wave.h hex_rollout_lanes_np);
   // boards below 3 x 3 have no lane-parallel playout.
@@ -1081,6 +1083,7 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
     HIP_TRY(hipMemset(e->d_az_shards.p, 0, sb));
   }
   e->az_ready = true;
+  e->az_stream = nullptr;
   return OS_OK;
 }
 
@@ -1088,6 +1091,9 @@ int AzPrepare(os_engine* e, const os_mcts_params* p, int32_t puct, int64_t R,
 int AzStep(os_engine* e, hipStream_t stream) {
   if (!e->az_ready) return Fail(OS_ERR_INVALID, "os_az_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(stream, &cap));
+  if (cap == hipStreamCaptureStatusNone) e->az_stream = stream;
   const GameLaunchers* L = LaunchersFor(e->game.cfg);
   if (!L || !L->az) return Fail(OS_ERR_UNSUPPORTED, "game");
   return L->az(e, stream);
@@ -1373,6 +1379,13 @@ int os_engine_get_layout(os_engine* e, int32_t* layout) {
   if (!e || !layout) return Fail(OS_ERR_INVALID, "null argument");
   if (e->search_layout < 0) return Fail(OS_ERR_INVALID, "no os_engine_prepare batch");
   *layout = e->search_layout;
+  return OS_OK;
+}
+
+int os_engine_get_searches_per_wave(os_engine* e, int32_t* searches) {
+  if (!e || !searches) return Fail(OS_ERR_INVALID, "null argument");
+  if (e->search_lanes <= 0) return Fail(OS_ERR_INVALID, "no search launched yet");
+  *searches = e->search_lanes;
   return OS_OK;
 }
 
@@ -1749,9 +1762,10 @@ int os_az_requests(os_engine* e, int64_t* total) {
   if (!e || !total) return Fail(OS_ERR_INVALID, "null argument");
   if (!e->az_ready) return Fail(OS_ERR_INVALID, "no os_az_prepare batch");
   HIP_TRY(hipSetDevice(e->device));
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(total, static_cast<int32_t*>(e->d_az_shards.p) + osm::kAzShards * osm::kAzShardStride,
-                    8, hipMemcpyDeviceToHost));
+  // k_az_pending wrote the total on the steps' stream: copy it there
+  HIP_TRY(hipMemcpyAsync(total, static_cast<int32_t*>(e->d_az_shards.p) + osm::kAzShards * osm::kAzShardStride,
+                         8, hipMemcpyDeviceToHost, e->az_stream));
+  HIP_TRY(hipStreamSynchronize(e->az_stream));
   return OS_OK;
 }
 
@@ -1768,7 +1782,7 @@ int os_az_export_rng(os_engine* e, uint32_t* bot_keys, int32_t* bot_pos) {
   if (!e->az_ready || !e->az_import)
     return Fail(OS_ERR_INVALID, "no os_az_prepare_stateful batch");
   HIP_TRY(hipSetDevice(e->device));
-  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipStreamSynchronize(e->az_stream));
   int32_t pending = 0;
   HIP_TRY(hipMemcpy(&pending, e->az_pending, 4, hipMemcpyDeviceToHost));
   if (pending != 0) return Fail(OS_ERR_INVALID, "searches still wait for the evaluator");
@@ -1952,7 +1966,7 @@ int os_az_fetch(os_engine* e, int32_t max_children, int32_t* child_action, int32
   if (!e) return Fail(OS_ERR_INVALID, "null engine");
   if (!e->az_ready) return Fail(OS_ERR_INVALID, "os_az_prepare was not called");
   HIP_TRY(hipSetDevice(e->device));
-  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipStreamSynchronize(e->az_stream));
   int32_t pending = 0;
   HIP_TRY(hipMemcpy(&pending, e->az_pending, 4, hipMemcpyDeviceToHost));
   if (pending != 0)

@@ -309,6 +309,7 @@ struct os_engine {
   bool import_state = false;
   bool shared_stream = false;
   int32_t search_layout = -1;  // layout of the last os_engine_prepare (AUTO resolved)
+  int32_t search_lanes = 0;    // searches per wave of the last search launch (1: wave layout)
   int32_t rollout_layout = OS_LAYOUT_LANE;  // 4-140x faster than WAVE (profiles/r01)
   // prepared rollout batch
   int64_t roll_n = 0;
@@ -327,6 +328,11 @@ struct os_engine {
   std::vector<uint32_t> sp_actor_seeds;
   // prepared external-evaluator batch (os_az_*): caller-owned device buffers
   bool az_ready = false;
+  // The stream of the last eager os_az_step_async (a step captured into a
+  // graph is replayed on its caller's stream, which ran the eager steps
+  // before): os_az_fetch / os_az_requests / os_az_export_rng wait on it
+  // alone, not on every stream of the device.
+  hipStream_t az_stream = nullptr;
   int32_t az_puct = 0;
   int32_t az_np = 0;  // OS_POLICY_NUMPY external-evaluator batch
   // os_az_stage: the host work of the NEXT os_az_prepare_staged batch, done

@@ -173,9 +173,9 @@ struct LsCaps {
   static constexpr int act = 1, zob = 1, heads = 1, log = 1, bloom = 1;
 };
 template <>
-struct LsCaps<Go> {
-  static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads * 64, log = kGoLogCap,
-                       bloom = GoCtx::kBloomWords * 64;
+struct LsCaps<Go> {  // act, heads and bloom per lane
+  static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads, log = kGoLogCap,
+                       bloom = GoCtx::kBloomWords;
 };
 template <>
 struct LsCaps<GoBig> {  // actions up to 361: u16 expansion buffers in HBM
@@ -194,13 +194,14 @@ struct LsWide<HexBig> : std::true_type {};
 
 template <class G>
 struct LCtx {
-  __device__ static NoCtx make(const DevArgs&, int64_t, int64_t, uint8_t*, uint32_t*) {
+  __device__ static NoCtx make(const DevArgs&, int64_t, int64_t, uint8_t*, uint32_t*, int) {
     return NoCtx();
   }
 };
 template <>
 struct LCtx<GoBig> {
-  __device__ static GoCtxW make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t*, uint32_t*) {
+  __device__ static GoCtxW make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t*, uint32_t*,
+                                int) {
     GoCtxW c;
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
@@ -219,18 +220,20 @@ struct LCtx<GoBig> {
 };
 template <>
 struct LCtx<Go> {
+  // lds_heads / lds_bloom: this lane's column of the block's lane-interleaved
+  // arrays (stride `lanes`, the block's width).
   __device__ static GoCtx make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t* lds_heads,
-                               uint32_t* lds_bloom) {
+                               uint32_t* lds_bloom, int lanes) {
     GoCtx c;
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
     c.n_base = a.root_nhash[gr];
     c.log = a.lglog + lr * kGoLogCap;
     c.link = a.lglink + lr * kGoLogCap;
-    c.head = lds_heads + (threadIdx.x & 63);
-    c.head_stride = 64;
+    c.head = lds_heads;
+    c.head_stride = lanes;
 #if OS_GO_LOG_BLOOM
-    c.bloom = lds_bloom + (threadIdx.x & 63);
+    c.bloom = lds_bloom;
 #else
     (void)lds_bloom;
 #endif
@@ -274,20 +277,27 @@ struct MtStreamNoMem {
   __device__ int finalize() const { return 0; }
 };
 
-template <class G, class R>
-__global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
+// kL: searches (active lanes) per wave, the block's width.  A lane runs a
+// whole search, so a wave is one dependent instruction stream per lane; at
+// 65536 roots, 64 lanes per wave are 1024 waves, one per SIMD, and nothing
+// hides a wave's memory and dependency stalls.  Narrower blocks trade VALU /
+// SALU issue per search (a wave instruction covers kL searches) for kOcc
+// resident waves per SIMD (LaunchLs picks kL from the batch size).
+template <class G, class R, int kL, int kOcc>
+__global__ __launch_bounds__(64, kOcc) void k_lsearch(DevArgs a) {
   // LDS: go's bucket heads and the expansion buffers, lane-interleaved
-  // ([i][64]), and the Zobrist table (read by every move of every lane).
-  __shared__ uint8_t heads[LsCaps<G>::heads];
-  __shared__ uint32_t lbloom[OS_GO_LOG_BLOOM ? LsCaps<G>::bloom : 1];  // go: superko log filter
-  __shared__ uint8_t acts[LsCaps<G>::act * 64];  // go actions up to 15 x 15 are < 256
+  // ([i][kL]), and the Zobrist table (read by every move of every lane).
+  __shared__ uint8_t heads[LsCaps<G>::heads * kL];
+  __shared__ uint32_t lbloom[OS_GO_LOG_BLOOM ? LsCaps<G>::bloom * kL : 1];  // go: superko log filter
+  __shared__ uint8_t acts[LsCaps<G>::act * kL];  // go actions up to 15 x 15 are < 256
   __shared__ uint64_t zob[LsCaps<G>::zob];
   if constexpr (G::State::kNeedsLog) {
     const int nz = 2 * a.cfg.rows * a.cfg.cols;
     for (int i = threadIdx.x; i < nz; i += blockDim.x) zob[i] = a.zob[i];
     __syncthreads();
   }
-  const int64_t lr = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int t = static_cast<int>(threadIdx.x);  // < kL (blockDim.x == kL)
+  const int64_t lr = static_cast<int64_t>(blockIdx.x) * kL + t;
   if (lr >= a.num_roots) return;
   const int64_t gr = a.root_base + lr;
   // Per-search contiguous buffers: the lanes of a wave drift apart (each at
@@ -297,9 +307,9 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
   MtStreamNoMem bot, ev;
 #elif OS_LS_WC
   // twisted words written 16 at a time from a lane-interleaved LDS buffer
-  __shared__ uint32_t mt_wb[2 * 16 * 64];
-  MtStreamWc bot{{a.mt + lr * 2 * kMtN, 1, 0, 0}, mt_wb + (threadIdx.x & 63), 64};
-  MtStreamWc ev{{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0}, mt_wb + 16 * 64 + (threadIdx.x & 63), 64};
+  __shared__ uint32_t mt_wb[2 * 16 * kL];
+  MtStreamWc bot{{a.mt + lr * 2 * kMtN, 1, 0, 0}, mt_wb + t, kL};
+  MtStreamWc ev{{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0}, mt_wb + 16 * kL + t, kL};
 #else
   MtStreamPf bot{a.mt + lr * 2 * kMtN, 1, 0, 0};
   MtStreamPf ev{a.mt + lr * 2 * kMtN + kMtN, 1, 0, 0};
@@ -312,17 +322,17 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
     ev.seed(a.eval_seeds[gr]);
   }
   StridedPtr<PathEnt<R>> path{static_cast<PathEnt<R>*>(a.lpath) + lr * a.path_cap, 1};
-  auto ctx = LCtx<G>::make(a, gr, lr, heads, lbloom);
+  auto ctx = LCtx<G>::make(a, gr, lr, heads + t, lbloom + t, kL);
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
 #if OS_LS_LOGWC
   // go: the superko log's open 8-entry group in LDS (GoCtxT::wlog)
   constexpr bool kLogWc = std::is_same<G, Go>::value;
-  __shared__ uint64_t ls_wlog[kLogWc ? GoCtx::kWg * 64 : 1];
-  __shared__ uint32_t ls_wlink[kLogWc ? GoCtx::kWg * 64 : 1];
+  __shared__ uint64_t ls_wlog[kLogWc ? GoCtx::kWg * kL : 1];
+  __shared__ uint32_t ls_wlink[kLogWc ? GoCtx::kWg * kL : 1];
   if constexpr (kLogWc) {
-    ctx.wlog = ls_wlog + (threadIdx.x & 63);
-    ctx.wlink = ls_wlink + (threadIdx.x & 63);
-    ctx.wst = 64;
+    ctx.wlog = ls_wlog + t;
+    ctx.wlink = ls_wlink + t;
+    ctx.wst = kL;
   }
 #endif
 #if OS_LS_AB & 2
@@ -337,7 +347,7 @@ __global__ __launch_bounds__(64) void k_lsearch(DevArgs a) {
     res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
                                         act, a.path_cap, a.pages, static_cast<uint32_t>(lr));
   } else {
-    StridedPtr<uint8_t> act{acts + (threadIdx.x & 63), 64};
+    StridedPtr<uint8_t> act{acts + t, kL};
     res = mcts_search<G, R, kPolicyCpp>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
                                         act, a.path_cap, a.pages, static_cast<uint32_t>(lr));
   }
@@ -379,7 +389,7 @@ struct WaveCtxMaker<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
     c.n_base = a.root_nhash[gr];
-    c.init_filters();
+    c.init_filters(a.cfg.rows * a.cfg.cols);
     return c;
   }
 };
@@ -479,12 +489,16 @@ __global__ __launch_bounds__(64, WaveOcc<G>::value) void k_wsearch(DevArgs a) {
 #if OS_PHASE_TIMING
   if constexpr (std::is_same<G, Go>::value) ctx.sub = ph.c;
 #endif
+  // Issue-priority pacing evens out a batch of resident waves; the LDS-tree
+  // launch (a few searches, one per CU) has nothing to pace against, so it
+  // skips the counter atomic every OS_PACE_EVERY simulations.
+  constexpr bool kPaceSearch = OS_PACE != 0 && !kLdsTree;
   SearchResult res = shared
       ? wave_search<G, R, Policy, kPaged, kPuct, kLdsTree ? kCacheAll : OS_NODE_CACHE,
-                    OS_PACE != 0>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
+                    kPaceSearch>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
                                   a.path_cap, ph, lcache)
       : wave_search<G, R, Policy, kPaged, kPuct, kLdsTree ? kCacheAll : OS_NODE_CACHE,
-                    OS_PACE != 0>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+                    kPaceSearch>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
                                   a.path_cap, ph, lcache);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
 #if OS_PHASE_TIMING
@@ -758,7 +772,7 @@ struct SpCtx<Go> {
     c.zob = a.zob;
     c.base = a.hist + gg * a.hash_stride;
     c.n_base = a.hist_n[gg];
-    c.init_filters();
+    c.init_filters(a.cfg.rows * a.cfg.cols);
     return c;
   }
   // The move just applied logged its position (go.cc:199-208): it joins the
@@ -1110,7 +1124,7 @@ struct WazCtx<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes + r * a.hash_stride;
     c.n_base = a.root_nhash[r];
-    c.init_filters();
+    c.init_filters(a.cfg.rows * a.cfg.cols);
     return c;
   }
   // The pending simulation's positions since the root follow the base.
@@ -1674,14 +1688,14 @@ template <class G>
 struct RollCtx {
   using type = NoCtx;
   static constexpr int kLdsWords = 1;
-  __device__ static NoCtx make(const RollArgs&, int64_t, uint32_t*) { return NoCtx(); }
+  __device__ static NoCtx make(const RollArgs&, int64_t, uint32_t*, int) { return NoCtx(); }
 };
 #if OS_ROLL_BLOOM
 template <>
 struct RollCtx<Go> {
   using type = GoCtxBloom;
   static constexpr int kLdsWords = GoCtxBloom::kWords * 64;
-  __device__ static GoCtxBloom make(const RollArgs& a, int64_t i, uint32_t* lds) {
+  __device__ static GoCtxBloom make(const RollArgs& a, int64_t i, uint32_t* lds, int lanes) {
     GoCtxBloom c;
     c.zob = a.zob;
     c.base = a.root_hashes;
@@ -1693,8 +1707,8 @@ struct RollCtx<Go> {
     c.log = a.glog + i;
     c.stride = static_cast<int32_t>(a.n);
 #endif
-    c.filt = lds + (threadIdx.x & 63);
-    c.filt_stride = 64;
+    c.filt = lds + threadIdx.x;
+    c.filt_stride = lanes;
     c.cap = kGoLogCap;
     c.init_filters();
     return c;
@@ -1710,7 +1724,8 @@ struct RollCtx<Go> {
   // The bucket heads are the only per-move accesses that differ across the
   // lanes (each lane is at its own stone count): they live in LDS, lane-
   // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
-  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds) {
+  // lanes: the block's width (the stride of the lane-interleaved LDS arrays).
+  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds, int lanes) {
     uint8_t* lds_heads = reinterpret_cast<uint8_t*>(lds);
     uint16_t* glink = reinterpret_cast<uint16_t*>(a.glink);
     type c;
@@ -1726,10 +1741,10 @@ struct RollCtx<Go> {
     c.link = glink + i;
     c.stride = static_cast<int32_t>(a.n);
 #endif
-    c.head = lds_heads + (threadIdx.x & 63);
-    c.head_stride = 64;
+    c.head = lds_heads + threadIdx.x;
+    c.head_stride = lanes;
 #if OS_GO_LOG_BLOOM
-    c.bloom = lds + (((a.cfg.rows * a.cfg.cols + 1) * 64 + 3) / 4) + (threadIdx.x & 63);
+    c.bloom = lds + (((a.cfg.rows * a.cfg.cols + 1) * lanes + 3) / 4) + threadIdx.x;
 #endif
     c.n_log = 0;
     c.cap = kGoLogCap;
@@ -1751,7 +1766,7 @@ struct WaveRollCtx<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
-    c.init_filters();
+    c.init_filters(a.cfg.rows * a.cfg.cols);
     return c;
   }
 };
@@ -1818,7 +1833,7 @@ __global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
 #endif
   ev.seed(a.seeds[i]);
   extern __shared__ uint32_t roll_lds[];  // RollLdsBytes<G>(cfg) bytes
-  typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
+  typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds, static_cast<int>(blockDim.x));
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
   uint32_t moves = 0;
@@ -1927,6 +1942,22 @@ int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   return OS_OK;
 }
 
+// Searches per wave of k_lsearch for a chunk of n roots.  Go 9 x 9 .. 11 x 11
+// runs 16 lanes per block up to 32768 roots (2048 waves, all resident at two
+// per SIMD) and 32 above; boards above 11 x 11 keep 64.  A wave's time is its
+// lanes' longest dependent chain plus the union of their divergent paths, so
+// narrower waves finish sooner, and they spread a small batch over more SIMDs
+// (go9, 256 sims, ms per launch for 16 / 32 / 64 lanes, profiles/r06/g9_lanes:
+// 16384 roots 266 / 361 / 408; 32768 roots 332 / 336 / 444; 65536 roots
+// 642 / 428 / 442; 131072 roots - / 833 / 881).  block_size (16 / 32 / 64)
+// overrides the choice.
+template <class G>
+int LsLanes(int64_t n, int block_size) {
+  if (!std::is_same<G, Go>::value) return 64;
+  if (block_size == 16 || block_size == 32 || block_size == 64) return block_size;
+  return n <= 32768 ? 16 : 32;
+}
+
 template <class G, class R>
 int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
   if (a.shared_stream)
@@ -1938,8 +1969,19 @@ int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
     const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
     a.root_base = base;
     a.num_roots = n;
-    const unsigned grid = static_cast<unsigned>((n + 63) / 64);
-    hipLaunchKernelGGL((k_lsearch<G, R>), dim3(grid), dim3(64), 0, stream, a);
+    const int kl = LsLanes<G>(n, e->params.block_size);
+    e->search_lanes = kl;
+    const unsigned grid = static_cast<unsigned>((n + kl - 1) / kl);
+    if constexpr (std::is_same<G, Go>::value) {
+      if (kl == 16)
+        hipLaunchKernelGGL((k_lsearch<G, R, 16, 2>), dim3(grid), dim3(16), 0, stream, a);
+      else if (kl == 32)
+        hipLaunchKernelGGL((k_lsearch<G, R, 32, 2>), dim3(grid), dim3(32), 0, stream, a);
+      else
+        hipLaunchKernelGGL((k_lsearch<G, R, 64, 1>), dim3(grid), dim3(64), 0, stream, a);
+    } else {
+      hipLaunchKernelGGL((k_lsearch<G, R, 64, 1>), dim3(grid), dim3(64), 0, stream, a);
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess)
       return Fail(OS_ERR_DEVICE, std::string("k_lsearch launch failed: ") +
@@ -1960,6 +2002,7 @@ int LaunchSearchOnly(os_engine* e, const DevArgs& a, hipStream_t stream) {
 
 template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
+  e->search_lanes = 1;  // the wave layouts; the lane launchers below set theirs
   if constexpr (HasChance<G>::value) {
     if (a.path_cap > kChancePathCap) a.path_cap = kChancePathCap;
     if (e->params.layout == OS_LAYOUT_WAVE) {
@@ -1994,6 +2037,7 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   if (per_lane * bs > kLdsBytes) bs = static_cast<int>(kLdsBytes / per_lane);
   if (bs < 1) return Fail(OS_ERR_CAPACITY, "per-lane LDS slice exceeds the CU's LDS");
   const size_t lds = per_lane * bs;
+  e->search_lanes = bs;
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mcts<G, R, Policy>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds)));
@@ -2204,15 +2248,28 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
 // k_rollouts' dynamic LDS: go's bucket heads for this board size (one byte
 // per stone count per lane) and the log's Bloom filter; the heads' static
 // bound (11 x 11) would cost occupancy on 9 x 9.
+// Playouts (active lanes) per wave of k_rollouts.  A lane runs a whole
+// playout; below OS_ROLL_FULL playouts, 64-lane waves leave fewer than four
+// waves per SIMD to hide each other's stalls, so the block narrows to 32
+// lanes (A/B knob OS_ROLL_NARROW: the width used there).
+#ifndef OS_ROLL_NARROW
+#define OS_ROLL_NARROW 64
+#endif
+#ifndef OS_ROLL_FULL
+#define OS_ROLL_FULL (int64_t{4} * 1024 * 64)
+#endif
+inline int RollLanes(int64_t n) { return n < OS_ROLL_FULL ? OS_ROLL_NARROW : 64; }
+
 template <class G>
-size_t RollLdsBytes(const GameCfg& c) {
+size_t RollLdsBytes(const GameCfg& c, int lanes) {
 #if OS_ROLL_BLOOM
   (void)c;
+  (void)lanes;
   return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #else
   if constexpr (std::is_same<G, Go>::value)
-    return 4 * (((c.rows * c.cols + 1) * 64 + 3) / 4 +
-                (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * 64 : 0));
+    return 4 * (((c.rows * c.cols + 1) * lanes + 3) / 4 +
+                (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * lanes : 0));
   else
     return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #endif
@@ -2247,9 +2304,9 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
     }
   }
   {
-    const int bs = 64;
+    const int bs = RollLanes(n);
     hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                       dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
+                       dim3(bs), RollLdsBytes<G>(a.cfg, bs), stream, a);
   }
   HIP_TRY(hipGetLastError());
   return OS_OK;

@@ -1,3 +1,3 @@
 """open_spiel.python.algorithms.mcts drop-in (see os_amd.mcts)."""
-from os_amd.mcts import (Evaluator, MCTSBot, RandomRolloutEvaluator,  # noqa: F401
+from os_amd.mcts import (Evaluator, Float32ModelError, MCTSBot, RandomRolloutEvaluator,  # noqa: F401
                          SearchNode)

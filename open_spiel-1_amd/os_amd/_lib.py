@@ -180,6 +180,7 @@ _sig("os_az_set_requests", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_az_set_layout", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_az_get_layout", ctypes.c_int, [_vp, _P])
 _sig("os_engine_get_layout", ctypes.c_int, [_vp, _P])
+_sig("os_engine_get_searches_per_wave", ctypes.c_int, [_vp, _P])
 _sig("os_az_requests", ctypes.c_int, [_vp, _P])
 _sig("os_engine_set_run_timing", ctypes.c_int, [_vp, ctypes.c_int32])
 _sig("os_engine_last_run_ms", ctypes.c_int, [_vp, _P])

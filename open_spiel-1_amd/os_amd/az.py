@@ -212,6 +212,14 @@ class ExternalEvaluatorSearch:
     if staged:
       if bot_rng is not None or root_noise is not None:
         raise ValueError("staged batches are seeded C++-policy batches")
+      asked = self._batch_args(R, puct, max_simulations, uct_c, solve, max_memory_mb,
+                               dirichlet_alpha, dirichlet_epsilon, block_size)
+      staged_args = getattr(self, "_staged_args", None)
+      if staged_args is not None and staged_args != asked:
+        raise ValueError("run(staged=True) must describe the batch stage() staged: staged %r, "
+                         "asked %r" % (staged_args, asked))
+      # os_az_prepare_staged consumes the staged batch (and refuses a second run)
+      self._staged_args = None
       check(lib.os_az_prepare_staged(self.eng._h, kind.data_ptr(), obs.data_ptr(),
                                      legal.data_ptr(), prior.data_ptr(), value.data_ptr(),
                                      pending.data_ptr()))
@@ -333,9 +341,20 @@ class ExternalEvaluatorSearch:
     offs = _lib.i64(root_offsets)
     bs = _lib.u32(bot_seeds)
     self._stage_keep = (p, acts, offs, bs)
+    self._staged_args = self._batch_args(len(offs) - 1, puct, max_simulations, uct_c, solve,
+                                         max_memory_mb, dirichlet_alpha, dirichlet_epsilon,
+                                         block_size)
     check(lib.os_az_stage(self.eng._h, ctypes.byref(p), 1 if puct else 0, len(offs) - 1,
                           ptr(acts), ptr(offs), ptr(bs), float(dirichlet_alpha),
                           float(dirichlet_epsilon)))
+
+  @staticmethod
+  def _batch_args(R, puct, max_simulations, uct_c, solve, max_memory_mb, dirichlet_alpha,
+                  dirichlet_epsilon, block_size):
+    """The search arguments a staged batch fixes (stage() vs run(staged=True))."""
+    return (int(R), bool(puct), int(max_simulations), float(uct_c), bool(solve),
+            int(max_memory_mb), float(dirichlet_alpha), float(dirichlet_epsilon),
+            int(block_size))
 
   def tree(self, r=0):
     """Search r's tree after run(): os_engine_tree's flat arrays plus the

@@ -20,7 +20,7 @@ import collections
 import numpy as np
 
 from . import pyspiel
-from .mcts import Evaluator
+from .mcts import Evaluator, Float32ModelError
 
 
 class LRUCache(object):
@@ -98,7 +98,21 @@ class AlphaZeroEvaluator(Evaluator):
   def evaluate_batch(self, obs, legal, kind):
     """One round of device requests (os_amd/az.py protocol): obs float32
     [N, C, H, W], legal bool [N, A], kind int32 [N] (0 = idle) on the GPU;
-    returns (prior float64 [N, A] action-indexed, value float64 [N], player 0)."""
+    returns (prior float64 [N, A] action-indexed, value float64 [N], player 0).
+
+    Every live row goes through the LRU cache under the key `_inference`
+    builds (ObservationTensor as float64 bytes + legal mask as int64 bytes),
+    and the misses go to the model as one batch.  A device request is a fused
+    Evaluate + Prior, so cache_info() counts one lookup per request where the
+    reference's host loop counts two per expanded node (its evaluate, then
+    its prior on the second visit).
+
+    The device search accumulates values and scores children in float64.
+    The reference's mcts.py inherits the model's dtype instead (NumPy 2 keeps
+    float32 in `total_reward += value` and in PUCTValue), so a model with
+    float32 outputs is refused here (Float32ModelError) rather than searched
+    with different arithmetic; MCTSBot(backend="auto") then runs the host
+    loop, which is the reference's own arithmetic."""
     import torch
     n, a = legal.shape
     prior = np.zeros((n, a), np.float64)
@@ -109,8 +123,27 @@ class AlphaZeroEvaluator(Evaluator):
       # tensor's values are exact in float32), legal_actions_mask as int64
       o = obs.reshape(n, -1)[live].to(torch.float64).cpu().numpy()
       m = legal[live].to(torch.int64).cpu().numpy()
-      v, p = self._model.inference(o, m)
-      prior[live] = np.asarray(p, np.float64)
-      value[live] = np.asarray(v, np.float64).reshape(len(live), -1)[:, 0]
+      keys = [o[i].tobytes() + m[i].tobytes() for i in range(len(live))]
+      got = [None] * len(live)
+      miss = []
+      for i, k in enumerate(keys):
+        if k in self._cache._data:
+          got[i] = self._cache.make(k, None)
+        else:
+          miss.append(i)
+      if miss:
+        v, p = self._model.inference(o[miss], m[miss])
+        v, p = np.asarray(v), np.asarray(p)
+        if v.dtype != np.float64 or p.dtype != np.float64:
+          raise Float32ModelError(
+              "the model returns %s values / %s policies: the device search computes in "
+              "float64, the reference mcts.py in the model's dtype" % (v.dtype, p.dtype))
+        for j, i in enumerate(miss):
+          row = (v[j:j + 1], p[j:j + 1])
+          got[i] = self._cache.make(keys[i], lambda row=row: row)
+      for i, r in enumerate(live):
+        value[r] = got[i][0].reshape(-1)[0]
+        prior[r] = got[i][1].reshape(-1)
     dev = obs.device
     return torch.from_numpy(prior).to(dev), torch.from_numpy(value).to(dev)
+

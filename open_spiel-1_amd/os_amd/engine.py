@@ -304,6 +304,13 @@ class Engine:
     check(lib.os_engine_get_layout(self._h, ptr(out)))
     return int(out[0])
 
+  def searches_per_wave(self):
+    """Searches per wavefront of the last search launch (1 on the wave
+    layout; the lane layout's block width)."""
+    out = np.zeros(1, np.int32)
+    check(lib.os_engine_get_searches_per_wave(self._h, ptr(out)))
+    return int(out[0])
+
   def last_sims(self):
     return int(lib.os_engine_last_sims(self._h))
 

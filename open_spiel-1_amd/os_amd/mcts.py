@@ -33,6 +33,11 @@ from . import _lib
 from . import pyspiel
 
 
+class Float32ModelError(TypeError):
+  """An evaluator's model answered in a dtype other than float64: the device
+  search, which computes in float64, refuses it (az_evaluator.py)."""
+
+
 class Evaluator(object):
   """Evaluation function interface (mcts.py:29-43)."""
 
@@ -262,6 +267,7 @@ class MCTSBot(pyspiel.Bot):
                        "and either RandomRolloutEvaluator without Dirichlet noise or an "
                        "evaluator with a batched protocol (evaluate_into / evaluate_batch)")
     self._warned_host = False
+    self._f32_model = False  # set when backend="auto" meets a float32 model
 
   def _gpu_eligible(self):
     return self._rollout_eligible() or self._external_eligible()
@@ -298,9 +304,11 @@ class MCTSBot(pyspiel.Bot):
     if self._use_gpu() and not self.verbose:
       # The engine's BestChild (mcts.py sort_key order, first maximum) is all a
       # step needs: no tree export, no SearchNode objects.
-      chosen = int(self._run_gpu(state)[0]["best_action"][0])
-      return [(a, 1.0 if a == chosen else 0.0)
-              for a in state.legal_actions(state.current_player())], chosen
+      out = self._gpu_or_none(state)
+      if out is not None:
+        chosen = int(out[0]["best_action"][0])
+        return [(a, 1.0 if a == chosen else 0.0)
+                for a in state.legal_actions(state.current_player())], chosen
     root = self.mcts_search(state)
     best = root.best_child()
     if self.verbose:
@@ -325,26 +333,39 @@ class MCTSBot(pyspiel.Bot):
     return self.step_with_policy(state)[1]
 
   def _use_gpu(self):
-    return self.backend == "hip" or (self.backend == "auto" and self._gpu_eligible())
+    return self.backend == "hip" or (self.backend == "auto" and not self._f32_model and
+                                     self._gpu_eligible())
+
+  def _gpu_or_none(self, state):
+    """_run_gpu, or None when backend="auto" meets a model whose outputs are
+    not float64 (az_evaluator.Float32ModelError): that bot then searches on
+    the host, in the model's own arithmetic as the reference does."""
+    try:
+      return self._run_gpu(state)
+    except Float32ModelError:
+      if self.backend != "auto":
+        raise
+      self._f32_model = True
+      return None
 
   def mcts_search(self, state):
     if self._use_gpu():
-      return self._search_gpu(state)
+      out = self._gpu_or_none(state)
+      if out is not None:
+        return tree_to_search_nodes(out[1].tree(0), state, self._game)
     if self.backend == "auto" and not self._warned_host:
       # Never a silent CPU search: say once why this bot runs on the host.
-      warnings.warn("MCTSBot(backend='auto') runs this search on the host CPU (the "
-                    "GPU engine needs RandomRolloutEvaluator, UCT or PUCT selection, "
-                    "no Dirichlet noise and a game it runs on the device); pass "
-                    "backend='host' to silence this or backend='hip' to make it an "
-                    "error", RuntimeWarning, stacklevel=2)
+      why = ("the evaluator's model answers in float32, which the device search "
+             "(float64) would not reproduce" if self._f32_model else
+             "the GPU engine needs RandomRolloutEvaluator without Dirichlet noise or a "
+             "batched evaluator, UCT or PUCT selection and a game it runs on the device")
+      warnings.warn("MCTSBot(backend='auto') runs this search on the host CPU (%s); "
+                    "pass backend='host' to silence this or backend='hip' to make it "
+                    "an error" % why, RuntimeWarning, stacklevel=2)
       self._warned_host = True
     return self._search_host(state)
 
   # ---- GPU path -------------------------------------------------------------
-  def _search_gpu(self, state):
-    _, eng = self._run_gpu(state)
-    return tree_to_search_nodes(eng.tree(0), state, self._game)
-
   def _run_gpu(self, state):
     """One search on the device continuing the RandomState streams; returns
     (root outputs, object whose tree(0) is the search tree)."""
@@ -375,25 +396,31 @@ class MCTSBot(pyspiel.Bot):
     (fused Evaluate + Prior for a pure evaluator)."""
     search = pyspiel._az_search_for(self._game)
     rs = self._random_state
-    noise = None
-    eps = 0.0
-    if (self._dirichlet_noise and self.max_simulations >= 2 and not state.is_terminal()):
-      # mcts.py:314-316 at the root's expansion (simulation 1): the evaluator
-      # drew nothing before it, so it is the search's first use of the stream.
-      eps, alpha = self._dirichlet_noise
-      n = len(state.legal_actions(state.current_player()))
-      noise = np.zeros((1, search.eng.max_children), np.float64)
-      noise[0, :n] = rs.dirichlet([alpha] * n)
-    b = rs.get_state()
-    hist = np.asarray(state.history(), np.int64)
-    pure = bool(getattr(self.evaluator, "pure_function", False))
-    out = search.run(hist, np.array([0, len(hist)], np.int64), None, self._device_evaluator(),
-                     puct=self._child_selection_fn is SearchNode.puct_value,
-                     max_simulations=self.max_simulations, uct_c=self.uct_c,
-                     solve=self.solve, max_memory_mb=0,
-                     bot_rng=(np.asarray(b[1], np.uint32)[None], np.array([b[2]], np.int32)),
-                     requests="fused" if pure else "separate", policy="numpy",
-                     root_noise=noise, dirichlet_epsilon=eps)
+    saved = rs.get_state()
+    try:
+      noise = None
+      eps = 0.0
+      if (self._dirichlet_noise and self.max_simulations >= 2 and not state.is_terminal()):
+        # mcts.py:314-316 at the root's expansion (simulation 1): the evaluator
+        # drew nothing before it, so it is the search's first use of the stream.
+        eps, alpha = self._dirichlet_noise
+        n = len(state.legal_actions(state.current_player()))
+        noise = np.zeros((1, search.eng.max_children), np.float64)
+        noise[0, :n] = rs.dirichlet([alpha] * n)
+      b = rs.get_state()
+      hist = np.asarray(state.history(), np.int64)
+      pure = bool(getattr(self.evaluator, "pure_function", False))
+      out = search.run(hist, np.array([0, len(hist)], np.int64), None, self._device_evaluator(),
+                       puct=self._child_selection_fn is SearchNode.puct_value,
+                       max_simulations=self.max_simulations, uct_c=self.uct_c,
+                       solve=self.solve, max_memory_mb=0,
+                       bot_rng=(np.asarray(b[1], np.uint32)[None], np.array([b[2]], np.int32)),
+                       requests="fused" if pure else "separate", policy="numpy",
+                       root_noise=noise, dirichlet_epsilon=eps)
+    except BaseException:
+      # no search happened: the bot's stream is where the reference's would be
+      rs.set_state(saved)
+      raise
     keys, pos = search.bot_rng_out
     rs.set_state(("MT19937", keys[0], int(pos[0]), b[3], b[4]))
     return out, search

@@ -13,7 +13,11 @@ import numpy as np
 
 class ToyModel(object):
 
-  def __init__(self, obs_size, num_actions, seed=12345):
+  def __init__(self, obs_size, num_actions, seed=12345, dtype=np.float64):
+    # dtype: the outputs' dtype.  float32 stands in for the reference's
+    # TensorFlow model (alpha_zero/model.py:339-344 returns float32 arrays),
+    # whose dtype mcts.py then carries into its sums under NumPy 2.
+    self.dtype = np.dtype(dtype)
     rs = np.random.RandomState(seed)
     # integer weights: obs values are 0 / 1, so every dot product is an exact
     # small integer whatever the summation order
@@ -29,4 +33,4 @@ class ToyModel(object):
     den[den == 0] = 1
     policy = num.astype(np.float64) / den.astype(np.float64)
     value = (np.mod(z[:, self.A:], 21) - 10).astype(np.float64) / 10.0
-    return value, policy
+    return value.astype(self.dtype), policy.astype(self.dtype)

@@ -470,6 +470,11 @@ def test_gpu_staged_batch_matches_oracle(require_gpu, game):
   with pytest.raises(RuntimeError):  # a staged batch is consumed once
     search.run(acts, offs, seeds, ev, staged=True, **kw)
     search.run(acts, offs, seeds, ev, staged=True, **kw)
+  # run(staged=True) must describe the staged batch: its own arguments are
+  # not used, so a mismatch is an error, not a silently different search
+  search.stage(acts, offs, seeds, **kw)
+  with pytest.raises(ValueError):
+    search.run(acts, offs, seeds, ev, staged=True, **dict(kw, max_simulations=sims + 1))
 
 
 def _bf16_round(x):

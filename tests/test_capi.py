@@ -63,7 +63,8 @@ def test_gpu_engine_reports_resolved_layout(require_gpu):
            ("hex(board_size=5)", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_WAVE),
            ("hex(board_size=2)", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_LANE),
            ("go(board_size=5)", 8, _lib.LAYOUT_AUTO, _lib.LAYOUT_WAVE),
-           ("go(board_size=5)", 16384, _lib.LAYOUT_AUTO, _lib.LAYOUT_LANE))
+           ("go(board_size=5)", 16384, _lib.LAYOUT_AUTO, _lib.LAYOUT_WAVE),
+           ("go(board_size=5)", 32768, _lib.LAYOUT_AUTO, _lib.LAYOUT_LANE))
   for game, R, asked, want in cases:
     eng = E.Engine(game)
     with pytest.raises(RuntimeError):

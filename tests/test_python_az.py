@@ -54,7 +54,8 @@ def _play(case, backend):
   from open_spiel.python.algorithms import mcts
   from open_spiel.python.algorithms.alpha_zero import evaluator as evl
   game = pyspiel.load_game(case["game"])
-  model = ToyModel(int(np.prod(game.observation_tensor_shape())), game.num_distinct_actions())
+  model = ToyModel(int(np.prod(game.observation_tensor_shape())), game.num_distinct_actions(),
+                   dtype=case.get("model_dtype", "float64"))
   bot = _init_bot(mcts, case["config"], game, evl.AlphaZeroEvaluator(game, model),
                   case["evaluation"], backend)
   bot._random_state.seed(case["seed"])
@@ -76,7 +77,12 @@ def _play(case, backend):
   return bot
 
 
-CASE_IDS = ["%s-%d" % (c["game"].split("(")[0], c["seed"]) for c in _cases()]
+CASE_IDS = ["%s-%d-%s" % (c["game"].split("(")[0], c["seed"], c.get("model_dtype", "float64"))
+            for c in _cases()]
+F64 = [c for c in _cases() if c.get("model_dtype", "float64") == "float64"]
+F64_IDS = [i for i, c in zip(CASE_IDS, _cases()) if c in F64]
+F32 = [c for c in _cases() if c.get("model_dtype") == "float32"]
+F32_IDS = [i for i, c in zip(CASE_IDS, _cases()) if c in F32]
 
 
 @pytest.mark.parametrize("case", _cases(), ids=CASE_IDS)
@@ -103,10 +109,40 @@ def test_az_bot_is_routed_to_the_device():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", _cases(), ids=CASE_IDS)
+@pytest.mark.parametrize("case", F64, ids=F64_IDS)
 def test_gpu_equals_reference_az_bot(require_gpu, case):
   bot = _play(case, "hip")
   assert bot._use_gpu() and bot._external_eligible()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", F32, ids=F32_IDS)
+def test_float32_model_runs_the_host_loop_under_auto(require_gpu, case):
+  """A float32 model (the reference's TensorFlow one returns float32): the
+  device search, in float64, would not reproduce mcts.py's float32 sums, so
+  backend="auto" takes the host loop after the first device round refuses
+  the model -- and the searches still equal the reference's."""
+  with pytest.warns(RuntimeWarning, match="float32"):
+    bot = _play(case, "auto")
+  assert bot._f32_model and not bot._use_gpu()
+
+
+@pytest.mark.gpu
+def test_float32_model_is_refused_on_hip_without_touching_the_stream(require_gpu):
+  import pyspiel
+  from open_spiel.python.algorithms import mcts
+  from open_spiel.python.algorithms.alpha_zero import evaluator as evl
+  case = F32[0]
+  game = pyspiel.load_game(case["game"])
+  model = ToyModel(int(np.prod(game.observation_tensor_shape())), game.num_distinct_actions(),
+                   dtype=np.float32)
+  bot = _init_bot(mcts, case["config"], game, evl.AlphaZeroEvaluator(game, model),
+                  case["evaluation"], "hip")
+  bot._random_state.seed(case["seed"])
+  before = _rs_state(bot._random_state)
+  with pytest.raises(mcts.Float32ModelError):
+    bot.step(game.new_initial_state())
+  assert _rs_state(bot._random_state) == before  # the noise draw was undone
 
 
 @pytest.mark.gpu
@@ -130,7 +166,7 @@ def test_gpu_az_bot_step_matches_search(require_gpu):
     state.apply_action(a)
 
 
-@pytest.mark.parametrize("case", _cases(), ids=CASE_IDS)
+@pytest.mark.parametrize("case", F64, ids=F64_IDS)
 def test_host_compiled_az_kernel_equals_reference_az_bot(case):
   """The device search's own code (csrc/os_az.h az_step with the numpy
   policy), compiled for the host (tests/hostcheck), against the same

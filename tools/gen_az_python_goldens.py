@@ -85,6 +85,7 @@ def main():
 
   plan = [
       # game, max_simulations, moves, seeds, evaluation (no noise), alpha, eps
+      # [, model dtype]
       ("tic_tac_toe", 100, 4, [0, 42], False, 1.0, 0.25),
       # alpha > 1: the gamma draws use the polar normal, whose spare value
       # stays cached in the RandomState (has_gauss) across searches
@@ -95,16 +96,23 @@ def main():
       ("hex(board_size=5)", 150, 3, [1], False, 0.5, 0.25),
       ("breakthrough(rows=6,columns=6)", 120, 2, [2], False, 1.0, 0.25),
       ("go(board_size=7,komi=4.5)", 100, 2, [4], False, 0.03 * 361 / 49, 0.25),
+      # a float32 model, as the reference's TensorFlow one: mcts.py's sums and
+      # PUCT values then stay float32 (NumPy 2 promotion)
+      ("tic_tac_toe", 100, 3, [0], False, 1.0, 0.25, "float32"),
+      ("connect_four", 200, 3, [0], False, 1.0, 0.25, "float32"),
+      ("connect_four", 150, 2, [5], True, 1.0, 0.25, "float32"),
   ]
   cases = []
-  for gs, sims, moves, seeds, evaluation, alpha, eps in plan:
+  for entry in plan:
+    gs, sims, moves, seeds, evaluation, alpha, eps = entry[:7]
+    dtype = entry[7] if len(entry) > 7 else "float64"
     game = pyspiel.load_game(gs)
     A = game.num_distinct_actions()
     obs_size = int(np.prod(game.observation_tensor_shape()))
     for seed in seeds:
       config = {"uct_c": 2.0, "max_simulations": sims, "policy_epsilon": eps,
                 "policy_alpha": alpha}
-      model = ToyModel(obs_size, A)
+      model = ToyModel(obs_size, A, dtype=dtype)
       bot = init_bot(config, game, evl.AlphaZeroEvaluator(game, model), evaluation)
       bot._random_state.seed(seed)
       state = game.new_initial_state()
@@ -126,7 +134,7 @@ def main():
         })
         state.apply_action(best.action)
       cases.append({"game": gs, "seed": seed, "config": config, "evaluation": evaluation,
-                    "searches": searches})
+                    "model_dtype": dtype, "searches": searches})
       print("%-32s seed %d: %d searches" % (gs, seed, len(searches)))
   doc = {"_source": "tools/gen_az_python_goldens.py: unmodified reference "
                     "python/algorithms/mcts.py + alpha_zero/evaluator.py + utils/lru_cache.py, "

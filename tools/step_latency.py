@@ -111,8 +111,54 @@ def measure(gs, sims, reps, torch):
           "gpu_over_oracle": float(np.median(osecs)) / cpp_ms}
 
 
+def measure_az(gs, sims, reps):
+  """One `mcts.MCTSBot.step` of the reference's AlphaZero bot construction
+  (alpha_zero.py:185-192: PUCT, Dirichlet (0.25, 1.0), solve=False, uct_c 2,
+  the example's 300 simulations) over the AlphaZeroEvaluator drop-in, on the
+  device (backend="hip", one evaluator round per simulation) and in the host
+  loop (backend="host").  The network is tests/az_toy_model.ToyModel, which
+  costs the same few microseconds per call on both paths, so the difference
+  is the search machinery.  Both paths must choose the same action and leave
+  the RandomState in the same place."""
+  import pyspiel
+  from open_spiel.python.algorithms import mcts
+  from os_amd.az_evaluator import AlphaZeroEvaluator
+  from az_toy_model import ToyModel
+  game = pyspiel.load_game(gs)
+  st = game.new_initial_state()
+  model = ToyModel(int(np.prod(game.observation_tensor_shape())), game.num_distinct_actions())
+
+  def bot(backend):
+    rs = np.random.RandomState(3)
+    ev = AlphaZeroEvaluator(game, model)
+    return mcts.MCTSBot(game, 2.0, sims, ev, solve=False, random_state=rs,
+                        dirichlet_noise=(0.25, 1.0),
+                        child_selection_fn=mcts.SearchNode.puct_value, backend=backend), rs
+
+  row = {"game": gs, "sims": sims, "model": "ToyModel (float64)"}
+  picks = {}
+  for backend in ("hip", "host"):
+    b, _ = bot(backend)
+    b.step(st)  # warm: engine, arena, kernels
+    ts = []
+    for _ in range(reps):
+      b, rs = bot(backend)
+      t0 = time.perf_counter()
+      a = b.step(st)
+      ts.append((time.perf_counter() - t0) * 1e3)
+    picks[backend] = (a, rs.get_state()[2])
+    row[backend + "_step_ms"] = float(np.median(ts))
+    row[backend + "_steps_ms"] = ts
+  row["same_action_and_stream"] = picks["hip"] == picks["host"]
+  row["faster"] = "hip" if row["hip_step_ms"] < row["host_step_ms"] else "host"
+  return row
+
+
 def main():
   ap = argparse.ArgumentParser()
+  ap.add_argument("--az", action="store_true",
+                  help="the AlphaZero bot drop-in (device vs host loop) instead")
+  ap.add_argument("--az-sims", type=int, default=300)
   ap.add_argument("--sims", type=int, default=1000)
   ap.add_argument("--reps", type=int, default=10)
   ap.add_argument("--games", default=",".join(GAMES))
@@ -120,6 +166,23 @@ def main():
   args = ap.parse_args()
   import torch
   torch.cuda.init()
+  if args.az:
+    rows = []
+    for gs in ("connect_four", "tic_tac_toe"):
+      r = measure_az(gs, args.az_sims, args.reps)
+      rows.append(r)
+      print(json.dumps(r), flush=True)
+    os.makedirs(args.out, exist_ok=True)
+    with open(os.path.join(args.out, "az_step_latency.json"), "w") as f:
+      json.dump(rows, f, indent=1)
+    with open(os.path.join(args.out, "az_step_latency.md"), "w") as f:
+      f.write("| game | sims | device step ms (backend=hip) | host loop step ms (backend=host) "
+              "| same action + stream | faster |\n|---|---|---|---|---|---|\n")
+      for r in rows:
+        f.write("| %s | %d | %.2f | %.2f | %s | %s |\n" % (
+            r["game"], r["sims"], r["hip_step_ms"], r["host_step_ms"],
+            r["same_action_and_stream"], r["faster"]))
+    return
   rows = []
   for gs in args.games.split(","):
     r = measure(gs, args.sims, args.reps, torch)
