@@ -568,7 +568,20 @@ __host__ __device__ constexpr size_t WaveChanceLdsBytes(int path_cap) {
          static_cast<size_t>(kMaxChildren) * 2;
 }
 
-template <class G, class R, int Policy>
+#ifndef OS_CHANCE_LDS_TREE
+#define OS_CHANCE_LDS_TREE 1  // A/B knob: 0 = the arena stays in HBM
+#endif
+// kLdsTree: the search's whole arena lives in LDS (after the MT states, path
+// and expansion buffer, 16-byte aligned), and the nodes it used are copied to
+// the HBM arena when it ends, where fetch and tree export read them.  For a
+// batch of at most one search per CU whose reserved arena fits the CU's LDS
+// -- a single bot's step: pig's tree walk, wave-uniform scalar code, then
+// reads each node in ~100 cycles instead of an L2 round trip.
+template <class R>
+__host__ __device__ constexpr size_t ChanceTreeLdsOffset(size_t lds) {
+  return (lds + 15) & ~size_t(15);
+}
+template <class G, class R, int Policy, bool kLdsTree = false>
 __global__ __launch_bounds__(64) void k_wsearch_chance(DevArgs a) {
   const int64_t lr = blockIdx.x;
   if (lr >= a.num_roots) return;
@@ -602,12 +615,22 @@ __global__ __launch_bounds__(64) void k_wsearch_chance(DevArgs a) {
   const typename G::State root = make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
   typename G::Ctx ctx;
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
+  Node<R>* arena = nodes;
+  if constexpr (kLdsTree)
+    arena = reinterpret_cast<Node<R>*>(
+        smem + ChanceTreeLdsOffset<R>(WaveChanceLdsBytes<G, R>(a.path_cap)));
   SearchResult res = shared
-      ? mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, bot, path,
+      ? mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, arena, a.cap, bot, bot, path,
                                          actbuf, a.path_cap)
-      : mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, nodes, a.cap, bot, ev, path,
+      : mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, arena, a.cap, bot, ev, path,
                                          actbuf, a.path_cap);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
+  if constexpr (kLdsTree) {  // the nodes used, to the HBM arena (coalesced)
+    __syncthreads();
+    const uint32_t used = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+        static_cast<int>(res.used < a.cap ? res.used : a.cap)));
+    for (uint32_t i = static_cast<uint32_t>(l); i < used; i += 64) nodes[i] = arena[i];
+  }
   __threadfence_block();
   const Node<R> rn = nodes[0];
   const int P0 = G::to_move(root);
@@ -2009,15 +2032,28 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
       if (a.pages) return Fail(OS_ERR_UNSUPPORTED, "paged arena on the chance-node wave layout");
       const size_t lds = WaveChanceLdsBytes<G, R>(a.path_cap);
       if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
-      HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(lds)));
+      // A small batch whose reserved arenas fit the CU's LDS: the tree in LDS.
+      const size_t tree_lds =
+          ChanceTreeLdsOffset<R>(lds) + static_cast<size_t>(a.cap) * sizeof(Node<R>);
+      const bool lds_tree = a.pages == nullptr && e->num_roots <= kLdsTreeMaxRoots &&
+                            e->chunk_roots >= e->num_roots && tree_lds <= kLdsBytes &&
+                            OS_CHANCE_LDS_TREE;
+      const void* fn = lds_tree
+          ? reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy, true>)
+          : reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy, false>);
+      const size_t dyn = lds_tree ? tree_lds : lds;
+      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(dyn)));
       for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
         const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
         a.root_base = base;
         a.num_roots = n;
-        hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy>), dim3(static_cast<unsigned>(n)),
-                           dim3(64), lds, stream, a);
+        if (lds_tree)
+          hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy, true>), dim3(static_cast<unsigned>(n)),
+                             dim3(64), dyn, stream, a);
+        else
+          hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy, false>),
+                             dim3(static_cast<unsigned>(n)), dim3(64), dyn, stream, a);
         HIP_TRY(hipGetLastError());
       }
       return OS_OK;

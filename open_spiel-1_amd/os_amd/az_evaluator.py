@@ -111,8 +111,9 @@ class AlphaZeroEvaluator(Evaluator):
     The reference's mcts.py inherits the model's dtype instead (NumPy 2 keeps
     float32 in `total_reward += value` and in PUCTValue), so a model with
     float32 outputs is refused here (Float32ModelError) rather than searched
-    with different arithmetic; MCTSBot(backend="auto") then runs the host
-    loop, which is the reference's own arithmetic."""
+    with different arithmetic.  MCTSBot(backend="auto") runs a lone search
+    over this evaluator in the host loop anyway (faster, os_amd/mcts.py
+    _use_gpu), whose arithmetic is the reference's for either dtype."""
     import torch
     n, a = legal.shape
     prior = np.zeros((n, a), np.float64)

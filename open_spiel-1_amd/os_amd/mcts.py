@@ -267,7 +267,6 @@ class MCTSBot(pyspiel.Bot):
                        "and either RandomRolloutEvaluator without Dirichlet noise or an "
                        "evaluator with a batched protocol (evaluate_into / evaluate_batch)")
     self._warned_host = False
-    self._f32_model = False  # set when backend="auto" meets a float32 model
 
   def _gpu_eligible(self):
     return self._rollout_eligible() or self._external_eligible()
@@ -304,11 +303,9 @@ class MCTSBot(pyspiel.Bot):
     if self._use_gpu() and not self.verbose:
       # The engine's BestChild (mcts.py sort_key order, first maximum) is all a
       # step needs: no tree export, no SearchNode objects.
-      out = self._gpu_or_none(state)
-      if out is not None:
-        chosen = int(out[0]["best_action"][0])
-        return [(a, 1.0 if a == chosen else 0.0)
-                for a in state.legal_actions(state.current_player())], chosen
+      chosen = int(self._run_gpu(state)[0]["best_action"][0])
+      return [(a, 1.0 if a == chosen else 0.0)
+              for a in state.legal_actions(state.current_player())], chosen
     root = self.mcts_search(state)
     best = root.best_child()
     if self.verbose:
@@ -333,32 +330,30 @@ class MCTSBot(pyspiel.Bot):
     return self.step_with_policy(state)[1]
 
   def _use_gpu(self):
-    return self.backend == "hip" or (self.backend == "auto" and not self._f32_model and
-                                     self._gpu_eligible())
-
-  def _gpu_or_none(self, state):
-    """_run_gpu, or None when backend="auto" meets a model whose outputs are
-    not float64 (az_evaluator.Float32ModelError): that bot then searches on
-    the host, in the model's own arithmetic as the reference does."""
-    try:
-      return self._run_gpu(state)
-    except Float32ModelError:
-      if self.backend != "auto":
-        raise
-      self._f32_model = True
-      return None
+    """backend="auto": random-rollout searches run on the device.  A search
+    over an external evaluator does too under backend="hip", but "auto" keeps
+    it in the host loop: one bot searches one state, so every simulation is
+    one evaluator round trip (kernel step, request to the host, the model,
+    answer back), and that costs more than the host loop's whole simulation
+    -- connect_four, 300 simulations, PUCT + Dirichlet (alpha_zero.py:185-192):
+    60.6 ms per step on the device against 13.9 ms in the host loop
+    (profiles/r06/az_step_latency.md).  The batched actor (os_amd/az.py),
+    thousands of searches per round, is where the device wins."""
+    if self.backend == "hip":
+      return True
+    return self.backend == "auto" and self._rollout_eligible()
 
   def mcts_search(self, state):
     if self._use_gpu():
-      out = self._gpu_or_none(state)
-      if out is not None:
-        return tree_to_search_nodes(out[1].tree(0), state, self._game)
+      return tree_to_search_nodes(self._run_gpu(state)[1].tree(0), state, self._game)
     if self.backend == "auto" and not self._warned_host:
       # Never a silent CPU search: say once why this bot runs on the host.
-      why = ("the evaluator's model answers in float32, which the device search "
-             "(float64) would not reproduce" if self._f32_model else
-             "the GPU engine needs RandomRolloutEvaluator without Dirichlet noise or a "
-             "batched evaluator, UCT or PUCT selection and a game it runs on the device")
+      if self._external_eligible():
+        why = ("one search over an external evaluator is faster in the host loop than "
+               "one device round trip per simulation; backend='hip' runs it on the device")
+      else:
+        why = ("the GPU engine needs RandomRolloutEvaluator without Dirichlet noise or a "
+               "batched evaluator, UCT or PUCT selection and a game it runs on the device")
       warnings.warn("MCTSBot(backend='auto') runs this search on the host CPU (%s); "
                     "pass backend='host' to silence this or backend='hip' to make it "
                     "an error" % why, RuntimeWarning, stacklevel=2)

@@ -91,7 +91,7 @@ def test_host_loop_equals_reference_az_bot(case):
   assert not bot._use_gpu()
 
 
-def test_az_bot_is_routed_to_the_device():
+def test_az_bot_device_eligibility_and_auto_routing():
   import pyspiel
   from open_spiel.python.algorithms import mcts
   from open_spiel.python.algorithms.alpha_zero import evaluator as evl
@@ -100,6 +100,11 @@ def test_az_bot_is_routed_to_the_device():
   cfg = {"uct_c": 2.0, "max_simulations": 50, "policy_epsilon": 0.25, "policy_alpha": 1.0}
   bot = _init_bot(mcts, cfg, game, ev, False, "auto")
   assert bot._gpu_eligible() and bot._external_eligible() and not bot._rollout_eligible()
+  # one search over an external evaluator: "auto" keeps the host loop (faster
+  # than a device round trip per simulation, profiles/r06/az_step_latency.md);
+  # "hip" runs it on the device
+  assert not bot._use_gpu()
+  assert _init_bot(mcts, cfg, game, ev, False, "hip")._use_gpu()
   # a chance game, or a custom selection function, stays on the host
   pig = pyspiel.load_game("pig")
   with pytest.raises(ValueError):
@@ -115,16 +120,15 @@ def test_gpu_equals_reference_az_bot(require_gpu, case):
   assert bot._use_gpu() and bot._external_eligible()
 
 
-@pytest.mark.gpu
 @pytest.mark.parametrize("case", F32, ids=F32_IDS)
-def test_float32_model_runs_the_host_loop_under_auto(require_gpu, case):
+def test_float32_model_under_auto_equals_reference(case):
   """A float32 model (the reference's TensorFlow one returns float32): the
-  device search, in float64, would not reproduce mcts.py's float32 sums, so
-  backend="auto" takes the host loop after the first device round refuses
-  the model -- and the searches still equal the reference's."""
-  with pytest.warns(RuntimeWarning, match="float32"):
+  host loop that backend="auto" runs computes in the model's dtype, as the
+  reference mcts.py does under NumPy 2, so the searches equal the
+  reference's float32 fixtures."""
+  with pytest.warns(RuntimeWarning, match="host loop"):
     bot = _play(case, "auto")
-  assert bot._f32_model and not bot._use_gpu()
+  assert not bot._use_gpu()
 
 
 @pytest.mark.gpu
