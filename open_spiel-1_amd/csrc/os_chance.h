@@ -214,7 +214,9 @@ OS_HD SearchResult mcts_search_chance(const GameCfg& g, const SearchParams& sp,
           if (k) ret.add(code, g);
           else ret.set(code, g);
         }
-        ret.div(sp.n_rollouts);  // x / 1 == x: the single-rollout case too
+        // The reference divides by n_rollouts (mcts.cc:69) -- for one rollout
+        // x / 1 == x exactly, so the kMaxPlayers f64 divisions are skipped.
+        if (sp.n_rollouts != 1) ret.div(sp.n_rollouts);
       }
       // ---- backup + MCTS-Solver (mcts.cc:351-396) ----
       for (int d = depth; d >= 0; --d) {

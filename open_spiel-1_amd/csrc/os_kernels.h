@@ -389,7 +389,7 @@ struct WaveCtxMaker<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes + gr * a.hash_stride;
     c.n_base = a.root_nhash[gr];
-    c.init_filters(a.cfg.rows * a.cfg.cols);
+    c.init_filters();
     return c;
   }
 };
@@ -572,8 +572,9 @@ __host__ __device__ constexpr size_t WaveChanceLdsBytes(int path_cap) {
 #define OS_CHANCE_LDS_TREE 1  // A/B knob: 0 = the arena stays in HBM
 #endif
 // kLdsTree: the search's whole arena lives in LDS (after the MT states, path
-// and expansion buffer, 16-byte aligned), and the nodes it used are copied to
-// the HBM arena when it ends, where fetch and tree export read them.  For a
+// and expansion buffer, 16-byte aligned; the log / sqrt LUT after it), and the
+// nodes it used are copied to the HBM arena when it ends, where fetch and
+// tree export read them.  For a
 // batch of at most one search per CU whose reserved arena fits the CU's LDS
 // -- a single bot's step: pig's tree walk, wave-uniform scalar code, then
 // reads each node in ~100 cycles instead of an L2 round trip.
@@ -616,13 +617,20 @@ __global__ __launch_bounds__(64) void k_wsearch_chance(DevArgs a) {
   typename G::Ctx ctx;
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   Node<R>* arena = nodes;
-  if constexpr (kLdsTree)
-    arena = reinterpret_cast<Node<R>*>(
-        smem + ChanceTreeLdsOffset<R>(WaveChanceLdsBytes<G, R>(a.path_cap)));
+  SearchParams sp = a.sp;
+  if constexpr (kLdsTree) {
+    // [.. | arena (cap nodes) | log / sqrt LUT (max_simulations + 1)]
+    const size_t off = ChanceTreeLdsOffset<R>(WaveChanceLdsBytes<G, R>(a.path_cap));
+    arena = reinterpret_cast<Node<R>*>(smem + off);
+    double* lut = reinterpret_cast<double*>(smem + off + static_cast<size_t>(a.cap) * sizeof(Node<R>));
+    for (int i = l; i <= a.sp.max_simulations; i += 64) lut[i] = a.sp.log_lut[i];
+    __syncthreads();
+    sp.log_lut = lut;
+  }
   SearchResult res = shared
-      ? mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, arena, a.cap, bot, bot, path,
+      ? mcts_search_chance<G, R, Policy>(a.cfg, sp, root, ctx, arena, a.cap, bot, bot, path,
                                          actbuf, a.path_cap)
-      : mcts_search_chance<G, R, Policy>(a.cfg, a.sp, root, ctx, arena, a.cap, bot, ev, path,
+      : mcts_search_chance<G, R, Policy>(a.cfg, sp, root, ctx, arena, a.cap, bot, ev, path,
                                          actbuf, a.path_cap);
   res.rng_words = bot.words.get() + (shared ? 0u : ev.words.get());
   if constexpr (kLdsTree) {  // the nodes used, to the HBM arena (coalesced)
@@ -795,7 +803,7 @@ struct SpCtx<Go> {
     c.zob = a.zob;
     c.base = a.hist + gg * a.hash_stride;
     c.n_base = a.hist_n[gg];
-    c.init_filters(a.cfg.rows * a.cfg.cols);
+    c.init_filters();
     return c;
   }
   // The move just applied logged its position (go.cc:199-208): it joins the
@@ -1147,7 +1155,7 @@ struct WazCtx<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes + r * a.hash_stride;
     c.n_base = a.root_nhash[r];
-    c.init_filters(a.cfg.rows * a.cfg.cols);
+    c.init_filters();
     return c;
   }
   // The pending simulation's positions since the root follow the base.
@@ -1711,14 +1719,14 @@ template <class G>
 struct RollCtx {
   using type = NoCtx;
   static constexpr int kLdsWords = 1;
-  __device__ static NoCtx make(const RollArgs&, int64_t, uint32_t*, int) { return NoCtx(); }
+  __device__ static NoCtx make(const RollArgs&, int64_t, uint32_t*) { return NoCtx(); }
 };
 #if OS_ROLL_BLOOM
 template <>
 struct RollCtx<Go> {
   using type = GoCtxBloom;
   static constexpr int kLdsWords = GoCtxBloom::kWords * 64;
-  __device__ static GoCtxBloom make(const RollArgs& a, int64_t i, uint32_t* lds, int lanes) {
+  __device__ static GoCtxBloom make(const RollArgs& a, int64_t i, uint32_t* lds) {
     GoCtxBloom c;
     c.zob = a.zob;
     c.base = a.root_hashes;
@@ -1730,8 +1738,8 @@ struct RollCtx<Go> {
     c.log = a.glog + i;
     c.stride = static_cast<int32_t>(a.n);
 #endif
-    c.filt = lds + threadIdx.x;
-    c.filt_stride = lanes;
+    c.filt = lds + (threadIdx.x & 63);
+    c.filt_stride = 64;
     c.cap = kGoLogCap;
     c.init_filters();
     return c;
@@ -1747,8 +1755,7 @@ struct RollCtx<Go> {
   // The bucket heads are the only per-move accesses that differ across the
   // lanes (each lane is at its own stone count): they live in LDS, lane-
   // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
-  // lanes: the block's width (the stride of the lane-interleaved LDS arrays).
-  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds, int lanes) {
+  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds) {
     uint8_t* lds_heads = reinterpret_cast<uint8_t*>(lds);
     uint16_t* glink = reinterpret_cast<uint16_t*>(a.glink);
     type c;
@@ -1764,10 +1771,10 @@ struct RollCtx<Go> {
     c.link = glink + i;
     c.stride = static_cast<int32_t>(a.n);
 #endif
-    c.head = lds_heads + threadIdx.x;
-    c.head_stride = lanes;
+    c.head = lds_heads + (threadIdx.x & 63);
+    c.head_stride = 64;
 #if OS_GO_LOG_BLOOM
-    c.bloom = lds + (((a.cfg.rows * a.cfg.cols + 1) * lanes + 3) / 4) + threadIdx.x;
+    c.bloom = lds + (((a.cfg.rows * a.cfg.cols + 1) * 64 + 3) / 4) + (threadIdx.x & 63);
 #endif
     c.n_log = 0;
     c.cap = kGoLogCap;
@@ -1789,7 +1796,7 @@ struct WaveRollCtx<Go> {
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
-    c.init_filters(a.cfg.rows * a.cfg.cols);
+    c.init_filters();
     return c;
   }
 };
@@ -1856,7 +1863,7 @@ __global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
 #endif
   ev.seed(a.seeds[i]);
   extern __shared__ uint32_t roll_lds[];  // RollLdsBytes<G>(cfg) bytes
-  typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds, static_cast<int>(blockDim.x));
+  typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
   const typename G::State root = *static_cast<const typename G::State*>(a.root);
   double s0 = 0.0, s1 = 0.0;
   uint32_t moves = 0;
@@ -2033,8 +2040,9 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
       const size_t lds = WaveChanceLdsBytes<G, R>(a.path_cap);
       if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
       // A small batch whose reserved arenas fit the CU's LDS: the tree in LDS.
-      const size_t tree_lds =
-          ChanceTreeLdsOffset<R>(lds) + static_cast<size_t>(a.cap) * sizeof(Node<R>);
+      const size_t tree_lds = ChanceTreeLdsOffset<R>(lds) +
+                              static_cast<size_t>(a.cap) * sizeof(Node<R>) +
+                              static_cast<size_t>(a.sp.max_simulations + 1) * sizeof(double);
       const bool lds_tree = a.pages == nullptr && e->num_roots <= kLdsTreeMaxRoots &&
                             e->chunk_roots >= e->num_roots && tree_lds <= kLdsBytes &&
                             OS_CHANCE_LDS_TREE;
@@ -2284,28 +2292,15 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
 // k_rollouts' dynamic LDS: go's bucket heads for this board size (one byte
 // per stone count per lane) and the log's Bloom filter; the heads' static
 // bound (11 x 11) would cost occupancy on 9 x 9.
-// Playouts (active lanes) per wave of k_rollouts.  A lane runs a whole
-// playout; below OS_ROLL_FULL playouts, 64-lane waves leave fewer than four
-// waves per SIMD to hide each other's stalls, so the block narrows to 32
-// lanes (A/B knob OS_ROLL_NARROW: the width used there).
-#ifndef OS_ROLL_NARROW
-#define OS_ROLL_NARROW 64
-#endif
-#ifndef OS_ROLL_FULL
-#define OS_ROLL_FULL (int64_t{4} * 1024 * 64)
-#endif
-inline int RollLanes(int64_t n) { return n < OS_ROLL_FULL ? OS_ROLL_NARROW : 64; }
-
 template <class G>
-size_t RollLdsBytes(const GameCfg& c, int lanes) {
+size_t RollLdsBytes(const GameCfg& c) {
 #if OS_ROLL_BLOOM
   (void)c;
-  (void)lanes;
   return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #else
   if constexpr (std::is_same<G, Go>::value)
-    return 4 * (((c.rows * c.cols + 1) * lanes + 3) / 4 +
-                (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * lanes : 0));
+    return 4 * (((c.rows * c.cols + 1) * 64 + 3) / 4 +
+                (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * 64 : 0));
   else
     return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #endif
@@ -2340,9 +2335,13 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
     }
   }
   {
-    const int bs = RollLanes(n);
+    // 64 lanes per block: 32-lane blocks (four waves per SIMD at C5's
+    // per-rank 131072 playouts instead of two) were slower, 2.36 -> 3.16 ms
+    // (profiles/r06/ab_narrow): a wave instruction then serves half as many
+    // playouts, and this kernel's VALU is already half busy.
+    const int bs = 64;
     hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                       dim3(bs), RollLdsBytes<G>(a.cfg, bs), stream, a);
+                       dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
   }
   HIP_TRY(hipGetLastError());
   return OS_OK;

@@ -493,49 +493,14 @@ struct GoWaveCtx {
   int32_t n;              // entries held (base included)
   int32_t cand_end;       // entries [0, cand_end) can repeat a new position
   uint64_t s0, s1, s2, s3;  // per lane: entries lane, lane + 64, + 128, + 192
-  // Per lane: the Zobrist values of points lane (z0) and lane + 64 (z1) for
-  // black (c0) and white (c1), so the playout's hash updates are readlanes
-  // and one lane reduction, not dependent loads of zob[] per stone.
-  uint64_t z0c0, z0c1, z1c0, z1c1;
 
   __device__ void reset() {
     n = n_base;
     cand_end = n_base;
   }
-  // zob[2 p + c] (go.cc ZobristTable order).
-  __device__ uint64_t zpoint(int p, int c) const {
-    const uint64_t v0 = c ? z0c1 : z0c0, v1 = c ? z1c1 : z1c0;
-    return p < 64 ? rl64(v0, p) : rl64(v1, p - 64);
-  }
-  // XOR of zob[2 p + c] over the points p of m: every lane contributes its
-  // two points, the row butterflies leave each row's XOR in all its lanes,
-  // and the scalar unit joins the four rows.
-  __device__ uint64_t zset(B128 m, int c) const {
+  // Copies the base into the slots (every lane loads its four entries).
+  __device__ void init_filters() {
     const int l = lane_id();
-    uint64_t v = (((m.lo >> l) & 1ull) ? (c ? z0c1 : z0c0) : 0ull) ^
-                 (((m.hi >> l) & 1ull) ? (c ? z1c1 : z1c0) : 0ull);
-    uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
-#define OS_XOR_DPP(ctrl)                                                                        \
-  lo ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(lo), ctrl, 0xf, 0xf, \
-                                                          false));                               \
-  hi ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(hi), ctrl, 0xf, 0xf, false))
-    OS_XOR_DPP(0xB1);   // quad_perm [1,0,3,2]
-    OS_XOR_DPP(0x4E);   // quad_perm [2,3,0,1]
-    OS_XOR_DPP(0x141);  // row_half_mirror
-    OS_XOR_DPP(0x140);  // row_mirror
-#undef OS_XOR_DPP
-    const uint32_t rlo = rl32(lo, 0) ^ rl32(lo, 16) ^ rl32(lo, 32) ^ rl32(lo, 48);
-    const uint32_t rhi = rl32(hi, 0) ^ rl32(hi, 16) ^ rl32(hi, 32) ^ rl32(hi, 48);
-    return (static_cast<uint64_t>(rhi) << 32) | rlo;
-  }
-  // Copies the base into the slots (every lane loads its four entries) and
-  // the Zobrist values of the board's npts points into the lanes.
-  __device__ void init_filters(int npts) {
-    const int l = lane_id();
-    z0c0 = l < npts ? zob[2 * l] : 0ull;
-    z0c1 = l < npts ? zob[2 * l + 1] : 0ull;
-    z1c0 = l + 64 < npts ? zob[2 * (l + 64)] : 0ull;
-    z1c1 = l + 64 < npts ? zob[2 * (l + 64) + 1] : 0ull;
     n_base = n_base < kCap ? n_base : kCap;
     s0 = l < n_base ? base[l] : 0ull;
     s1 = l + 64 < n_base ? base[l + 64] : 0ull;
@@ -1860,6 +1825,9 @@ __device__ __forceinline__ uint32_t wave_scan_map4(uint32_t f) {
 // there; numpy then draws nothing), the horizon (the first node with
 // total_moves >= horizon), otherwise the turn's bank or bust.  The same
 // words, moves and outcomes as the serial walk (pig_rollout_wave).
+#ifndef OS_PIG_PAR2
+#define OS_PIG_PAR2 1  // A/B knob: 0 = two players walk the turns like n players
+#endif
 template <int Policy>
 __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
   s = make_uniform(s);
@@ -1876,14 +1844,18 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
   const int win = g.pig_win, hz = g.pig_horizon, np = g.pig_players, dice = g.pig_dice;
   const double p = 1.0 / dice;  // Pig::chance_prob
   int tp = s.turn_player, tt = s.turn_total, moves = s.moves;
-  uint32_t role0 = s.cur < 0 ? kChance : kDec;  // role of the window's word 0
+  uint32_t role0 = s.cur < 0 ? kChance : kDec;  // numpy: role of the window's word 0
+  bool chance0 = s.cur < 0;                      // C++: the window's node 0 is a chance node
+  // A lane is a node under the C++ policy (two words each: 64 nodes, 128
+  // words per window) and a word under numpy (64 words per window).
+  constexpr int kWordsPerLane = kCpp ? 2 : 1;
   int wb = ev.offset();  // stream offset of the window's word 0 (current block)
   int used = 0;          // words drawn
   bool chance_end = false;
   for (;;) {
-    const uint32_t w0 = MtStream::temper(ev.peek_raw(wb + l));
-    const uint32_t w1 = MtStream::temper(ev.peek_raw(wb + l + 1));
-    int o;  // chance action 1..dice if this word starts a chance node
+    const uint32_t w0 = MtStream::temper(ev.peek_raw(wb + kWordsPerLane * l));
+    const uint32_t w1 = MtStream::temper(ev.peek_raw(wb + kWordsPerLane * l + 1));
+    int o;  // chance action 1..dice if this lane starts a chance node
     if (kCpp) {
       uint64_t bits = (static_cast<uint64_t>(w0) << 32) | w1;  // AbslUniformDouble01
       double u = 0.0;
@@ -1909,17 +1881,34 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
     }
     // A decision's action: C++ the low bit of its second word
     // (AbslUniform(2)), numpy the low bit of its word (mask 1, never
-    // rejected); 0 = roll.  own_roll: this word read as the deciding word.
-    const bool own_roll = (w0 & 1u) == 0;
+    // rejected); 0 = roll.
     const bool stop_here = ((kCpp ? w1 : w0) & 1u) != 0;  // the decision starting here stops
-    // Transition map of this word (role -> role of the next word).
-    const uint32_t f = kCpp ? (1u | ((own_roll ? 2u : 0u) << 2) | (3u << 4) | (0u << 6))
-                            : ((own_roll ? 2u : 0u) | (1u << 2) | (3u << 4) | (0u << 6));
-    const uint32_t F = wave_scan_map4(f);  // role of word l + 1 = F(role0)
-    const uint32_t after = map4_apply(F, role0);
-    const uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(after), 1));
-    const uint32_t role = l == 0 ? role0 : prev;
-    const bool dec = role == kDec, chn = role == kChance;
+    bool dec, chn;
+    uint32_t after = 0;  // numpy: role of the next word
+    if (kCpp) {
+      // Node types from one ballot: after a node read as a stop the next node
+      // is a decision (a stop, and a chance outcome, lead to one), and along
+      // a run of roll-reading nodes the types alternate (a roll leads to a
+      // chance node, a chance node back to a decision) -- from the last stop
+      // below this lane, or from the window's first node.
+      const uint64_t m = ballot(stop_here) & below;
+      const bool odd = m ? ((l - (63 - static_cast<int>(__clzll(static_cast<long long>(m)))) - 1) & 1)
+                         : (l & 1);
+      chn = odd != chance0;
+      if (m) chn = odd;
+      dec = !chn;
+    } else {
+      // Word roles: a 4-state automaton (decision, -, chance word 1, chance
+      // word 2) scanned over the lanes' transition maps.
+      const bool own_roll = (w0 & 1u) == 0;
+      const uint32_t f = (own_roll ? 2u : 0u) | (1u << 2) | (3u << 4) | (0u << 6);
+      const uint32_t F = wave_scan_map4(f);  // role of word l + 1 = F(role0)
+      after = map4_apply(F, role0);
+      const uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(after), 1));
+      const uint32_t role = l == 0 ? role0 : prev;
+      dec = role == kDec;
+      chn = role == kChance;
+    }
     const bool stop = dec && stop_here, bust = chn && o == 1;
     const uint32_t gain = (chn && o != 1) ? static_cast<uint32_t>(o + 1) : 0u;
     const uint64_t endm = ballot(stop || bust);
@@ -1929,46 +1918,97 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
     const int mv = moves + static_cast<int>(__builtin_popcountll(dm & below));  // total_moves here
     const uint64_t hzm = ballot((dec || chn) && mv >= hz);
     const int jh = hzm ? static_cast<int>(ctz64(hzm)) : 64;
-    int pos = 0, end_words = -1;
-    while (pos < 64) {
-      const uint64_t from = ~((1ull << pos) - 1ull);
-      const uint64_t e = endm & from;
-      const int b = e ? static_cast<int>(ctz64(e)) : 64;  // the turn's last node (its first word)
-      const int lim = b < 64 ? b : 63;
-      const uint64_t seg = from & (lim == 63 ? ~0ull : ((1ull << (lim + 1)) - 1ull));
-      const int pexpos = rli(pex, pos);
-      const int cs = rli(static_cast<int32_t>(sc), tp);
-      const int need = win - cs - tt + pexpos;  // tt + pex_j - pex_pos >= win - cs
-      const uint64_t wm = ballot(dec && pex >= need) & seg;
+    int end_words = -1;
+    if (np == 2 && OS_PIG_PAR2) {
+      // Two players: no walk at all.  Per word: the turns ended before it
+      // (mbcnt of the ends), its turn's first word (the last end below it),
+      // hence its turn total (gains since that word, one bpermute) and its
+      // turn's player (tp flipped per turn); a stop banks its turn total, and
+      // each player's banks are one prefix sum, so every decision knows its
+      // player's score and the first one that can win by stopping is a
+      // ballot away, as is the horizon.
+      const uint64_t eb = endm & below;
+      const int tix = static_cast<int>(__builtin_popcountll(eb));
+      const int seg0 = eb ? 64 - static_cast<int>(__clzll(static_cast<long long>(eb))) : 0;
+      const int pstart = __shfl(pex, seg0);
+      const int ttj = (tix == 0 ? tt : 0) + pex - pstart;  // turn total before this word
+      const int pj = tp ^ (tix & 1);                        // its turn's player
+      const uint32_t bank = stop ? static_cast<uint32_t>(ttj) : 0u;
+      const uint32_t b0 = pj == 0 ? bank : 0u, b1 = bank - b0;
+      const uint32_t S0 = wave_scan_add32(b0), S1 = wave_scan_add32(b1);
+      const int E0 = static_cast<int>(S0 - b0), E1 = static_cast<int>(S1 - b1);
+      const int sc0 = static_cast<int>(rl32(sc, 0)), sc1 = static_cast<int>(rl32(sc, 1));
+      const int csj = pj == 0 ? sc0 + E0 : sc1 + E1;  // its player's banked score
+      const uint64_t wm = ballot(dec && csj + ttj >= win);
       const int jw = wm ? static_cast<int>(ctz64(wm)) : 64;
-      if (jw <= lim || jh <= lim) {
-        if (jw < jh) {  // only stop is legal: bank and win (pig.cc:151-152, 193-199)
-          const int bank = cs + tt + rli(pex, jw) - pexpos;
-          sc = l == tp ? static_cast<uint32_t>(bank) : sc;
-          tt = 0;
-          tp = tp + 1 < np ? tp + 1 : 0;
-          moves = rli(mv, jw) + 1;
-          end_words = jw + (kCpp ? 2 : 0);
-          chance_end = false;
-        } else {  // total_moves reached the horizon before node jh
-          tt += rli(pex, jh) - pexpos;
-          moves = rli(mv, jh);
-          end_words = jh;
-          chance_end = rli(static_cast<int32_t>(role), jh) == static_cast<int>(kChance);
+      int n0, n1;
+      if (jw < 64 && jw < jh) {  // only stop is legal: bank and win (pig.cc:151-152, 193-199)
+        const int p = rli(pj, jw), t = rli(ttj, jw);
+        n0 = sc0 + rli(E0, jw) + (p == 0 ? t : 0);
+        n1 = sc1 + rli(E1, jw) + (p == 1 ? t : 0);
+        tt = 0;
+        tp = p ^ 1;
+        moves = rli(mv, jw) + 1;
+        end_words = kWordsPerLane * jw + (kCpp ? 2 : 0);
+        chance_end = false;
+      } else if (jh < 64) {  // total_moves reached the horizon before node jh
+        n0 = sc0 + rli(E0, jh);
+        n1 = sc1 + rli(E1, jh);
+        tt = rli(ttj, jh);
+        tp = rli(pj, jh);
+        moves = rli(mv, jh);
+        end_words = kWordsPerLane * jh;
+        chance_end = rli(chn ? 1 : 0, jh) != 0;
+      } else {  // the whole window: the state after its last word
+        n0 = sc0 + static_cast<int>(rl32(S0, 63));
+        n1 = sc1 + static_cast<int>(rl32(S1, 63));
+        const bool e63 = (endm >> 63) & 1ull;
+        tt = e63 ? 0 : rli(ttj, 63) + static_cast<int>(rl32(gain, 63));
+        tp = rli(pj, 63) ^ (e63 ? 1 : 0);
+      }
+      sc = l == 0 ? static_cast<uint32_t>(n0) : (l == 1 ? static_cast<uint32_t>(n1) : sc);
+    } else {
+      int pos = 0;
+      while (pos < 64) {
+        const uint64_t from = ~((1ull << pos) - 1ull);
+        const uint64_t e = endm & from;
+        const int b = e ? static_cast<int>(ctz64(e)) : 64;  // the turn's last node (its first word)
+        const int lim = b < 64 ? b : 63;
+        const uint64_t seg = from & (lim == 63 ? ~0ull : ((1ull << (lim + 1)) - 1ull));
+        const int pexpos = rli(pex, pos);
+        const int cs = rli(static_cast<int32_t>(sc), tp);
+        const int need = win - cs - tt + pexpos;  // tt + pex_j - pex_pos >= win - cs
+        const uint64_t wm = ballot(dec && pex >= need) & seg;
+        const int jw = wm ? static_cast<int>(ctz64(wm)) : 64;
+        if (jw <= lim || jh <= lim) {
+          if (jw < jh) {  // only stop is legal: bank and win (pig.cc:151-152, 193-199)
+            const int bank = cs + tt + rli(pex, jw) - pexpos;
+            sc = l == tp ? static_cast<uint32_t>(bank) : sc;
+            tt = 0;
+            tp = tp + 1 < np ? tp + 1 : 0;
+            moves = rli(mv, jw) + 1;
+            end_words = kWordsPerLane * jw + (kCpp ? 2 : 0);
+            chance_end = false;
+          } else {  // total_moves reached the horizon before node jh
+            tt += rli(pex, jh) - pexpos;
+            moves = rli(mv, jh);
+            end_words = kWordsPerLane * jh;
+            chance_end = rli(chn ? 1 : 0, jh) != 0;
+          }
+          break;
         }
-        break;
+        if (b == 64) {  // the turn goes on into the next window
+          tt += static_cast<int>(rl32(P, 63)) - pexpos;
+          break;
+        }
+        if (rli(dec ? 1 : 0, b) != 0) {  // stop: bank
+          const int bank = cs + tt + rli(pex, b) - pexpos;
+          sc = l == tp ? static_cast<uint32_t>(bank) : sc;
+        }
+        tt = 0;  // stop or a 1 (pig.cc:193-199, 205-210)
+        tp = tp + 1 < np ? tp + 1 : 0;
+        pos = b + 1;
       }
-      if (b == 64) {  // the turn goes on into the next window
-        tt += static_cast<int>(rl32(P, 63)) - pexpos;
-        break;
-      }
-      if (rli(static_cast<int32_t>(role), b) == static_cast<int>(kDec)) {  // stop: bank
-        const int bank = cs + tt + rli(pex, b) - pexpos;
-        sc = l == tp ? static_cast<uint32_t>(bank) : sc;
-      }
-      tt = 0;  // stop or a 1 (pig.cc:193-199, 205-210)
-      tp = tp + 1 < np ? tp + 1 : 0;
-      pos = b + 1;
     }
     if (end_words >= 0) {
       used += end_words;
@@ -1976,9 +2016,12 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
       break;
     }
     moves += static_cast<int>(__builtin_popcountll(dm));
-    role0 = static_cast<uint32_t>(rli(static_cast<int32_t>(after), 63));
-    used += 64;
-    wb += 64;
+    if (kCpp)  // after node 63: a chance node iff it is a decision that rolls
+      chance0 = rli((dec && !stop_here) ? 1 : 0, 63) != 0;
+    else
+      role0 = static_cast<uint32_t>(rli(static_cast<int32_t>(after), 63));
+    used += 64 * kWordsPerLane;
+    wb += 64 * kWordsPerLane;
     if (wb >= kMtN) {  // the next window starts in the next block: twist, rebase
       ev.seek(wb);
       wb -= kMtN;
@@ -2000,9 +2043,17 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
 #ifndef OS_PIG_TURNS
 #define OS_PIG_TURNS 1
 #endif
+// OS_AB_PIG_NOROLL (timing-only attribution builds; results are NOT the
+// reference's): 1 = every playout returns at once.
+#ifndef OS_AB_PIG_NOROLL
+#define OS_AB_PIG_NOROLL 0
+#endif
 template <int Policy>
 struct ChanceRollout<Pig, Policy, WaveMt> {
   __device__ static int run(const Pig::State& s, const GameCfg& g, NoCtx&, WaveMt& ev) {
+#if OS_AB_PIG_NOROLL
+    return 0;
+#endif
 #if OS_PIG_TURNS
     return pig_rollout_turns<Policy>(s, g, ev);
 #else
@@ -2237,136 +2288,7 @@ __device__ __forceinline__ int go_kth_lanes(B128 mask, int k, int pass) {
 }
 
 // GoT::apply (go_board.cc:217-299 via go.cc:124-216) with chains from labels.
-// Two forms of the same move (identical states, hashes and logs):
-//  * go_apply_lanes_par (C++ policy): the Zobrist values sit in the lanes
-//    (GoWaveCtx::zpoint / zset: readlanes and one lane reduction instead of
-//    a dependent zob[] load per stone), and a's four neighbours' labels are
-//    read up front -- the own chains they name are relabelled at once, the
-//    opponent chains taken one after another without a label -> chain ->
-//    next-neighbour round trip;
-//  * go_apply_lanes_serial (numpy policy): chain by chain.  The numpy wave
-//    kernel sits at the edge of its register budget (its shuffles keep more
-//    state live), and the parallel form's extra scalars push it into scratch
-//    (248 VGPRs + 1.1 KB scratch against 115 VGPRs).
-__device__ __forceinline__ void go_apply_lanes_par(Go::State& s, GoSides& sd, const GameCfg& g,
-                                               GoWaveCtx& ctx, GoLabels& lab,
-                                               const GoNbrLanes& nbl, int a) {
-  using M = CfgMasks<B128>;
-  const int c = s.to_play;
-  const int pass = g.rows * g.cols;
-  s.flags = static_cast<uint8_t>((s.flags & Go::kSuperko) |
-                                 ((s.flags & Go::kLastPass) ? Go::kPrevPass : 0));
-  if (a == pass) {
-    s.ko = -1;
-    s.flags |= Go::kLastPass;
-    const B128 t = sd.me;
-    sd.me = sd.them;
-    sd.them = t;
-  } else {
-#if OS_PHASE_TIMING
-    uint64_t tx = OS_PH_NOW();
-#endif
-    const B128 pb = bit128(a);
-    const B128 nb = nbl.at(a);
-    const B128 own0 = sd.me;
-    const B128 own = own0 | pb;
-    B128 opp = sd.them;
-    const bool enemy_eye = !any(nb & ~opp);
-    s.hash ^= ctx.zpoint(a, c);
-    B128 E = M::board(g) & ~(own | opp);
-    // a's (up to four) neighbours, each with its label read up front: the
-    // readlanes are independent, so they issue back to back instead of one
-    // label -> chain -> next neighbour round trip per chain.
-    const int n = g.rows;
-    const int col = a % n;
-    const int q0 = a - n, q1 = col > 0 ? a - 1 : -1, q2 = col < n - 1 ? a + 1 : -1, q3 = a + n;
-    const int npts = g.rows * g.cols;
-    const bool v0 = q0 >= 0, v1 = q1 >= 0, v2 = q2 >= 0, v3 = q3 < npts;
-    const int L0 = v0 ? lab.at(q0) : -2, L1 = v1 ? lab.at(q1) : -2;
-    const int L2 = v2 ? lab.at(q2) : -2, L3 = v3 ? lab.at(q3) : -2;
-    // Own chains next to a join the new stone's chain, labelled a: one
-    // relabel of all four neighbours' labels (an opponent's or an empty
-    // point's label never names an own chain's stone: labels are stones of
-    // their own chain, and stale labels name empty points).
-    {
-      const bool o0 = v0 && test(own0, q0), o1 = v1 && test(own0, q1);
-      const bool o2 = v2 && test(own0, q2), o3 = v3 && test(own0, q3);
-      const int J0 = o0 ? L0 : -2, J1 = o1 ? L1 : -2, J2 = o2 ? L2 : -2, J3 = o3 ? L3 : -2;
-      lab.l0 = (lab.l0 == J0 || lab.l0 == J1 || lab.l0 == J2 || lab.l0 == J3) ? a : lab.l0;
-      lab.l1 = (lab.l1 == J0 || lab.l1 == J1 || lab.l1 == J2 || lab.l1 == J3) ? a : lab.l1;
-    }
-    lab.set(a, a);
-#if OS_PHASE_TIMING
-    OS_PH_ADD(ctx.sub[kPhX0], tx);
-    tx = OS_PH_NOW();
-#endif
-    int captured = 0;
-    int cap_pt = -1;
-    B128 atari = s.atari;
-    B128 capd = b128(0, 0);
-    // Adjacent opponent chains, in neighbour order, each once (a chain next
-    // to a twice is met at its first neighbour).  Their liberty sets do not
-    // interact: a captured chain's points were opponent stones, so none of
-    // them touches another opponent chain (it would be the same chain).
-    {
-      // (an empty neighbour may carry a stale label equal to a live chain's,
-      // so only opponent neighbours are compared)
-      const bool o0 = v0 && test(opp, q0), o1 = v1 && test(opp, q1);
-      const bool o2 = v2 && test(opp, q2), o3 = v3 && test(opp, q3);
-      auto take = [&](int L, int q) {
-        const B128 ch = lab.chain(L) & opp;
-        const B128 libs = nbl.any(ch) & E;
-        if (!any(libs)) {
-          opp = opp & ~ch;
-          E = E | ch;
-          capd = capd | ch;
-          captured += popc(ch);
-          cap_pt = q;
-        }
-        atari = (atari & ~ch) | sel128(popc(libs) == 1, ch, b128(0, 0));
-      };
-      if (o0) take(L0, q0);
-      if (o1 && !(o0 && L0 == L1)) take(L1, q1);
-      if (o2 && !(o0 && L0 == L2) && !(o1 && L1 == L2)) take(L2, q2);
-      if (o3 && !(o0 && L0 == L3) && !(o1 && L1 == L3) && !(o2 && L2 == L3)) take(L3, q3);
-    }
-    if (captured) s.hash ^= ctx.zset(capd, 1 - c);
-#if OS_PHASE_TIMING
-    OS_PH_ADD(ctx.sub[kPhX1], tx);
-    tx = OS_PH_NOW();
-#endif
-    // The mover's chain (label a) and, after captures, the own chains next to
-    // the captured stones.  (Skipping the liberty counts where the atari set
-    // or two empty neighbours settle them was measured slower here: 1.70e7 ->
-    // 1.63e7 sims/s at 4096 roots; the lane kernels do use it, GoT::apply.)
-    {
-      const B128 ch = lab.chain(a) & own;
-      atari = (atari & ~ch) | sel128(popc(nbl.any(ch) & E) == 1, ch, b128(0, 0));
-      B128 todo = any(capd) ? nbl.any(capd) & own & ~ch : b128(0, 0);
-      while (any(todo)) {
-        const B128 cx = lab.chain(lab.at(lowest(todo))) & own;
-        todo = todo & ~cx;
-        atari = (atari & ~cx) | sel128(popc(nbl.any(cx) & E) == 1, cx, b128(0, 0));
-      }
-    }
-#if OS_PHASE_TIMING
-    OS_PH_ADD(ctx.sub[kPhX2], tx);
-    tx = OS_PH_NOW();
-#endif
-    s.atari = atari;
-    sd.me = opp;  // the next player's stones
-    sd.them = own;
-    s.ko = static_cast<int16_t>((enemy_eye && captured == 1) ? cap_pt : -1);
-#if OS_PHASE_TIMING
-    OS_PH_ADD(ctx.sub[kPhX3], tx);
-#endif
-    if (!ctx.insert(s.hash, captured > 0, popc(own) + popc(opp))) s.flags |= Go::kSuperko;
-  }
-  s.to_play = static_cast<uint8_t>(1 - c);
-  s.moves++;
-}
-
-__device__ __forceinline__ void go_apply_lanes_serial(Go::State& s, GoSides& sd, const GameCfg& g,
+__device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const GameCfg& g,
                                                GoWaveCtx& ctx, GoLabels& lab,
                                                const GoNbrLanes& nbl, int a) {
   using M = CfgMasks<B128>;
@@ -2464,19 +2386,6 @@ __device__ __forceinline__ void go_apply_lanes_serial(Go::State& s, GoSides& sd,
   s.moves++;
 }
 
-#ifndef OS_GO_PAR
-#define OS_GO_PAR 1  // A/B knob: 0 = the serial form for both policies
-#endif
-template <int Policy>
-__device__ __forceinline__ void go_apply_lanes(Go::State& s, GoSides& sd, const GameCfg& g,
-                                               GoWaveCtx& ctx, GoLabels& lab,
-                                               const GoNbrLanes& nbl, int a) {
-  if constexpr (Policy == kPolicyCpp && OS_GO_PAR)
-    go_apply_lanes_par(s, sd, g, ctx, lab, nbl, a);
-  else
-    go_apply_lanes_serial(s, sd, g, ctx, lab, nbl, a);
-}
-
 template <int Policy, class Rng>
 __device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rng& ev) {
   s = make_uniform(s);
@@ -2505,7 +2414,7 @@ __device__ int go_rollout_wave(Go::State s, const GameCfg& g, GoWaveCtx& ctx, Rn
     const uint64_t t1 = OS_PH_NOW();
     OS_PH_ADD(ctx.sub[kPhGoLegal], t0);
 #endif
-    go_apply_lanes<Policy>(s, sd, g, ctx, lab, nbl, act);
+    go_apply_lanes(s, sd, g, ctx, lab, nbl, act);
 #if OS_PHASE_TIMING
     OS_PH_ADD(ctx.sub[kPhGoApply], t1);
 #endif
