@@ -1899,7 +1899,10 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
       dec = !chn;
     } else {
       // Word roles: a 4-state automaton (decision, -, chance word 1, chance
-      // word 2) scanned over the lanes' transition maps.
+      // word 2) scanned over the lanes' transition maps.  (Walking the
+      // window's stop bits on the scalar unit instead, a few scalar steps per
+      // node, was slower: 16.1 -> 19.3 ms per 1000-simulation step,
+      // profiles/r06/pig_nodes.)
       const bool own_roll = (w0 & 1u) == 0;
       const uint32_t f = (own_roll ? 2u : 0u) | (1u << 2) | (3u << 4) | (0u << 6);
       const uint32_t F = wave_scan_map4(f);  // role of word l + 1 = F(role0)
