@@ -74,3 +74,32 @@ def test_gpu_engine_reports_resolved_layout(require_gpu):
     seeds = np.arange(R, dtype=np.uint32)
     eng.prepare(acts, offs, seeds, seeds + np.uint32(1), max_simulations=4, layout=asked)
     assert eng.layout() == want, (game, R, asked)
+
+
+@pytest.mark.gpu
+def test_gpu_engine_reports_searches_per_wave(require_gpu):
+  """os_engine_get_searches_per_wave: 1 on the wave layout; the go lane
+  search's block width (16 lanes up to 32768 roots, 32 above, or the
+  block_size asked for), and the results do not depend on it."""
+  import numpy as np
+  from os_amd import _lib
+  from os_amd import engine as E
+  eng = E.Engine("connect_four")
+  with pytest.raises(RuntimeError):
+    eng.searches_per_wave()  # nothing launched yet
+  acts, offs = E.make_roots("connect_four", 8, 1000, 4)
+  seeds = np.arange(8, dtype=np.uint32)
+  eng.mcts_batch(acts, offs, seeds, seeds + np.uint32(1), max_simulations=8)
+  assert eng.searches_per_wave() == 1
+  go = E.Engine("go(board_size=5)")
+  R = 96
+  acts, offs = E.make_roots("go(board_size=5)", R, 1000, 4)
+  seeds = np.arange(R, dtype=np.uint32)
+  outs = {}
+  for block, want in ((0, 16), (32, 32), (64, 64)):
+    outs[want] = go.mcts_batch(acts, offs, seeds, seeds + np.uint32(1), max_simulations=16,
+                               layout=_lib.LAYOUT_LANE, block_size=block)
+    assert go.searches_per_wave() == want
+  for k in E.OUTPUT_KEYS:
+    np.testing.assert_array_equal(outs[16][k], outs[32][k], err_msg=k)
+    np.testing.assert_array_equal(outs[16][k], outs[64][k], err_msg=k)
