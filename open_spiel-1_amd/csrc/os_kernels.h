@@ -582,6 +582,29 @@ template <class R>
 __host__ __device__ constexpr size_t ChanceTreeLdsOffset(size_t lds) {
   return (lds + 15) & ~size_t(15);
 }
+// The root record of search i: the host writes G::State records, except for
+// Pig2, whose roots are the 10-player Pig records narrowed to two players.
+template <class G>
+struct ChanceRoot {
+  __device__ static typename G::State load(const void* roots, int64_t i) {
+    return static_cast<const typename G::State*>(roots)[i];
+  }
+};
+template <>
+struct ChanceRoot<Pig2> {
+  __device__ static Pig2::State load(const void* roots, int64_t i) {
+    const Pig::State& r = static_cast<const Pig::State*>(roots)[i];
+    Pig2::State s;
+    s.score[0] = r.score[0];
+    s.score[1] = r.score[1];
+    s.turn_total = r.turn_total;
+    s.cur = r.cur;
+    s.turn_player = r.turn_player;
+    s.moves = r.moves;
+    return s;
+  }
+};
+
 template <class G, class R, int Policy, bool kLdsTree = false>
 __global__ __launch_bounds__(64) void k_wsearch_chance(DevArgs a) {
   const int64_t lr = blockIdx.x;
@@ -613,7 +636,7 @@ __global__ __launch_bounds__(64) void k_wsearch_chance(DevArgs a) {
     bot.init_seeded();
     ev.init_seeded();
   }
-  const typename G::State root = make_uniform(static_cast<const typename G::State*>(a.roots)[gr]);
+  const typename G::State root = make_uniform(ChanceRoot<G>::load(a.roots, gr));
   typename G::Ctx ctx;
   Node<R>* nodes = static_cast<Node<R>*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   Node<R>* arena = nodes;
@@ -2031,40 +2054,48 @@ int LaunchSearchOnly(os_engine* e, const DevArgs& a, hipStream_t stream) {
 }
 
 template <class G, class R, int Policy>
+int LaunchChanceWave(os_engine* e, DevArgs a, hipStream_t stream) {
+  if (a.pages) return Fail(OS_ERR_UNSUPPORTED, "paged arena on the chance-node wave layout");
+  const size_t lds = WaveChanceLdsBytes<G, R>(a.path_cap);
+  if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
+  // A small batch whose reserved arenas fit the CU's LDS: the tree in LDS.
+  const size_t tree_lds = ChanceTreeLdsOffset<R>(lds) +
+                          static_cast<size_t>(a.cap) * sizeof(Node<R>) +
+                          static_cast<size_t>(a.sp.max_simulations + 1) * sizeof(double);
+  const bool lds_tree = a.pages == nullptr && e->num_roots <= kLdsTreeMaxRoots &&
+                        e->chunk_roots >= e->num_roots && tree_lds <= kLdsBytes &&
+                        OS_CHANCE_LDS_TREE;
+  const void* fn = lds_tree
+      ? reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy, true>)
+      : reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy, false>);
+  const size_t dyn = lds_tree ? tree_lds : lds;
+  HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(dyn)));
+  for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
+    const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
+    a.root_base = base;
+    a.num_roots = n;
+    if (lds_tree)
+      hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy, true>), dim3(static_cast<unsigned>(n)),
+                         dim3(64), dyn, stream, a);
+    else
+      hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy, false>),
+                         dim3(static_cast<unsigned>(n)), dim3(64), dyn, stream, a);
+    HIP_TRY(hipGetLastError());
+  }
+  return OS_OK;
+}
+
+template <class G, class R, int Policy>
 int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
   e->search_lanes = 1;  // the wave layouts; the lane launchers below set theirs
   if constexpr (HasChance<G>::value) {
     if (a.path_cap > kChancePathCap) a.path_cap = kChancePathCap;
     if (e->params.layout == OS_LAYOUT_WAVE) {
-      if (a.pages) return Fail(OS_ERR_UNSUPPORTED, "paged arena on the chance-node wave layout");
-      const size_t lds = WaveChanceLdsBytes<G, R>(a.path_cap);
-      if (lds > kLdsBytes) return Fail(OS_ERR_CAPACITY, "wave LDS slice exceeds the CU's LDS");
-      // A small batch whose reserved arenas fit the CU's LDS: the tree in LDS.
-      const size_t tree_lds = ChanceTreeLdsOffset<R>(lds) +
-                              static_cast<size_t>(a.cap) * sizeof(Node<R>) +
-                              static_cast<size_t>(a.sp.max_simulations + 1) * sizeof(double);
-      const bool lds_tree = a.pages == nullptr && e->num_roots <= kLdsTreeMaxRoots &&
-                            e->chunk_roots >= e->num_roots && tree_lds <= kLdsBytes &&
-                            OS_CHANCE_LDS_TREE;
-      const void* fn = lds_tree
-          ? reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy, true>)
-          : reinterpret_cast<const void*>(&k_wsearch_chance<G, R, Policy, false>);
-      const size_t dyn = lds_tree ? tree_lds : lds;
-      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(dyn)));
-      for (int64_t base = 0; base < e->num_roots; base += e->chunk_roots) {
-        const int64_t n = std::min<int64_t>(e->chunk_roots, e->num_roots - base);
-        a.root_base = base;
-        a.num_roots = n;
-        if (lds_tree)
-          hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy, true>), dim3(static_cast<unsigned>(n)),
-                             dim3(64), dyn, stream, a);
-        else
-          hipLaunchKernelGGL((k_wsearch_chance<G, R, Policy, false>),
-                             dim3(static_cast<unsigned>(n)), dim3(64), dyn, stream, a);
-        HIP_TRY(hipGetLastError());
-      }
-      return OS_OK;
+      // two-player pig: the same search over two-player state arrays (Pig2)
+      if constexpr (std::is_same<G, Pig>::value)
+        if (a.cfg.pig_players == 2) return LaunchChanceWave<Pig2, R, Policy>(e, a, stream);
+      return LaunchChanceWave<G, R, Policy>(e, a, stream);
     }
   } else {
     if (e->params.layout == OS_LAYOUT_WAVE) return LaunchWaveSearch<G, R, Policy>(e, a, stream);

@@ -1648,18 +1648,18 @@ __device__ inline int hex_fill_end(const Hex::State& s, const GameCfg& g, B128 e
 //     changed since the last test).
 // Words drawn per move are those of the serial playout: decisions 2 (absl,
 // either action count) or 1 / 0 (numpy, two / one action), chance nodes 2.
-template <int Policy>
-__device__ int pig_rollout_wave(Pig::State s, const GameCfg& g, WaveMt& ev) {
+template <int Policy, class PG = Pig>
+__device__ int pig_rollout_wave(typename PG::State s, const GameCfg& g, WaveMt& ev) {
   s = make_uniform(s);
   ev.uniformize();
   NoCtx nctx;
-  if (Pig::terminal(s, g)) return Pig::ret0(s, g, nctx);
+  if (PG::terminal(s, g)) return PG::ret0(s, g, nctx);
   const int l = lane_id();
   uint32_t sc = 0;  // lane p: score of player p
 #pragma unroll
-  for (int i = 0; i < Pig::kMaxPlayers; ++i) sc = l == i ? static_cast<uint32_t>(s.score[i]) : sc;
+  for (int i = 0; i < PG::kMaxPlayers; ++i) sc = l == i ? static_cast<uint32_t>(s.score[i]) : sc;
   const int win = g.pig_win, hz = g.pig_horizon, np = g.pig_players, dice = g.pig_dice;
-  const double p = 1.0 / dice;  // Pig::chance_prob
+  const double p = 1.0 / dice;  // PG::chance_prob
   int tp = s.turn_player, tt = s.turn_total, moves = s.moves;
   bool at_chance = s.cur < 0;
   int cs = static_cast<int>(rl32(sc, tp));
@@ -1712,7 +1712,7 @@ __device__ int pig_rollout_wave(Pig::State s, const GameCfg& g, WaveMt& ev) {
   for (;;) {
     if (moves >= hz) break;  // terminal (a winner ends the loop where it is made)
     if (!at_chance) {
-      const bool only_stop = cs + tt >= win;  // Pig::legal: stop alone
+      const bool only_stop = cs + tt >= win;  // PG::legal: stop alone
       const int nw = Policy == kPolicyCpp ? 2 : (only_stop ? 0 : 1);
       need(nw + 2);  // the decision's words and the chance pair a roll draws next
       const uint32_t pd = rl32(pk, c), pc = rl32(pk, c + nw);
@@ -1759,14 +1759,14 @@ __device__ int pig_rollout_wave(Pig::State s, const GameCfg& g, WaveMt& ev) {
     }
   }
 #pragma unroll
-  for (int i = 0; i < Pig::kMaxPlayers; ++i) s.score[i] = static_cast<int32_t>(rl32(sc, i));
+  for (int i = 0; i < PG::kMaxPlayers; ++i) s.score[i] = static_cast<int32_t>(rl32(sc, i));
   s.turn_total = tt;
   s.turn_player = tp;
   s.cur = at_chance ? -1 : tp;
   s.moves = moves;
   ev.seek(wb + c);
   ev.words.add(used);
-  return Pig::ret0(s, g, nctx);
+  return PG::ret0(s, g, nctx);
 }
 
 // Inclusive sum over the 64 lanes (the DPP row scan, then the row_bcast15 /
@@ -1828,21 +1828,21 @@ __device__ __forceinline__ uint32_t wave_scan_map4(uint32_t f) {
 #ifndef OS_PIG_PAR2
 #define OS_PIG_PAR2 1  // A/B knob: 0 = two players walk the turns like n players
 #endif
-template <int Policy>
-__device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
+template <int Policy, class PG = Pig>
+__device__ int pig_rollout_turns(typename PG::State s, const GameCfg& g, WaveMt& ev) {
   s = make_uniform(s);
   ev.uniformize();
   NoCtx nctx;
-  if (Pig::terminal(s, g)) return Pig::ret0(s, g, nctx);
+  if (PG::terminal(s, g)) return PG::ret0(s, g, nctx);
   constexpr bool kCpp = Policy == kPolicyCpp;
   constexpr uint32_t kDec = 0, kChance = 2;  // node-start roles (1: C++ decision word 2; 3: chance word 2)
   const int l = lane_id();
   const uint64_t below = (1ull << l) - 1ull;
   uint32_t sc = 0;  // lane p: score of player p
 #pragma unroll
-  for (int i = 0; i < Pig::kMaxPlayers; ++i) sc = l == i ? static_cast<uint32_t>(s.score[i]) : sc;
+  for (int i = 0; i < PG::kMaxPlayers; ++i) sc = l == i ? static_cast<uint32_t>(s.score[i]) : sc;
   const int win = g.pig_win, hz = g.pig_horizon, np = g.pig_players, dice = g.pig_dice;
-  const double p = 1.0 / dice;  // Pig::chance_prob
+  const double p = 1.0 / dice;  // PG::chance_prob
   int tp = s.turn_player, tt = s.turn_total, moves = s.moves;
   uint32_t role0 = s.cur < 0 ? kChance : kDec;  // numpy: role of the window's word 0
   bool chance0 = s.cur < 0;                      // C++: the window's node 0 is a chance node
@@ -2031,14 +2031,14 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
     }
   }
 #pragma unroll
-  for (int i = 0; i < Pig::kMaxPlayers; ++i) s.score[i] = static_cast<int32_t>(rl32(sc, i));
+  for (int i = 0; i < PG::kMaxPlayers; ++i) s.score[i] = static_cast<int32_t>(rl32(sc, i));
   s.turn_total = tt;
   s.turn_player = tp;
   s.cur = chance_end ? -1 : tp;
   s.moves = moves;
   ev.seek(wb);
   ev.words.add(used);
-  return Pig::ret0(s, g, nctx);
+  return PG::ret0(s, g, nctx);
 }
 
 // OS_PIG_TURNS: 1 = pig playouts by turns (pig_rollout_turns), 0 = node by
@@ -2051,16 +2051,17 @@ __device__ int pig_rollout_turns(Pig::State s, const GameCfg& g, WaveMt& ev) {
 #ifndef OS_AB_PIG_NOROLL
 #define OS_AB_PIG_NOROLL 0
 #endif
-template <int Policy>
-struct ChanceRollout<Pig, Policy, WaveMt> {
-  __device__ static int run(const Pig::State& s, const GameCfg& g, NoCtx&, WaveMt& ev) {
+template <int Policy, int kMaxP>
+struct ChanceRollout<PigT<kMaxP>, Policy, WaveMt> {
+  __device__ static int run(const typename PigT<kMaxP>::State& s, const GameCfg& g, NoCtx&,
+                            WaveMt& ev) {
 #if OS_AB_PIG_NOROLL
     return 0;
 #endif
 #if OS_PIG_TURNS
-    return pig_rollout_turns<Policy>(s, g, ev);
+    return pig_rollout_turns<Policy, PigT<kMaxP>>(s, g, ev);
 #else
-    return pig_rollout_wave<Policy>(s, g, ev);
+    return pig_rollout_wave<Policy, PigT<kMaxP>>(s, g, ev);
 #endif
   }
 };
