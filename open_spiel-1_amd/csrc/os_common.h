@@ -127,6 +127,111 @@ OS_HD B128 lowmask128(int n) {
   return b128(~0ull, ~0ull);
 }
 
+// 96-bit bitboard (three u32 words) for boards of at most 96 cells (go up to
+// 9 x 9 on the lane kernels, os_kernels.h Go9).  Bit i = cell i, as B128.  A
+// B128 word operation is two 32-bit VALU operations and a B128 shift five
+// (two 64-bit shifts, the carried-in half, two ORs); here they are three
+// (a shift and two funnel shifts, v_alignbit_b32), and a board is three VGPRs.
+struct B96 {
+  uint32_t w0, w1, w2;
+};
+OS_HD B96 b96(uint32_t w0, uint32_t w1, uint32_t w2) {
+  B96 r;
+  r.w0 = w0; r.w1 = w1; r.w2 = w2;
+  return r;
+}
+OS_HD B96 b96_of(const B128& x) {  // the low 96 cells
+  return b96(static_cast<uint32_t>(x.lo), static_cast<uint32_t>(x.lo >> 32),
+             static_cast<uint32_t>(x.hi));
+}
+OS_HD B128 b128_of(const B96& x) {
+  return b128(static_cast<uint64_t>(x.w0) | (static_cast<uint64_t>(x.w1) << 32), x.w2);
+}
+OS_HD B96 sel96(bool c, B96 x, B96 y) {  // word by word (see sel128)
+  const uint32_t w0 = c ? x.w0 : y.w0;
+  const uint32_t w1 = c ? x.w1 : y.w1;
+  const uint32_t w2 = c ? x.w2 : y.w2;
+  return b96(w0, w1, w2);
+}
+OS_HD B96 pick(const B96* a, int i) { return sel96(i != 0, a[1], a[0]); }
+OS_HD void put(B96* a, int i, B96 v) {
+  const B96 v0 = sel96(i != 0, a[0], v), v1 = sel96(i != 0, v, a[1]);
+  a[0] = v0;
+  a[1] = v1;
+}
+OS_HD B96 operator|(B96 a, B96 b) { return b96(a.w0 | b.w0, a.w1 | b.w1, a.w2 | b.w2); }
+OS_HD B96 operator&(B96 a, B96 b) { return b96(a.w0 & b.w0, a.w1 & b.w1, a.w2 & b.w2); }
+OS_HD B96 operator^(B96 a, B96 b) { return b96(a.w0 ^ b.w0, a.w1 ^ b.w1, a.w2 ^ b.w2); }
+OS_HD B96 operator~(B96 a) { return b96(~a.w0, ~a.w1, ~a.w2); }
+OS_HD bool operator==(B96 a, B96 b) {
+  return ((a.w0 ^ b.w0) | (a.w1 ^ b.w1) | (a.w2 ^ b.w2)) == 0u;
+}
+OS_HD bool operator!=(B96 a, B96 b) { return !(a == b); }
+OS_HD bool any(B96 a) { return (a.w0 | a.w1 | a.w2) != 0u; }
+OS_HD int popc32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popc(x);
+#else
+  return __builtin_popcount(x);
+#endif
+}
+OS_HD int ctz32(uint32_t x) {  // x != 0
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ffs(static_cast<int>(x)) - 1;
+#else
+  return __builtin_ctz(x);
+#endif
+}
+OS_HD int popc(B96 a) { return popc32(a.w0) + popc32(a.w1) + popc32(a.w2); }
+// Funnel shifts: the compiler maps (hi << s) | (lo >> (32 - s)) to one
+// v_alignbit_b32.
+OS_HD B96 shl(B96 a, int s) {  // 0 < s < 32
+  return b96(a.w0 << s, (a.w1 << s) | (a.w0 >> (32 - s)), (a.w2 << s) | (a.w1 >> (32 - s)));
+}
+OS_HD B96 shr(B96 a, int s) {  // 0 < s < 32
+  return b96((a.w0 >> s) | (a.w1 << (32 - s)), (a.w1 >> s) | (a.w2 << (32 - s)), a.w2 >> s);
+}
+OS_HD B96 bit96(int i) {  // 0 <= i < 96
+  const uint32_t m = 1u << (i & 31);
+  const int q = i >> 5;
+  return b96(q == 0 ? m : 0u, q == 1 ? m : 0u, q == 2 ? m : 0u);
+}
+OS_HD bool test(B96 a, int i) {
+  const int q = i >> 5;
+  const uint32_t w = q == 0 ? a.w0 : (q == 1 ? a.w1 : a.w2);
+  return (w >> (i & 31)) & 1u;
+}
+OS_HD int lowest(B96 a) {  // a != 0
+  return a.w0 ? ctz32(a.w0) : (a.w1 ? 32 + ctz32(a.w1) : 64 + ctz32(a.w2));
+}
+// Index of the k-th (0-based) set bit of x, ascending; k < popc(x).
+OS_HD int select32(uint32_t x, int k) {
+  int base = 0;
+  int c = popc32(x & 0xFFFFu);
+  if (k >= c) { k -= c; x >>= 16; base += 16; }
+  c = popc32(x & 0xFFu);
+  if (k >= c) { k -= c; x >>= 8; base += 8; }
+  c = popc32(x & 0xFu);
+  if (k >= c) { k -= c; x >>= 4; base += 4; }
+  c = popc32(x & 0x3u);
+  if (k >= c) { k -= c; x >>= 2; base += 2; }
+  c = static_cast<int>(x & 1u);
+  if (k >= c) { base += 1; }
+  return base;
+}
+OS_HD int select96(B96 a, int k) {  // k < popc(a)
+  const int c0 = popc32(a.w0);
+  if (k < c0) return select32(a.w0, k);
+  k -= c0;
+  const int c1 = popc32(a.w1);
+  return k < c1 ? 32 + select32(a.w1, k) : 64 + select32(a.w2, k - c1);
+}
+OS_HD B96 lowmask96(int n) {  // 0 <= n <= 96
+  return b96(n >= 32 ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u),
+             n >= 64 ? ~0u : (n <= 32 ? 0u : (1u << (n - 32)) - 1u),
+             n >= 96 ? ~0u : (n <= 64 ? 0u : (1u << (n - 64)) - 1u));
+}
+
 // 384-bit bitboard (six u64 words) for boards above 11 x 11 (hex, go up to
 // 19 x 19).  Same operations as B128; every loop is unrolled, so the words
 // are only ever indexed by constants.
@@ -212,6 +317,15 @@ struct BB<B128> {
   OS_HD static B128 lowmask(int n) { return lowmask128(n); }
   OS_HD static int select(B128 a, int k) { return select128(a, k); }
   OS_HD static B128 sel(bool c, B128 x, B128 y) { return sel128(c, x, y); }
+};
+template <>
+struct BB<B96> {
+  static constexpr int kBits = 96;
+  OS_HD static B96 zero() { return b96(0u, 0u, 0u); }
+  OS_HD static B96 bit(int i) { return bit96(i); }
+  OS_HD static B96 lowmask(int n) { return lowmask96(n); }
+  OS_HD static int select(B96 a, int k) { return select96(a, k); }
+  OS_HD static B96 sel(bool c, B96 x, B96 y) { return sel96(c, x, y); }
 };
 template <>
 struct BB<B384> {

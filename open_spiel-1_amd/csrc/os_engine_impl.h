@@ -445,6 +445,17 @@ extern GameLaunchers kPigLaunchers;
 inline bool GoBigBoard(const GameCfg& c) { return c.kind == kGo && c.rows > 11; }
 inline bool BigBoard(const GameCfg& c) { return (c.kind == kGo || c.kind == kHex) && c.rows > 11; }
 
+// go up to 9 x 9 on the lane kernels runs GoT<B96> (os_games.h Go9;
+// os_game_go9.hip); OS_GO9=0 builds keep GoT<B128> there (A/B knob).
+#ifndef OS_GO9
+#define OS_GO9 1
+#endif
+inline bool UseGo9(const GameCfg& c) {
+  return OS_GO9 && c.kind == kGo && c.rows <= kGo9MaxSide;
+}
+int LaunchGo9Search(os_engine* e, const DevArgs& a, hipStream_t stream);  // k_lsearch<Go9>
+int LaunchGo9Rollouts(os_engine* e, hipStream_t stream);                  // k_rollouts<Go9>
+
 inline const GameLaunchers* LaunchersFor(int32_t kind) {
   switch (kind) {
     case kTicTacToe: return &kTicTacToeLaunchers;

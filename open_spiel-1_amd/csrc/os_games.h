@@ -74,6 +74,12 @@ struct CfgMasks<B128> {
   OS_HD static const B128& hex_b(const GameCfg& g) { return g.hex_b; }
 };
 template <>
+struct CfgMasks<B96> {  // the low 96 cells of the B128 masks (go up to 9 x 9)
+  OS_HD static B96 board(const GameCfg& g) { return b96_of(g.board); }
+  OS_HD static B96 notcol0(const GameCfg& g) { return b96_of(g.notcol0); }
+  OS_HD static B96 notcollast(const GameCfg& g) { return b96_of(g.notcollast); }
+};
+template <>
 struct CfgMasks<B384> {
   OS_HD static const B384& board(const GameCfg& g) { return g.big_board; }
   OS_HD static const B384& notcol0(const GameCfg& g) { return g.big_notcol0; }
@@ -1176,6 +1182,25 @@ struct GoT {
 };
 using Go = GoT<B128>;
 using GoBig = GoT<B384>;  // board_size 12..19 (host State API)
+// board_size <= 9 on the lane kernels (k_lsearch, k_rollouts): the same game
+// over three-word bitboards, so every board operation issues 3 VALU words
+// instead of 4 and a shift 3 instead of 5.  Roots arrive as Go::State records
+// (os_kernels.h GoRoot narrows them); bit i is cell i in both.
+using Go9 = GoT<B96>;
+constexpr int kGo9MaxSide = 9;
+OS_HD Go9::State go9_state(const Go::State& r) {
+  Go9::State s;
+  s.bw[0] = b96_of(r.bw[0]);
+  s.bw[1] = b96_of(r.bw[1]);
+  s.atari = b96_of(r.atari);
+  s.hash = r.hash;
+  s.ko = r.ko;
+  s.moves = r.moves;
+  s.to_play = r.to_play;
+  s.flags = r.flags;
+  s.pad = r.pad;
+  return s;
+}
 
 // ----------------------------------------------------------------------------
 // pig (pig.cc:81-244), 2..10 players.  A decision node offers roll (0) and

@@ -178,6 +178,13 @@ struct LsCaps<Go> {  // act, heads and bloom per lane
                        bloom = GoCtx::kBloomWords;
 };
 template <>
+struct LsCaps<Go9> {  // 9 x 9: 82 actions, stone counts 0 .. 81
+  static constexpr int act = kGo9MaxSide * kGo9MaxSide + 1,
+                       zob = 2 * kGo9MaxSide * kGo9MaxSide,
+                       heads = kGo9MaxSide * kGo9MaxSide + 1, log = kGoLogCap,
+                       bloom = GoCtx::kBloomWords;
+};
+template <>
 struct LsCaps<GoBig> {  // actions up to 361: u16 expansion buffers in HBM
   static constexpr int act = 1, zob = 2 * 361, heads = 1, log = kGoLogCapBig, bloom = 1;
 };
@@ -245,6 +252,28 @@ struct LCtx<Go> {
     return c;
   }
 };
+
+template <>
+struct LCtx<Go9> : LCtx<Go> {};
+
+// Root records of the lane kernels: the host's G::State, except for Go9,
+// whose roots are Go::State records narrowed to three-word bitboards.
+template <class G>
+struct LaneRoot {
+  __device__ static typename G::State load(const void* roots, int64_t i) {
+    return static_cast<const typename G::State*>(roots)[i];
+  }
+};
+template <>
+struct LaneRoot<Go9> {
+  __device__ static Go9::State load(const void* roots, int64_t i) {
+    return go9_state(static_cast<const Go::State*>(roots)[i]);
+  }
+};
+// go on the lane kernels, either bitboard width.
+template <class G>
+struct IsLaneGo : std::integral_constant<bool, std::is_same<G, Go>::value ||
+                                                   std::is_same<G, Go9>::value> {};
 
 // k_lsearch's go superko log written 8 entries at a time (GoCtxT::wlog; 1)
 // or entry by entry (0).  A/B knob.
@@ -326,7 +355,7 @@ __global__ __launch_bounds__(64, kOcc) void k_lsearch(DevArgs a) {
   if constexpr (G::State::kNeedsLog) ctx.zob = zob;
 #if OS_LS_LOGWC
   // go: the superko log's open 8-entry group in LDS (GoCtxT::wlog)
-  constexpr bool kLogWc = std::is_same<G, Go>::value;
+  constexpr bool kLogWc = IsLaneGo<G>::value;
   __shared__ uint64_t ls_wlog[kLogWc ? GoCtx::kWg * kL : 1];
   __shared__ uint32_t ls_wlink[kLogWc ? GoCtx::kWg * kL : 1];
   if constexpr (kLogWc) {
@@ -338,7 +367,7 @@ __global__ __launch_bounds__(64, kOcc) void k_lsearch(DevArgs a) {
 #if OS_LS_AB & 2
   if constexpr (G::State::kNeedsLog) ctx.cap = 0;
 #endif
-  const typename G::State root = static_cast<const typename G::State*>(a.roots)[gr];
+  const typename G::State root = LaneRoot<G>::load(a.roots, gr);
   using N = Node<R, LsWide<G>::value>;
   N* nodes = static_cast<N*>(a.arena) + lr * static_cast<int64_t>(a.cap);
   SearchResult res;
@@ -1808,6 +1837,9 @@ struct RollCtx<Go> {
 };
 #endif
 
+template <>
+struct RollCtx<Go9> : RollCtx<Go> {};
+
 template <class G>
 struct WaveRollCtx {
   __device__ static NoCtx make(const RollArgs&) { return NoCtx(); }
@@ -1887,7 +1919,7 @@ __global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
   ev.seed(a.seeds[i]);
   extern __shared__ uint32_t roll_lds[];  // RollLdsBytes<G>(cfg) bytes
   typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
-  const typename G::State root = *static_cast<const typename G::State*>(a.root);
+  const typename G::State root = LaneRoot<G>::load(a.root, 0);
   double s0 = 0.0, s1 = 0.0;
   uint32_t moves = 0;
   for (int k = 0; k < a.n_rollouts; ++k) {
@@ -2006,7 +2038,7 @@ int LaunchWaveSearch(os_engine* e, DevArgs a, hipStream_t stream) {
 // overrides the choice.
 template <class G>
 int LsLanes(int64_t n, int block_size) {
-  if (!std::is_same<G, Go>::value) return 64;
+  if (!IsLaneGo<G>::value) return 64;
   if (block_size == 16 || block_size == 32 || block_size == 64) return block_size;
   return n <= 32768 ? 16 : 32;
 }
@@ -2025,7 +2057,7 @@ int LaunchLs(os_engine* e, DevArgs a, hipStream_t stream) {
     const int kl = LsLanes<G>(n, e->params.block_size);
     e->search_lanes = kl;
     const unsigned grid = static_cast<unsigned>((n + kl - 1) / kl);
-    if constexpr (std::is_same<G, Go>::value) {
+    if constexpr (IsLaneGo<G>::value) {
       if (kl == 16)
         hipLaunchKernelGGL((k_lsearch<G, R, 16, 2>), dim3(grid), dim3(16), 0, stream, a);
       else if (kl == 32)
@@ -2104,6 +2136,8 @@ int LaunchSearch(os_engine* e, DevArgs a, hipStream_t stream) {
     // go: k_lsearch, per-search buffers in HBM (the LDS-slice kernel k_mcts
     // would hold the superko log in private memory).
     if (Policy != kPolicyCpp) return Fail(OS_ERR_UNSUPPORTED, "k_lsearch runs the C++ policy");
+    if constexpr (std::is_same<G, Go>::value)
+      if (UseGo9(a.cfg)) return LaunchGo9Search(e, a, stream);  // os_game_go9.hip
     return LaunchLs<G, R>(e, a, stream);
   } else {
   int bs = e->params.block_size > 0 ? e->params.block_size : kDefaultBlock;
@@ -2329,7 +2363,7 @@ size_t RollLdsBytes(const GameCfg& c) {
   (void)c;
   return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #else
-  if constexpr (std::is_same<G, Go>::value)
+  if constexpr (IsLaneGo<G>::value)
     return 4 * (((c.rows * c.cols + 1) * 64 + 3) / 4 +
                 (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * 64 : 0));
   else
@@ -2357,7 +2391,7 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
   const int64_t n = e->roll_n;
   if (e->game.cfg.pig_players > 2)
     return Fail(OS_ERR_UNSUPPORTED, "rollout batches return two players' values");
-  if constexpr (!HasChance<G>::value) {
+  if constexpr (!HasChance<G>::value && !std::is_same<G, Go9>::value) {
     if (e->rollout_layout == OS_LAYOUT_WAVE) {
       hipLaunchKernelGGL(k_wrollouts<G>, dim3(static_cast<unsigned>(n)), dim3(64), 0, stream,
                          a);
@@ -2365,6 +2399,8 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
       return OS_OK;
     }
   }
+  if constexpr (std::is_same<G, Go>::value)
+    if (UseGo9(a.cfg)) return LaunchGo9Rollouts(e, stream);  // os_game_go9.hip
   {
     // 64 lanes per block: 32-lane blocks (four waves per SIMD at C5's
     // per-rank 131072 playouts instead of two) were slower, 2.36 -> 3.16 ms

@@ -677,6 +677,53 @@ int hc_rollouts_go_link16(const char* game_string, const int64_t* actions, int64
   return 0;
 }
 
+// k_rollouts<Go9>: the link16 context over three-word bitboards (os_games.h
+// Go9, board_size <= 9), the root narrowed as the kernels narrow it.
+int hc_rollouts_go9(const char* game_string, const int64_t* actions, int64_t n_actions,
+                    int64_t n, const uint32_t* seeds, double* out) {
+  HostGame game;
+  bool unsup = false;
+  std::string err = LoadHostGame(game_string, &game, &unsup);
+  if (!err.empty() || game.cfg.kind != kGo || game.cfg.rows > kGo9MaxSide) {
+    g_err = err.empty() ? "go up to 9 x 9 only" : err;
+    return -1;
+  }
+  HostState hs;
+  hs.game = &game;
+  StateInit(&hs);
+  for (int64_t i = 0; i < n_actions; ++i) StateApply(&hs, actions[i]);
+  const Go9::State root = go9_state(*reinterpret_cast<const Go::State*>(hs.raw));
+  using Ctx16 = GoCtxT<uint8_t, uint16_t>;
+  const int cap = 248, cells = game.cfg.rows * game.cfg.cols;
+  std::vector<uint32_t> mt(kMtN);
+  std::vector<uint64_t> log(cap);
+  std::vector<uint16_t> link(cap);
+  std::vector<uint8_t> head(cells + 1);
+  std::vector<uint32_t> bloom(Ctx16::kBloomWords * 64);
+  for (int64_t i = 0; i < n; ++i) {
+    MtStream ev{mt.data(), kMtN, 0};
+    mt_seed(ev.s, seeds[i]);
+    Ctx16 c;
+    std::memset(static_cast<void*>(&c), 0, sizeof c);
+    c.zob = game.zob.data();
+    c.base = hs.hashes.data();
+    c.n_base = static_cast<int32_t>(hs.hashes.size());
+    c.log = log.data();
+    c.link = link.data();
+    c.head = head.data();
+    c.stride = 1;
+    c.head_stride = 1;
+    c.cap = cap;
+    c.n_heads = cells + 1;
+    c.bloom = bloom.data();
+    c.init_filters();
+    const int r0 = rollout_ret0<Go9, kPolicyCpp>(root, game.cfg, c, ev);
+    out[2 * i] = r0;
+    out[2 * i + 1] = -r0;
+  }
+  return 0;
+}
+
 int hc_rollouts_go_bloom(const char* game_string, const int64_t* actions, int64_t n_actions,
                          int64_t n, const uint32_t* seeds, double* out) {
   HostGame game;

@@ -28,6 +28,7 @@ def lib():
     L.hc_rollouts_go_bloom.argtypes = L.hc_rollouts.argtypes
     L.hc_rollouts_go_logbloom.argtypes = L.hc_rollouts.argtypes
     L.hc_rollouts_go_link16.argtypes = L.hc_rollouts.argtypes
+    L.hc_rollouts_go9.argtypes = L.hc_rollouts.argtypes
     L.hc_go_score.restype = ctypes.c_float
     L.hc_go_score.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64]
     L.hc_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
@@ -262,6 +263,18 @@ def rollouts_go_link16(game_string, history, seeds):
   out = np.zeros((len(s), 2), np.float64)
   rc = lib().hc_rollouts_go_link16(game_string.encode(), a.ctypes.data, len(a), len(s),
                                    s.ctypes.data, out.ctypes.data)
+  if rc:
+    raise RuntimeError(lib().hc_last_error().decode())
+  return out
+
+
+def rollouts_go9(game_string, history, seeds):
+  """go playouts as k_rollouts<Go9> plays them (three-word bitboards, <= 9 x 9)."""
+  a = np.ascontiguousarray(history, np.int64)
+  s = np.ascontiguousarray(seeds, np.uint32)
+  out = np.zeros((len(s), 2), np.float64)
+  rc = lib().hc_rollouts_go9(game_string.encode(), a.ctypes.data, len(a), len(s),
+                             s.ctypes.data, out.ctypes.data)
   if rc:
     raise RuntimeError(lib().hc_last_error().decode())
   return out

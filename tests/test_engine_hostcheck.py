@@ -158,6 +158,8 @@ def test_go_playouts_match_oracle_many_seeds(gs):
     assert np.array_equal(H.rollouts_go_bloom(gs, acts, seeds), ref)
     assert np.array_equal(H.rollouts_go_logbloom(gs, acts, seeds), ref)
     assert np.array_equal(H.rollouts_go_link16(gs, acts, seeds), ref)
+    if "board_size=11" not in gs:  # three-word bitboards (Go9) up to 9 x 9
+      assert np.array_equal(H.rollouts_go9(gs, acts, seeds), ref)
 
 
 @pytest.mark.parametrize("gs", ["go(board_size=9)", "go(board_size=7,komi=4.5)",
