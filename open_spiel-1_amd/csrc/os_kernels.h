@@ -1895,9 +1895,23 @@ __global__ __launch_bounds__(64) void k_wrollouts(RollArgs a) {
 #ifndef OS_ROLL_OCC
 #define OS_ROLL_OCC 1
 #endif
-template <class G>
+// kZob: go's Zobrist table staged in LDS by each block (every move of every
+// lane reads it) instead of read through the caches.  It pays where few
+// waves share a SIMD and each load's latency is exposed: C5's per-rank share
+// (131072 playouts, two waves per SIMD) 2.31 -> 2.13 ms; at 2^20 (four
+// resident, sixteen per SIMD in all) the per-block fill costs more than it
+// saves, 10.59 -> 10.73 ms (profiles/r06/zob/).  RollLaunch picks it by size.
+constexpr int64_t kRollZobLdsMax = 131072;
+template <class G, bool kZob>
 __global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  constexpr bool kZobLds = kZob && IsLaneGo<G>::value;
+  __shared__ uint64_t zob_lds[kZobLds ? LsCaps<G>::zob : 1];
+  if constexpr (kZobLds) {  // before any lane leaves: the whole block loads it
+    const int nz = 2 * a.cfg.rows * a.cfg.cols;
+    for (int z = threadIdx.x; z < nz; z += blockDim.x) zob_lds[z] = a.zob[z];
+    __syncthreads();
+  }
   if (i >= a.n) return;
   // OS_ROLL_MT (A/B): 0 MtStreamSoA, 1 MtStreamReg (first block from seed
   // cursors alone: no MT traffic below 624 words, more VALU), 2 MtStreamPf.
@@ -1919,6 +1933,7 @@ __global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
   ev.seed(a.seeds[i]);
   extern __shared__ uint32_t roll_lds[];  // RollLdsBytes<G>(cfg) bytes
   typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
+  if constexpr (kZobLds) ctx.zob = zob_lds;
   const typename G::State root = LaneRoot<G>::load(a.root, 0);
   double s0 = 0.0, s1 = 0.0;
   uint32_t moves = 0;
@@ -2407,8 +2422,11 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
     // (profiles/r06/ab_narrow): a wave instruction then serves half as many
     // playouts, and this kernel's VALU is already half busy.
     const int bs = 64;
-    hipLaunchKernelGGL(k_rollouts<G>, dim3(static_cast<unsigned>((n + bs - 1) / bs)),
-                       dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
+    const dim3 grid(static_cast<unsigned>((n + bs - 1) / bs));
+    if (IsLaneGo<G>::value && n <= kRollZobLdsMax)
+      hipLaunchKernelGGL((k_rollouts<G, true>), grid, dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
+    else
+      hipLaunchKernelGGL((k_rollouts<G, false>), grid, dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
   }
   HIP_TRY(hipGetLastError());
   return OS_OK;

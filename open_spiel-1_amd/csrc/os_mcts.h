@@ -74,6 +74,12 @@ OS_HD double puct_unsolved(double w, int32_t n, double cprior, double sqrtN) {
   return q + cprior * sqrtN / static_cast<double>(n + 1);
 }
 
+// Lane-layout UCT selection screened in f32 (mcts_search; 1) or the f64
+// scan alone (0).  A/B knob; both exact.
+#ifndef OS_LANE_SCREEN
+#define OS_LANE_SCREEN 1
+#endif
+
 struct SearchResult {
   int32_t status;
   int32_t sims;     // simulations run (== root explore_count)
@@ -160,6 +166,17 @@ OS_HD int rollout_ret0(typename G::State s, const GameCfg& g, Ctx& ctx, Rng& ev)
   }
   return G::ret0(s, g, ctx);
 }
+
+// Legal types that write LegalActions() into a buffer in one pass (go);
+// OS_LEGAL_FILL=0 keeps one kth() per action (A/B knob, same actions).
+#ifndef OS_LEGAL_FILL
+#define OS_LEGAL_FILL 1
+#endif
+template <class L, class A, class = void>
+struct HasFill : std::false_type {};
+template <class L, class A>
+struct HasFill<L, A, std::void_t<decltype(std::declval<const L&>().fill(std::declval<A&>()))>>
+    : std::true_type {};
 
 template <class R>
 struct RewardOps;
@@ -304,7 +321,10 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
       if (cur_nc == 0) {
         const typename G::Legal l = G::legal(s, g, ctx);
         const int nc = l.count;
-        for (int k = 0; k < nc; ++k) actbuf[k] = static_cast<uint16_t>(l.kth(k));
+        if constexpr (OS_LEGAL_FILL && HasFill<typename G::Legal, ActA>::value)
+          l.fill(actbuf);
+        else
+          for (int k = 0; k < nc; ++k) actbuf[k] = static_cast<uint16_t>(l.kth(k));
         if (Policy == kPolicyCpp) CppShuffle(actbuf, nc, bot);
         else NpShuffle(actbuf, nc, bot);
         if (used + static_cast<uint32_t>(nc) > cap &&
@@ -347,6 +367,68 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         chosen = 0;
         res.scanned += cur_nc;
         Node<R, W> bc = nodes[cur_first];
+        bool screened = false;
+#if defined(__HIP_DEVICE_COMPILE__) && OS_LANE_SCREEN
+        // UCT with integer rewards: the argmax screened in f32 first, as the
+        // wave kernels' uct_argmax_screen (os_wave.h; the same per-child value,
+        // within E = (1 + |c| sqrt(log N)) 2^-20 of the f64 one,
+        // tests/test_uct_screen.py), in one serial pass per lane.  The first
+        // unvisited unsolved child is +inf in f64 and wins the strict '>' scan
+        // outright, so the pass stops there.  Otherwise j, the first child
+        // holding the f32 maximum m1, is the f64 argmax when every child of a
+        // different (n, w, out) scores below m1 - 8E: m2 bounds those children
+        // from above (a child of j's identity scores exactly j's value and
+        // comes later, so j still wins; when the maximum moves to a new
+        // identity the old maximum becomes m2, covering every child seen
+        // before).  Any other case runs the exact f64 scan below.
+        if constexpr (std::is_same<R, int32_t>::value) {
+          if (!sp.puct) {
+            const float lf = static_cast<float>(logN);
+            const float cf = static_cast<float>(sp.uct_c);
+            float m1 = -__builtin_huge_valf(), m2 = -__builtin_huge_valf();
+            int j = -1, jinf = -1;
+            int32_t jn = 0, jw = 0, jo = 0;
+            auto screen = [&](const Node<R, W>& c, int k) {
+              if (c.out == kUnsolved && c.n == 0) {
+                jinf = k;
+                return;
+              }
+              const float r = __builtin_amdgcn_rcpf(static_cast<float>(c.n));
+              float a = static_cast<float>(c.w) * r + cf * __builtin_amdgcn_sqrtf(lf * r);
+              const int32_t o = static_cast<int32_t>(c.out);
+              a = o != kUnsolved ? static_cast<float>(cp == 0 ? o : -o) : a;
+              if (j >= 0 && c.n == jn && c.w == jw && o == jo) return;
+              if (a > m1) {
+                m2 = m1;
+                m1 = a;
+                j = k;
+                jn = c.n;
+                jw = c.w;
+                jo = o;
+              } else {
+                m2 = fmaxf(m2, a);
+              }
+            };
+            int k = 0;
+            for (; k + 4 <= cur_nc && jinf < 0; k += 4) {
+              const Node<R, W> c0 = nodes[cur_first + k], c1 = nodes[cur_first + k + 1];
+              const Node<R, W> c2 = nodes[cur_first + k + 2], c3 = nodes[cur_first + k + 3];
+              screen(c0, k);
+              if (jinf < 0) screen(c1, k + 1);
+              if (jinf < 0) screen(c2, k + 2);
+              if (jinf < 0) screen(c3, k + 3);
+            }
+            for (; k < cur_nc && jinf < 0; ++k) screen(nodes[cur_first + k], k);
+            const float e2 = (1.0f + fabsf(cf) * __builtin_amdgcn_sqrtf(fmaxf(lf, 0.0f))) * 0x1p-17f;
+            const int pick_k = jinf >= 0 ? jinf : (m2 < m1 - e2 ? j : -1);
+            if (pick_k >= 0) {
+              chosen = pick_k;
+              bc = nodes[cur_first + pick_k];
+              screened = true;
+            }
+          }
+        }
+#endif
         auto consider = [&](const Node<R, W>& c, int k) {
           double v;
           if (c.out != kUnsolved) {
@@ -367,16 +449,18 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
         };
         // Four children loaded before any is scored: one memory latency per
         // four nodes on the lane layouts, the same first-maximum order.
-        int k = 0;
-        for (; k + 4 <= cur_nc; k += 4) {
-          const Node<R, W> c0 = nodes[cur_first + k], c1 = nodes[cur_first + k + 1];
-          const Node<R, W> c2 = nodes[cur_first + k + 2], c3 = nodes[cur_first + k + 3];
-          consider(c0, k);
-          consider(c1, k + 1);
-          consider(c2, k + 2);
-          consider(c3, k + 3);
+        if (!screened) {
+          int k = 0;
+          for (; k + 4 <= cur_nc; k += 4) {
+            const Node<R, W> c0 = nodes[cur_first + k], c1 = nodes[cur_first + k + 1];
+            const Node<R, W> c2 = nodes[cur_first + k + 2], c3 = nodes[cur_first + k + 3];
+            consider(c0, k);
+            consider(c1, k + 1);
+            consider(c2, k + 2);
+            consider(c3, k + 3);
+          }
+          for (; k < cur_nc; ++k) consider(nodes[cur_first + k], k);
         }
-        for (; k < cur_nc; ++k) consider(nodes[cur_first + k], k);
         c_action = bc.action;
         c_first = bc.first;
         c_n = bc.n;
