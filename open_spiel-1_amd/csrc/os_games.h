@@ -771,6 +771,11 @@ using GoCtxW = GoCtxT<uint16_t>;
 #ifndef OS_GO_LAZY_ATARI
 #define OS_GO_LAZY_ATARI 2
 #endif
+// Mode 2's captures and own-chain releases as one multi-seed flood each (1)
+// or one flood per chain (0).  A/B knob; the same atari set.
+#ifndef OS_GO_APPLY_MS
+#define OS_GO_APPLY_MS 1
+#endif
 
 template <class B>
 struct GoT {
@@ -929,6 +934,42 @@ struct GoT {
       // merge into a's chain) or next to captured stones leave the set; a's
       // chain enters it iff it has exactly one liberty.  Same set as mode 0.
       const B opp_at = opp & atari;
+#if OS_GO_APPLY_MS
+      // The same updates with the captures and the own chains leaving the set
+      // each as ONE flood from all their seeds (a flood of a union of seeds
+      // is the union of their chains), so the lanes do not diverge over a
+      // per-chain capture branch.  own_at is taken before the updates: they
+      // change only opponent stones' membership.  With one stone captured
+      // (the only case the ko point needs) that stone is the capturing
+      // neighbour, lowest(ch).
+      const B own_at = own0 & atari;
+      B touched = nb & own_at;
+      const B caps = on & opp_at;
+      if (any(caps)) {
+        const B ch = flood(caps, opp_at, g);
+        on = on & ~ch;
+        opp = opp & ~ch;
+        E = E | ch;
+        capd = ch;
+        captured = popc(ch);
+        cap_pt = lowest(ch);
+        atari = atari & ~ch;
+        touched = touched | (nbr4(ch, g) & own_at);
+        B rem = ch;
+        while (any(rem)) {
+          const int x = lowest(rem);
+          rem = rem & ~BB<B>::bit(x);
+          s.hash ^= ctx.zob[2 * x + (1 - c)];
+        }
+      }
+      while (any(on)) {
+        B libs;
+        const B ch = flood_libs2(BB<B>::bit(lowest(on)), opp, E, g, &libs);
+        on = on & ~ch;
+        atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
+      }
+      if (any(touched)) atari = atari & ~flood(touched, own_at, g);
+#else
       while (any(on)) {
         const int q = lowest(on);
         const B qb = BB<B>::bit(q);
@@ -961,6 +1002,7 @@ struct GoT {
         touched = touched & ~ch;
         atari = atari & ~ch;
       }
+#endif
       {
         B libs;
         const B ch = flood_libs2(pb, own, E, g, &libs);
