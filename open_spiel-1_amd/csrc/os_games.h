@@ -499,6 +499,14 @@ struct Filter256 {
 #ifndef OS_GO_NOWALK
 #define OS_GO_NOWALK 0
 #endif
+// Two filter bits per position before the root (1) or one (0).  A lane whose
+// hash hits the filter scans the root's history with dependent loads, and the
+// wave waits for it: with one bit and a 7-position history a lane hits on ~3%
+// of its moves, so at 32 lanes most moves carry some lane's scan; two bits
+// make it ~0.2%.  A/B knob; exact either way (a miss proves absence).
+#ifndef OS_GO_BASE_FILT2
+#define OS_GO_BASE_FILT2 1
+#endif
 // Contexts of wave-uniform code (GoWaveCtx) declare kWaveUniform.
 template <class C, class = void>
 struct WaveUniformCtx : std::false_type {};
@@ -610,11 +618,20 @@ struct GoCtxT {
   // Builds base_filt only: a resumed search keeps its log (os_az.h).
   OS_HD void init_base_filter() {
     base_filt.clear();
-    for (int i = 0; i < n_base; ++i) base_filt.add(fbit(base[i]));
+    for (int i = 0; i < n_base; ++i) {
+      base_filt.add(fbit(base[i]));
+      if (OS_GO_BASE_FILT2) base_filt.add(fbit2(base[i]));
+    }
   }
   OS_HD static int fbit(uint64_t h) { return static_cast<int>(h >> 56); }
+  OS_HD static int fbit2(uint64_t h) { return static_cast<int>((h >> 48) & 255u); }
+  // The pre-filter in front of the scan of the positions before the root:
+  // both of a hash's two bits set (OS_GO_BASE_FILT2), or its one bit.
+  OS_HD bool base_maybe(uint64_t h) const {
+    return base_filt.has(fbit(h)) && (!OS_GO_BASE_FILT2 || base_filt.has(fbit2(h)));
+  }
   OS_HD bool contains(uint64_t h, int stones) const {
-    if (base_filt.has(fbit(h)))
+    if (base_maybe(h))
       for (int i = 0; i < n_base; ++i)
         if (base[i] == h) return true;
 #if OS_GO_NOWALK  // timing A/B only (not exact): no bucket walk
