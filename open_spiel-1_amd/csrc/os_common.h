@@ -219,12 +219,27 @@ OS_HD int select32(uint32_t x, int k) {
   if (k >= c) { base += 1; }
   return base;
 }
+// Branch-free word choice, then one select32: the lanes of a wave pick
+// different words, and a branch per word would run every lane through all
+// three selects.
+#ifndef OS_SELECT96_FLAT
+#define OS_SELECT96_FLAT 1  // A/B knob: 0 = a branch per word
+#endif
 OS_HD int select96(B96 a, int k) {  // k < popc(a)
+  if (!OS_SELECT96_FLAT) {
+    const int c0 = popc32(a.w0);
+    if (k < c0) return select32(a.w0, k);
+    k -= c0;
+    const int c1 = popc32(a.w1);
+    return k < c1 ? 32 + select32(a.w1, k) : 64 + select32(a.w2, k - c1);
+  }
   const int c0 = popc32(a.w0);
-  if (k < c0) return select32(a.w0, k);
-  k -= c0;
-  const int c1 = popc32(a.w1);
-  return k < c1 ? 32 + select32(a.w1, k) : 64 + select32(a.w2, k - c1);
+  const int c01 = c0 + popc32(a.w1);
+  const bool in0 = k < c0, in1 = k < c01;
+  const uint32_t w = in0 ? a.w0 : (in1 ? a.w1 : a.w2);
+  const int base = in0 ? 0 : (in1 ? 32 : 64);
+  const int kk = k - (in0 ? 0 : (in1 ? c0 : c01));
+  return base + select32(w, kk);
 }
 OS_HD B96 lowmask96(int n) {  // 0 <= n <= 96
   return b96(n >= 32 ? ~0u : (n <= 0 ? 0u : (1u << n) - 1u),

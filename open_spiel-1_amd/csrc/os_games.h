@@ -793,6 +793,13 @@ using GoCtxW = GoCtxT<uint16_t>;
 #ifndef OS_GO_APPLY_MS
 #define OS_GO_APPLY_MS 1
 #endif
+// With OS_GO_APPLY_MS: the points with two or more empty neighbours first,
+// as one bitboard expression (1), or every flood_libs2 from its seed (0).
+// Measured slower on g9 (348 -> 356 ms; C5 equal, profiles/r06/tl/): the
+// expression costs every move what the floods it spares cost a few.
+#ifndef OS_GO_TWO_LIB
+#define OS_GO_TWO_LIB 0
+#endif
 
 template <class B>
 struct GoT {
@@ -979,6 +986,22 @@ struct GoT {
           s.hash ^= ctx.zob[2 * x + (1 - c)];
         }
       }
+#if OS_GO_TWO_LIB
+      // Points with two or more empty neighbours, for every point at once
+      // (at least two of nbr4's four shifted copies of E): a chain through
+      // such a point has two liberties, which is all the first step of
+      // flood_libs2 would learn from it.  The opponent neighbours and the new
+      // stone that pass it skip their floods, so the lanes seldom enter the
+      // per-chain loop at all.
+      const int n = g.rows;
+      const B t1 = shl(E, n), t2 = shr(E, n);
+      const B t3 = shl(E, 1) & M::notcol0(g), t4 = shr(E, 1) & M::notcollast(g);
+      const B two = (t1 & t2) | (t3 & t4) | ((t1 | t2) & (t3 | t4));
+      on = on & ~two;
+      const bool own_two = test(two, a);
+#else
+      const bool own_two = false;
+#endif
       while (any(on)) {
         B libs;
         const B ch = flood_libs2(BB<B>::bit(lowest(on)), opp, E, g, &libs);
@@ -986,6 +1009,11 @@ struct GoT {
         atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
       }
       if (any(touched)) atari = atari & ~flood(touched, own_at, g);
+      if (!own_two) {
+        B libs;
+        const B ch = flood_libs2(pb, own, E, g, &libs);
+        atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
+      }
 #else
       while (any(on)) {
         const int q = lowest(on);
@@ -1019,12 +1047,12 @@ struct GoT {
         touched = touched & ~ch;
         atari = atari & ~ch;
       }
-#endif
       {
         B libs;
         const B ch = flood_libs2(pb, own, E, g, &libs);
         atari = atari | BB<B>::sel(popc(libs) == 1, ch, BB<B>::zero());
       }
+#endif
       } else {
       while (any(on)) {
         const int q = lowest(on);
