@@ -183,6 +183,11 @@ OS_HD int ctz32(uint32_t x) {  // x != 0
 #endif
 }
 OS_HD int popc(B96 a) { return popc32(a.w0) + popc32(a.w1) + popc32(a.w2); }
+// Branch-free word choice in lowest / select96 (1) or a branch per word (0).
+// A/B knob.
+#ifndef OS_SELECT96_FLAT
+#define OS_SELECT96_FLAT 1
+#endif
 // Funnel shifts: the compiler maps (hi << s) | (lo >> (32 - s)) to one
 // v_alignbit_b32.
 OS_HD B96 shl(B96 a, int s) {  // 0 < s < 32
@@ -201,8 +206,18 @@ OS_HD bool test(B96 a, int i) {
   const uint32_t w = q == 0 ? a.w0 : (q == 1 ? a.w1 : a.w2);
   return (w >> (i & 31)) & 1u;
 }
+// The word first, then one count (as select96): a ternary over three ctz's
+// is emitted as exec-mask branches.
 OS_HD int lowest(B96 a) {  // a != 0
-  return a.w0 ? ctz32(a.w0) : (a.w1 ? 32 + ctz32(a.w1) : 64 + ctz32(a.w2));
+  if (!OS_SELECT96_FLAT) return a.w0 ? ctz32(a.w0) : (a.w1 ? 32 + ctz32(a.w1) : 64 + ctz32(a.w2));
+  const bool z0 = a.w0 == 0u, z01 = z0 && a.w1 == 0u;
+  const uint32_t w = z0 ? (z01 ? a.w2 : a.w1) : a.w0;
+  const int base = z0 ? (z01 ? 64 : 32) : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return base + __builtin_ctz(w);  // w != 0
+#else
+  return base + ctz32(w);
+#endif
 }
 // Index of the k-th (0-based) set bit of x, ascending; k < popc(x).
 OS_HD int select32(uint32_t x, int k) {
@@ -222,9 +237,6 @@ OS_HD int select32(uint32_t x, int k) {
 // Branch-free word choice, then one select32: the lanes of a wave pick
 // different words, and a branch per word would run every lane through all
 // three selects.
-#ifndef OS_SELECT96_FLAT
-#define OS_SELECT96_FLAT 1  // A/B knob: 0 = a branch per word
-#endif
 OS_HD int select96(B96 a, int k) {  // k < popc(a)
   if (!OS_SELECT96_FLAT) {
     const int c0 = popc32(a.w0);
