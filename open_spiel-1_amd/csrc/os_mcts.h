@@ -74,6 +74,9 @@ OS_HD double puct_unsolved(double w, int32_t n, double cprior, double sqrtN) {
   return q + cprior * sqrtN / static_cast<double>(n + 1);
 }
 
+#ifndef OS_AB_LANE_NOROLL
+#define OS_AB_LANE_NOROLL 0
+#endif
 // Lane-layout UCT selection screened in f32 (mcts_search; 1) or the f64
 // scan alone (0).  A/B knob; both exact.
 #ifndef OS_LANE_SCREEN
@@ -498,7 +501,11 @@ OS_HD SearchResult mcts_search(const GameCfg& g, const SearchParams& sp,
       } else {
         solved = false;
         if (sp.n_rollouts == 1) {
+#if OS_AB_LANE_NOROLL  // timing A/B only (not the reference's results): no playout
+          const int r0 = 0;
+#else
           const int r0 = rollout_ret0<G, Policy>(s, g, ctx, ev);
+#endif
           rv0 = static_cast<R>(r0);
           rv1 = static_cast<R>(-r0);
         } else {
