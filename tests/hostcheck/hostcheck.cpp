@@ -677,6 +677,53 @@ int hc_rollouts_go_link16(const char* game_string, const int64_t* actions, int64
   return 0;
 }
 
+// B96 (three u32 words, os_common.h) against B128 on random boards of up to
+// 96 cells: every operation GoT uses, with shifts 1..31 and both word-choice
+// forms.  Returns the number of mismatching results.
+int64_t hc_b96_selftest(uint64_t seed, int64_t n) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&]() {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    return x;
+  };
+  auto mask96 = [](B128 v) { return b128(v.lo, v.hi & 0xFFFFFFFFull); };
+  int64_t bad = 0;
+  for (int64_t t = 0; t < n; ++t) {
+    // sparse and dense boards
+    const int dens = static_cast<int>(rnd() % 4);
+    B128 a = mask96(b128(rnd(), rnd())), b = mask96(b128(rnd(), rnd()));
+    for (int d = 0; d < dens; ++d) {
+      a = a & mask96(b128(rnd(), rnd()));
+      b = b | mask96(b128(rnd(), rnd()));
+    }
+    const B96 a9 = b96_of(a), b9 = b96_of(b);
+    const int s = 1 + static_cast<int>(rnd() % 31);
+    bad += !(b128_of(a9 | b9) == (a | b));
+    bad += !(b128_of(a9 & b9) == (a & b));
+    bad += !(b128_of(a9 ^ b9) == (a ^ b));
+    bad += !(b128_of(~a9 & b9) == (~a & b));
+    bad += (a9 == b9) != (a == b);
+    bad += any(a9) != any(a);
+    bad += popc(a9) != popc(a);
+    bad += !(b128_of(shl(a9, s)) == mask96(shl(a, s)));
+    bad += !(b128_of(shr(a9, s)) == shr(a, s));
+    const int i = static_cast<int>(rnd() % 96);
+    bad += !(b128_of(bit96(i)) == bit128(i));
+    bad += test(a9, i) != test(a, i);
+    bad += !(b128_of(lowmask96(i)) == lowmask128(i));
+    if (any(a)) {
+      bad += lowest(a9) != lowest(a);
+      const int k = static_cast<int>(rnd() % static_cast<uint64_t>(popc(a)));
+      bad += select96(a9, k) != select128(a, k);
+    }
+    const bool c = (rnd() & 1) != 0;
+    bad += !(b128_of(sel96(c, a9, b9)) == sel128(c, a, b));
+  }
+  return bad;
+}
+
 // k_rollouts<Go9>: the link16 context over three-word bitboards (os_games.h
 // Go9, board_size <= 9), the root narrowed as the kernels narrow it.
 int hc_rollouts_go9(const char* game_string, const int64_t* actions, int64_t n_actions,

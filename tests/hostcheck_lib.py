@@ -29,6 +29,8 @@ def lib():
     L.hc_rollouts_go_logbloom.argtypes = L.hc_rollouts.argtypes
     L.hc_rollouts_go_link16.argtypes = L.hc_rollouts.argtypes
     L.hc_rollouts_go9.argtypes = L.hc_rollouts.argtypes
+    L.hc_b96_selftest.restype = ctypes.c_int64
+    L.hc_b96_selftest.argtypes = [ctypes.c_uint64, ctypes.c_int64]
     L.hc_go_score.restype = ctypes.c_float
     L.hc_go_score.argtypes = [ctypes.c_char_p, vp, ctypes.c_int64]
     L.hc_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, vp]
@@ -266,6 +268,11 @@ def rollouts_go_link16(game_string, history, seeds):
   if rc:
     raise RuntimeError(lib().hc_last_error().decode())
   return out
+
+
+def b96_selftest(seed, n):
+  """Mismatches of B96 against B128 over n random boards (hc_b96_selftest)."""
+  return int(lib().hc_b96_selftest(seed, n))
 
 
 def rollouts_go9(game_string, history, seeds):
