@@ -522,7 +522,7 @@ struct WaveUniformCtx<C, std::void_t<decltype(C::kWaveUniform)>> : std::true_typ
 // L: link word.  uint32_t keeps the stone count for rewind (the searches);
 // a rollout-only context (k_rollouts, never rewound) stores the uint16_t
 // link alone: 2 B less HBM write per logged move.
-template <class H, class L = uint32_t>
+template <class H, class L = uint32_t, int kBW = 16>
 struct GoCtxT {
   const uint64_t* zob;     // [n*n][2] Zobrist values per (cell, colour)
   const uint64_t* base;    // hashes of positions before this search's root
@@ -543,7 +543,10 @@ struct GoCtxT {
   // the bucket walks' dependent HBM reads (k_rollouts / k_lsearch keep it in
   // LDS next to the bucket heads).
   uint32_t* bloom = nullptr;
-  static constexpr int kBloomWords = 16;  // 512 bits, 2 bits per position
+  static constexpr int kBloomWords = kBW;  // kBW * 32 bits, 2 bits per position
+  static_assert(kBW == 16 || kBW == 32, "Bloom filter of 512 or 1024 bits");
+  static constexpr uint32_t kBloomMask = kBW * 32 - 1;
+  static constexpr int kBloomShift = kBW == 32 ? 10 : 9;
   // Optional write-combining of the log (k_lsearch; nullptr: none).  A lane's
   // log entries land in lines no other lane shares, one 12-byte entry per
   // move, so the L2 writes back partly written lines; with wlog / wlink set,
@@ -588,8 +591,8 @@ struct GoCtxT {
     }
   }
 
-  OS_HD static int bbit0(uint64_t h) { return static_cast<int>(h & 511u); }
-  OS_HD static int bbit1(uint64_t h) { return static_cast<int>((h >> 9) & 511u); }
+  OS_HD static int bbit0(uint64_t h) { return static_cast<int>(h & kBloomMask); }
+  OS_HD static int bbit1(uint64_t h) { return static_cast<int>((h >> kBloomShift) & kBloomMask); }
   OS_HD bool bloom_has(uint64_t h) const {
     const int x = bbit0(h), y = bbit1(h);
     return ((bloom[(x >> 5) * head_stride] >> (x & 31)) & 1u) &&

@@ -177,12 +177,22 @@ struct LsCaps<Go> {  // act, heads and bloom per lane
   static constexpr int act = 124, zob = 2 * 121, heads = kGoHeads, log = kGoLogCap,
                        bloom = GoCtx::kBloomWords;
 };
+// k_lsearch<Go9>'s superko-log Bloom filter: 1024 bits per lane (1) or 512
+// (0).  A lane whose position hits the filter in a non-empty bucket walks the
+// bucket with dependent loads while its wave waits; late in a playout (~165
+// entries) 512 bits give ~23% false hits, 1024 ~8%.  The lane search has the
+// LDS for it (32 lanes per block); k_rollouts (64 lanes, four waves per
+// SIMD) keeps 512.  A/B knob; exact either way.
+#ifndef OS_LS_BLOOM1K
+#define OS_LS_BLOOM1K 1
+#endif
+using GoCtxLs = GoCtxT<uint8_t, uint32_t, OS_LS_BLOOM1K ? 32 : 16>;
 template <>
 struct LsCaps<Go9> {  // 9 x 9: 82 actions, stone counts 0 .. 81
   static constexpr int act = kGo9MaxSide * kGo9MaxSide + 1,
                        zob = 2 * kGo9MaxSide * kGo9MaxSide,
                        heads = kGo9MaxSide * kGo9MaxSide + 1, log = kGoLogCap,
-                       bloom = GoCtx::kBloomWords;
+                       bloom = GoCtxLs::kBloomWords;
 };
 template <>
 struct LsCaps<GoBig> {  // actions up to 361: u16 expansion buffers in HBM
@@ -254,7 +264,30 @@ struct LCtx<Go> {
 };
 
 template <>
-struct LCtx<Go9> : LCtx<Go> {};
+struct LCtx<Go9> {  // as LCtx<Go>, with k_lsearch's Bloom width (GoCtxLs)
+  __device__ static GoCtxLs make(const DevArgs& a, int64_t gr, int64_t lr, uint8_t* lds_heads,
+                                 uint32_t* lds_bloom, int lanes) {
+    GoCtxLs c;
+    c.zob = a.zob;
+    c.base = a.root_hashes + gr * a.hash_stride;
+    c.n_base = a.root_nhash[gr];
+    c.log = a.lglog + lr * kGoLogCap;
+    c.link = a.lglink + lr * kGoLogCap;
+    c.head = lds_heads;
+    c.head_stride = lanes;
+#if OS_GO_LOG_BLOOM
+    c.bloom = lds_bloom;
+#else
+    (void)lds_bloom;
+#endif
+    c.stride = 1;
+    c.n_log = 0;
+    c.cap = kGoLogCap;
+    c.n_heads = a.cfg.rows * a.cfg.cols + 1;
+    c.init_filters();
+    return c;
+  }
+};
 
 // Root records of the lane kernels: the host's G::State, except for Go9,
 // whose roots are Go::State records narrowed to three-word bitboards.
