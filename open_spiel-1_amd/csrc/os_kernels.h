@@ -1841,9 +1841,15 @@ struct RollCtx<Go> {
   // lanes (each lane is at its own stone count): they live in LDS, lane-
   // interleaved ([count][64] bytes); the log and links stay batch-SoA in HBM.
   __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds) {
+    return make_bw<16>(a, i, lds);
+  }
+  // The same context with a kBW-word Bloom filter (k_rollouts' small batches).
+  template <int kBW>
+  __device__ static GoCtxT<uint8_t, uint16_t, kBW> make_bw(const RollArgs& a, int64_t i,
+                                                           uint32_t* lds) {
     uint8_t* lds_heads = reinterpret_cast<uint8_t*>(lds);
     uint16_t* glink = reinterpret_cast<uint16_t*>(a.glink);
-    type c;
+    GoCtxT<uint8_t, uint16_t, kBW> c;
     c.zob = a.zob;
     c.base = a.root_hashes;
     c.n_base = a.n_root_hashes;
@@ -1872,6 +1878,33 @@ struct RollCtx<Go> {
 
 template <>
 struct RollCtx<Go9> : RollCtx<Go> {};
+
+// k_rollouts' context: batches of at most kRollZobLdsMax playouts (kSmall;
+// two waves per SIMD, LDS to spare) give go 9 x 9 a 1024-bit superko-log
+// Bloom filter, as the lane search has (GoCtxLs: fewer lanes walking a bucket
+// while their wave waits); larger batches keep 512 bits and four resident
+// waves per SIMD.  OS_ROLL_BLOOM1K=0: 512 bits everywhere (A/B knob).
+#ifndef OS_ROLL_BLOOM1K
+#define OS_ROLL_BLOOM1K 1
+#endif
+template <class G, bool kSmall>
+struct RollCtxOf {
+  using type = typename RollCtx<G>::type;
+  static constexpr int kBloomWords = GoCtx::kBloomWords;
+  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds) {
+    return RollCtx<G>::make(a, i, lds);
+  }
+};
+#if !OS_ROLL_BLOOM
+template <>
+struct RollCtxOf<Go9, true> {
+  static constexpr int kBloomWords = OS_ROLL_BLOOM1K ? 32 : 16;
+  using type = GoCtxT<uint8_t, uint16_t, kBloomWords>;
+  __device__ static type make(const RollArgs& a, int64_t i, uint32_t* lds) {
+    return RollCtx<Go>::make_bw<kBloomWords>(a, i, lds);
+  }
+};
+#endif
 
 template <class G>
 struct WaveRollCtx {
@@ -1965,7 +1998,7 @@ __global__ __launch_bounds__(64, OS_ROLL_OCC) void k_rollouts(RollArgs a) {
 #endif
   ev.seed(a.seeds[i]);
   extern __shared__ uint32_t roll_lds[];  // RollLdsBytes<G>(cfg) bytes
-  typename RollCtx<G>::type ctx = RollCtx<G>::make(a, i, roll_lds);
+  typename RollCtxOf<G, kZob>::type ctx = RollCtxOf<G, kZob>::make(a, i, roll_lds);
   if constexpr (kZobLds) ctx.zob = zob_lds;
   const typename G::State root = LaneRoot<G>::load(a.root, 0);
   double s0 = 0.0, s1 = 0.0;
@@ -2406,14 +2439,15 @@ int AzLaunch(os_engine* e, hipStream_t stream) {
 // per stone count per lane) and the log's Bloom filter; the heads' static
 // bound (11 x 11) would cost occupancy on 9 x 9.
 template <class G>
-size_t RollLdsBytes(const GameCfg& c) {
+size_t RollLdsBytes(const GameCfg& c, int bloom_words = GoCtx::kBloomWords) {
 #if OS_ROLL_BLOOM
   (void)c;
+  (void)bloom_words;
   return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #else
   if constexpr (IsLaneGo<G>::value)
     return 4 * (((c.rows * c.cols + 1) * 64 + 3) / 4 +
-                (OS_GO_LOG_BLOOM ? GoCtx::kBloomWords * 64 : 0));
+                (OS_GO_LOG_BLOOM ? bloom_words * 64 : 0));
   else
     return sizeof(uint32_t) * RollCtx<G>::kLdsWords;
 #endif
@@ -2457,7 +2491,8 @@ int RollLaunch(os_engine* e, hipStream_t stream) {
     const int bs = 64;
     const dim3 grid(static_cast<unsigned>((n + bs - 1) / bs));
     if (IsLaneGo<G>::value && n <= kRollZobLdsMax)
-      hipLaunchKernelGGL((k_rollouts<G, true>), grid, dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
+      hipLaunchKernelGGL((k_rollouts<G, true>), grid, dim3(bs),
+                         RollLdsBytes<G>(a.cfg, RollCtxOf<G, true>::kBloomWords), stream, a);
     else
       hipLaunchKernelGGL((k_rollouts<G, false>), grid, dim3(bs), RollLdsBytes<G>(a.cfg), stream, a);
   }
